@@ -1,0 +1,39 @@
+// Shared device/host helpers for the gtsfm_amd HIP kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gtsfm_hip.h"
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define GTSFM_CHECK_HIP(expr)                          \
+    do {                                               \
+        hipError_t _e = (expr);                        \
+        if (_e != hipSuccess) return GTSFM_ERR_HIP;    \
+    } while (0)
+
+__host__ __device__ static inline size_t gtsfm_align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Lane-wise min/max/median of three unsigned keys (v_min_u32 / v_med3_u32).
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    return umax(umin(a, b), umin(umax(a, b), c));  // lowers to v_med3_u32
+}
+
+// Insert key k into a running (b1 <= b2) top-2 of packed keys: second = med3(b1, b2, k), first = min(b1, k).
+__device__ __forceinline__ void top2_insert(uint32_t& b1, uint32_t& b2, uint32_t k) {
+    b2 = umed3(b1, b2, k);
+    b1 = umin(b1, k);
+}
+
+// Merge two top-2 lists (a1 <= a2, c1 <= c2) into a.
+__device__ __forceinline__ void top2_merge(uint32_t& a1, uint32_t& a2, uint32_t c1, uint32_t c2) {
+    uint32_t n1 = umin(a1, c1);
+    uint32_t n2 = umin(umax(a1, c1), umin(a2, c2));
+    a1 = n1;
+    a2 = n2;
+}

@@ -1,0 +1,558 @@
+// Mutual-nearest-neighbour + ratio-test matcher for batches of image pairs (gfx950).
+//
+// Replaces gtsfm/frontend/matcher/twoway_matcher.py:42-144 (TwoWayMatcher.match): two one-way
+// cv.BFMatcher(NORM_L2).knnMatch(k=2) passes (:102, :136), the ratio test `m1.distance <= r*m2.distance`
+// (:137), the stable sort by distance (:141), the query->train dict (:142) and the mutual filter in
+// 1->2 order (:117-120).
+//
+// Fast path (GTSFM_MATCH_INT_F16): one K1 x K2 distance GEMM per pair on fp16 MFMA
+// (v_mfma_f32_32x32x16_f16). The squared norms are folded into 4 extra K columns, so the accumulator
+// IS the squared L2 distance:   A'_r = [a, |a|^2 mod 2048, |a|^2 div 2048, 1, 2048]
+//                               B'_c = [-2b, 1, 2048, |b|^2 mod 2048, |b|^2 div 2048]
+// Every factor is an integer exactly representable in fp16 and every partial sum is an integer < 2^24,
+// so the fp32 accumulation is exact in any order: d2 = |a|^2 + |b|^2 - 2 a.b exactly.
+// The epilogue packs key = d2 << 12 | index (d2 < 2^20) and keeps a running top-2 per row in
+// registers (v_med3_u32 + v_min_u32 per element) and per column through LDS; the K1 x K2 matrix is
+// never written to HBM. Lexicographic (d2, index) order == OpenCV's strict-'<' scan order, and for
+// d2 < 2^22 ordering by d2 equals ordering by sqrtf(d2), so results are bit-identical to the oracle.
+//
+// Exact path (GTSFM_MATCH_EXACT_F32): float descriptors, per-row sequential fp32 sums (no FMA
+// contraction), top-2 on sqrtf distances — the oracle's arithmetic, for tests and non-SIFT data.
+//
+// Both paths end in match_finalize_kernel: ratio test in double on float32 distances, mutual check,
+// LDS compaction and a bitonic sort on (distance, i1) — the reference's output order.
+#include "common.hpp"
+
+namespace {
+
+// Packed key = (d2 << ib) | index with ib = ceil(log2(kmax)) (>= 11) index bits and 32-ib distance bits.
+// d2 saturates at 2^(32-ib)-1; finalize recomputes any row/column whose top-2 touched the saturated value.
+constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+constexpr int kMaxKmaxPacked = 8192;   // fast path
+constexpr int kMaxKmax = 65535;        // exact path (16-bit indices in the sort key)
+
+inline int index_bits(int kmax) {
+    int b = 11;
+    while ((1 << b) < kmax) ++b;
+    return b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pack float descriptors into the two fp16 MFMA operand forms (norm digits folded into K).
+// ---------------------------------------------------------------------------------------------
+__global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __restrict__ counts, int kmax, int dim,
+                                 int kpad, int da, _Float16* __restrict__ a_form, _Float16* __restrict__ b_form) {
+    const int img = blockIdx.y;
+    const int row = blockIdx.x * blockDim.y + threadIdx.y;  // one 64-lane wave per descriptor row
+    if (row >= kpad) return;
+    const int lane = threadIdx.x;
+    const int n = counts[img];
+    _Float16* ar = a_form + ((size_t)img * kpad + row) * da;
+    _Float16* br = b_form + ((size_t)img * kpad + row) * da;
+    if (row >= n) {  // padding rows: all-zero operands (masked in the epilogue)
+        for (int k = lane; k < da; k += 64) {
+            ar[k] = (_Float16)0.f;
+            br[k] = (_Float16)0.f;
+        }
+        return;
+    }
+    const float* src = desc + ((size_t)img * kmax + row) * dim;
+    float sq = 0.f;
+    for (int k = lane; k < dim; k += 64) {
+        float v = src[k];
+        sq += v * v;  // integer-valued: exact
+        ar[k] = (_Float16)v;
+        br[k] = (_Float16)(-2.f * v);
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
+    const uint32_t nsq = (uint32_t)sq;
+    const float lo = (float)(nsq & 2047u), hi = (float)(nsq >> 11);
+    for (int k = dim + lane; k < da; k += 64) {
+        const int e = k - dim;
+        float av = 0.f, bv = 0.f;
+        if (e == 0) { av = lo; bv = 1.f; }
+        else if (e == 1) { av = hi; bv = 2048.f; }
+        else if (e == 2) { av = 1.f; bv = lo; }
+        else if (e == 3) { av = 2048.f; bv = hi; }
+        ar[k] = (_Float16)av;
+        br[k] = (_Float16)bv;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused distance GEMM + row/column top-2. One workgroup (4 waves) per pair.
+// Each wave owns 64 rows (two 32-row MFMA tiles) of a 256-row pass; B streams through LDS in
+// 32-column chunks (double buffered, 304-B padded rows: conflict-free ds_read_b128).
+// ---------------------------------------------------------------------------------------------
+constexpr int kWaves = 4;
+constexpr int kThreads = kWaves * 64;
+constexpr int kRowsPerPass = kWaves * 64;
+constexpr int kChunk = 32;
+
+template <int NK>  // NK = da / 16 k-steps
+struct MnnCfg {
+    static constexpr int kDa = NK * 16;
+    static constexpr int kRowBytes = kDa * 2;                      // 288 B at dim 128 (B-form row)
+    static constexpr int kBufBytes = kChunk * kRowBytes;           // one B chunk, contiguous in HBM
+    static constexpr int kGlds = kBufBytes / 1024;                 // 1-KiB LDS-DMA wave-instructions
+    static_assert(kBufBytes % 1024 == 0, "chunk must be whole 1-KiB LDS-DMA pieces");
+};
+
+// Async HBM -> LDS copy of one 1-KiB piece by one wave (lane l moves bytes [16l, 16l+16)).
+__device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                     (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
+}
+
+template <int NK>
+__global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* __restrict__ a_form,
+                                                               const _Float16* __restrict__ b_form,
+                                                               const int* __restrict__ counts,
+                                                               const int* __restrict__ pairs, int kpad, int kmax,
+                                                               int ib, uint2* __restrict__ rowres,
+                                                               uint2* __restrict__ colres) {
+    using Cfg = MnnCfg<NK>;
+    const uint32_t dsat = (1u << (32 - ib)) - 1u;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    unsigned char* bbuf = smem;                                             // [2][kChunk][kRowBytes]
+    uint32_t* partial = (uint32_t*)(smem + 2 * Cfg::kBufBytes);             // [2][kWaves][kChunk][2]
+    uint2* colstate = (uint2*)(partial + 2 * kWaves * kChunk * 2);          // [kmax]
+
+    const int p = blockIdx.x;
+    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+    const int n1 = counts[i1], n2 = counts[i2];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int lrow = lane & 31, half = lane >> 5;
+    if (n1 <= 0 || n2 <= 0) return;  // nothing to match; finalize reads zero rows
+
+    const _Float16* A = a_form + (size_t)i1 * kpad * Cfg::kDa;
+    const unsigned char* Bbytes = (const unsigned char*)(b_form + (size_t)i2 * kpad * Cfg::kDa);
+    uint2* rres = rowres + (size_t)p * kmax;
+    uint2* cres = colres + (size_t)p * kmax;
+
+    for (int c = tid; c < n2; c += kThreads) colstate[c] = make_uint2(kNoKey, kNoKey);
+    const int nchunks = (n2 + kChunk - 1) / kChunk;
+
+    // Chunk `ch` of B (32 consecutive B-form rows = one contiguous block) -> LDS buffer `buf`.
+    auto issue_chunk = [&](int ch, int buf) {
+        const unsigned char* src = Bbytes + (size_t)ch * Cfg::kBufBytes + lane * 16;
+        unsigned char* dst = bbuf + buf * Cfg::kBufBytes;
+        for (int q = wave; q < Cfg::kGlds; q += kWaves) glds16(src + q * 1024, dst + q * 1024);
+    };
+    // Merge the 4 waves' column partials of chunk `ch` (buffer pb) into colstate (32 lanes of one wave).
+    auto merge_partials = [&](int ch, int pb) {
+        if (wave == (ch & (kWaves - 1)) && lane < kChunk) {
+            const int col = ch * kChunk + lane;
+            if (col < n2) {
+                uint2 s = colstate[col];
+                uint32_t s1 = s.x, s2 = s.y;
+#pragma unroll
+                for (int w = 0; w < kWaves; ++w) {
+                    const uint32_t* pp = partial + ((pb * kWaves + w) * kChunk + lane) * 2;
+                    top2_merge(s1, s2, pp[0], pp[1]);
+                }
+                colstate[col] = make_uint2(s1, s2);
+            }
+        }
+    };
+
+    for (int rp = 0; rp < n1; rp += kRowsPerPass) {
+        const int r0w = rp + wave * 64;
+        // A fragments for this wave's two row tiles: lane holds A[row = lrow][k = 16s + 8*half .. +8].
+        half8 afrag[2][NK];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const _Float16* arow = A + (size_t)(r0w + 32 * t + lrow) * Cfg::kDa + 8 * half;
+#pragma unroll
+            for (int s = 0; s < NK; ++s) afrag[t][s] = *(const half8*)(arow + 16 * s);
+        }
+        uint32_t rb1[2][16], rb2[2][16];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
+        const bool rows_partial0 = (r0w + 32 > n1);
+        const bool rows_partial1 = (r0w + 64 > n1);
+
+        issue_chunk(0, 0);
+        __syncthreads();  // vmcnt(0) + barrier: chunk 0 landed, colstate initialised
+
+        for (int ch = 0; ch < nchunks; ++ch) {
+            const int buf = ch & 1;
+            if (ch + 1 < nchunks) issue_chunk(ch + 1, buf ^ 1);  // lands during this chunk's MFMAs
+
+            // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows
+            const unsigned char* bb = bbuf + buf * Cfg::kBufBytes + lrow * Cfg::kRowBytes + half * 16;
+            f32x16 acc0 = {}, acc1 = {};
+#pragma unroll
+            for (int s = 0; s < NK; ++s) {
+                const half8 bf = *(const half8*)(bb + 32 * s);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc1, 0, 0, 0);
+            }
+
+            const uint32_t gcol = (uint32_t)(ch * kChunk + lrow);
+            const bool col_ok = (int)gcol < n2;
+            const bool cols_partial = (ch * kChunk + kChunk > n2);
+            uint32_t cb1 = kNoKey, cb2 = kNoKey;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const f32x16& acc = t ? acc1 : acc0;
+                const bool rows_partial = t ? rows_partial1 : rows_partial0;
+                const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 4 * half);
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const uint32_t d2 = umin((uint32_t)acc[g], dsat);
+                    const uint32_t grow = rowbase + (uint32_t)((g & 3) + 8 * (g >> 2));
+                    uint32_t rk = (d2 << ib) | gcol;
+                    uint32_t ck = (d2 << ib) | grow;
+                    if (cols_partial) rk = col_ok ? rk : kNoKey;
+                    if (rows_partial) ck = ((int)grow < n1) ? ck : kNoKey;
+                    top2_insert(rb1[t][g], rb2[t][g], rk);
+                    top2_insert(cb1, cb2, ck);
+                }
+            }
+            // combine the two half-waves (same column, rows +0/+4) and publish the wave's column partial
+            {
+                const uint32_t o1 = __shfl_xor(cb1, 32), o2 = __shfl_xor(cb2, 32);
+                top2_merge(cb1, cb2, o1, o2);
+                partial[((buf * kWaves + wave) * kChunk + lrow) * 2 + half] = half ? cb2 : cb1;
+            }
+            if (ch > 0) merge_partials(ch - 1, buf ^ 1);
+            __syncthreads();  // next chunk landed (vmcnt(0)); partials of this chunk visible
+        }
+        merge_partials(nchunks - 1, (nchunks - 1) & 1);
+
+        // reduce each row's top-2 across the 32 lanes of its half-wave and store it
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                uint32_t b1 = rb1[t][g], b2 = rb2[t][g];
+#pragma unroll
+                for (int m = 1; m < 32; m <<= 1) {
+                    const uint32_t o1 = __shfl_xor(b1, m), o2 = __shfl_xor(b2, m);
+                    top2_merge(b1, b2, o1, o2);
+                }
+                const int grow = r0w + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
+                if (lrow == g && grow < n1) rres[grow] = make_uint2(b1, b2);
+            }
+        }
+        __syncthreads();
+    }
+    for (int c = tid; c < n2; c += kThreads) cres[c] = colstate[c];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Exact fp32 path: one thread per query row, sequential-k sums (FMA contraction disabled for this
+// translation unit), top-2 on sqrtf distance with OpenCV's strict '<' insertion.
+// Result per row: (d1, d2) float distances and j1.
+// ---------------------------------------------------------------------------------------------
+struct ExactTop2 {
+    float d1, d2;
+    int j1, pad;
+};
+
+__global__ void exact_top2_kernel(const float* __restrict__ desc, const int* __restrict__ counts, int kmax, int dim,
+                                  const int* __restrict__ pairs, int swap, ExactTop2* __restrict__ out) {
+    const int p = blockIdx.y;
+    const int iq = pairs[2 * p + (swap ? 1 : 0)], it = pairs[2 * p + (swap ? 0 : 1)];
+    const int nq = counts[iq], nt = counts[it];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    const float* q = desc + ((size_t)iq * kmax + i) * dim;
+    const float* T = desc + (size_t)it * kmax * dim;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int j1 = -1;
+    for (int j = 0; j < nt; ++j) {
+        const float* t = T + (size_t)j * dim;
+        float acc = 0.f;
+        for (int k = 0; k < dim; ++k) {
+            const float df = __fsub_rn(q[k], t[k]);
+            acc = __fadd_rn(acc, __fmul_rn(df, df));
+        }
+        const float d = __fsqrt_rn(acc);
+        if (d < b2) {
+            if (d < b1) {
+                b2 = b1;
+                b1 = d;
+                j1 = j;
+            } else {
+                b2 = d;
+            }
+        }
+    }
+    out[(size_t)p * kmax + i] = ExactTop2{b1, b2, j1, 0};
+}
+
+// ---------------------------------------------------------------------------------------------
+// Finalize: ratio test + mutual check + compaction + bitonic sort by (distance, i1).
+// ---------------------------------------------------------------------------------------------
+constexpr int kFinThreads = 256;
+
+__device__ __forceinline__ bool ratio_ok(float d1, float d2, double ratio) {
+    if (ratio < 0.0) return true;
+    return (double)d1 <= ratio * (double)d2;  // twoway_matcher.py:137 (Python float compare)
+}
+
+// Exact top-2 of one query row against nt train rows, computed by the whole block (rare path: only for
+// rows/columns whose packed keys saturated). Same arithmetic as exact_top2_kernel.
+__device__ void block_exact_top2(const float* __restrict__ q, const float* __restrict__ T, int nt, int dim,
+                                 float* red_d, int* red_j, float& d1, float& d2, int& j1) {
+    const int tid = threadIdx.x;
+    float b1 = __builtin_inff(), b2 = __builtin_inff();
+    int bj = -1;
+    for (int j = tid; j < nt; j += kFinThreads) {  // each thread scans its own j in increasing order
+        const float* t = T + (size_t)j * dim;
+        float acc = 0.f;
+        for (int k = 0; k < dim; ++k) {
+            const float df = __fsub_rn(q[k], t[k]);
+            acc = __fadd_rn(acc, __fmul_rn(df, df));
+        }
+        const float d = __fsqrt_rn(acc);
+        if (d < b2) {
+            if (d < b1) { b2 = b1; b1 = d; bj = j; } else { b2 = d; }
+        }
+    }
+    // lexicographic (distance, index) merge across threads: thread t's second best has index > its best
+    red_d[2 * tid] = b1;
+    red_d[2 * tid + 1] = b2;
+    red_j[tid] = bj;
+    __syncthreads();
+    if (tid == 0) {
+        // best = lexicographic min of (b1, j) over threads; second distance = min(best thread's b2,
+        // every other thread's b1) — its index never matters, only its distance (ratio test)
+        int bt = -1;
+        for (int t = 0; t < kFinThreads; ++t) {
+            const int cj = red_j[t];
+            if (cj < 0) continue;
+            if (bt < 0 || red_d[2 * t] < red_d[2 * bt] || (red_d[2 * t] == red_d[2 * bt] && cj < red_j[bt])) bt = t;
+        }
+        float m1 = __builtin_inff(), m2 = __builtin_inff();
+        int mj = -1;
+        if (bt >= 0) {
+            m1 = red_d[2 * bt];
+            mj = red_j[bt];
+            m2 = red_d[2 * bt + 1];
+            for (int t = 0; t < kFinThreads; ++t)
+                if (t != bt && red_j[t] >= 0) m2 = fminf(m2, red_d[2 * t]);
+        }
+        red_d[0] = m1;
+        red_d[1] = m2;
+        red_j[0] = mj;
+    }
+    __syncthreads();
+    d1 = red_d[0];
+    d2 = red_d[1];
+    j1 = red_j[0];
+    __syncthreads();
+}
+
+template <bool kPacked>
+__global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void* __restrict__ rowres_v,
+                                                                     const void* __restrict__ colres_v,
+                                                                     const float* __restrict__ desc,
+                                                                     const int* __restrict__ counts,
+                                                                     const int* __restrict__ pairs, int kmax,
+                                                                     int dim, int ib, double ratio,
+                                                                     uint32_t* __restrict__ out_idx,
+                                                                     int* __restrict__ out_count) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int* hdr = (int*)smem;                                           // [0] matches, [1] redo rows
+    float* red_d = (float*)(smem + 16);                               // [2*kFinThreads]
+    int* red_j = (int*)(smem + 16 + 8 * kFinThreads);                 // [kFinThreads]
+    int* redo = (int*)(smem + 16 + 12 * kFinThreads);                 // [kmax]
+    unsigned long long* keys =
+        (unsigned long long*)(smem + 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * 4, 16));
+    const int p = blockIdx.x;
+    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+    const int n1 = counts[i1], n2 = counts[i2];
+    const int tid = threadIdx.x;
+    if (tid == 0) { hdr[0] = 0; hdr[1] = 0; }
+    __syncthreads();
+    const uint32_t imask = (1u << ib) - 1u, dsat = (1u << (32 - ib)) - 1u;
+    auto push = [&](int i, int j, float d1r) {
+        const int slot = atomicAdd(&hdr[0], 1);
+        keys[slot] = ((unsigned long long)__float_as_uint(d1r) << 32) | ((unsigned long long)i << 16) | (uint32_t)j;
+    };
+
+    for (int i = tid; i < n1 && n2 > 0; i += kFinThreads) {
+        float d1r, d2r, d1c, d2c;
+        int j, ic;
+        if (kPacked) {
+            const uint2 r = ((const uint2*)rowres_v)[(size_t)p * kmax + i];
+            if (r.x == kNoKey) continue;
+            j = (int)(r.x & imask);
+            const uint2 c = ((const uint2*)colres_v)[(size_t)p * kmax + j];
+            const bool sat = (r.x >> ib) == dsat || (r.y != kNoKey && (r.y >> ib) == dsat) || (c.x >> ib) == dsat ||
+                             (c.y != kNoKey && (c.y >> ib) == dsat);
+            if (sat) {
+                redo[atomicAdd(&hdr[1], 1)] = i;
+                continue;
+            }
+            d1r = __fsqrt_rn((float)(r.x >> ib));
+            d2r = (r.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(r.y >> ib));
+            ic = (int)(c.x & imask);
+            d1c = __fsqrt_rn((float)(c.x >> ib));
+            d2c = (c.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(c.y >> ib));
+        } else {
+            const ExactTop2 r = ((const ExactTop2*)rowres_v)[(size_t)p * kmax + i];
+            if (r.j1 < 0) continue;
+            j = r.j1;
+            d1r = r.d1;
+            d2r = r.d2;
+            const ExactTop2 c = ((const ExactTop2*)colres_v)[(size_t)p * kmax + j];
+            ic = c.j1;
+            d1c = c.d1;
+            d2c = c.d2;
+        }
+        if (ic == i && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
+    }
+    __syncthreads();
+    if (kPacked) {  // rare: saturated keys -> exact block-wide recomputation of that row and its column
+        const int nredo = hdr[1];
+        const float* D1 = desc + (size_t)i1 * kmax * dim;
+        const float* D2 = desc + (size_t)i2 * kmax * dim;
+        for (int r = 0; r < nredo; ++r) {
+            const int i = redo[r];
+            float d1r, d2r, d1c, d2c;
+            int j, ic;
+            block_exact_top2(D1 + (size_t)i * dim, D2, n2, dim, red_d, red_j, d1r, d2r, j);
+            if (j < 0) continue;
+            block_exact_top2(D2 + (size_t)j * dim, D1, n1, dim, red_d, red_j, d1c, d2c, ic);
+            if (tid == 0 && ic == i && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    const int m = hdr[0];
+    int np2 = 1;
+    while (np2 < m) np2 <<= 1;
+    for (int k = m + tid; k < np2; k += kFinThreads) keys[k] = ~0ull;
+    __syncthreads();
+    // bitonic sort (ascending) of np2 keys: (distance bits, i1, i2) == the reference's stable sort order
+    for (int size = 2; size <= np2; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int k = tid; k < np2; k += kFinThreads) {
+                const int o = k ^ stride;
+                if (o > k) {
+                    const unsigned long long a = keys[k], b = keys[o];
+                    const bool up = ((k & size) == 0);
+                    if ((a > b) == up) {
+                        keys[k] = b;
+                        keys[o] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    uint32_t* dst = out_idx + (size_t)p * kmax * 2;
+    for (int k = tid; k < m; k += kFinThreads) {
+        const unsigned long long key = keys[k];
+        dst[2 * k] = (uint32_t)((key >> 16) & 0xFFFFu);
+        dst[2 * k + 1] = (uint32_t)(key & 0xFFFFu);
+    }
+    if (tid == 0) out_count[p] = m;
+}
+
+inline int next_pow2(int x) {
+    int n = 1;
+    while (n < x) n <<= 1;
+    return n;
+}
+
+inline int pack_da(int dim) { return (int)gtsfm_align_up((size_t)dim + 4, 16); }
+inline int pack_kpad(int kmax) { return (int)gtsfm_align_up((size_t)kmax, kRowsPerPass); }
+
+template <int NK>
+int launch_mnn(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
+               int kpad, int kmax, int ib, uint2* rowres, uint2* colres, hipStream_t stream) {
+    using Cfg = MnnCfg<NK>;
+    const size_t lds = 2 * Cfg::kBufBytes + 2 * kWaves * kChunk * 2 * sizeof(uint32_t) + (size_t)kmax * sizeof(uint2);
+    if (lds > 65536)
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)mnn_mfma_kernel<NK>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(mnn_mfma_kernel<NK>, dim3(n_pairs), dim3(kThreads), lds, stream, a_form, b_form, counts, pairs,
+                       kpad, kmax, ib, rowres, colres);
+    return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
+}
+
+template <bool kPacked>
+int launch_finalize(const void* rowres, const void* colres, const float* desc, const int* counts, const int* pairs,
+                    int n_pairs, int kmax, int dim, int ib, double ratio, uint32_t* out_idx, int* out_count,
+                    hipStream_t stream) {
+    const size_t lds = 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * 4, 16) +
+                       (size_t)next_pow2(kmax) * sizeof(unsigned long long);
+    if (lds > 160 * 1024) return GTSFM_ERR_ARG;
+    if (lds > 65536)
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)match_finalize_kernel<kPacked>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(match_finalize_kernel<kPacked>, dim3(n_pairs), dim3(kFinThreads), lds, stream, rowres, colres,
+                       desc, counts, pairs, kmax, dim, ib, ratio, out_idx, out_count);
+    return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, int mode) {
+    if (n_img <= 0 || kmax <= 0 || dim <= 0 || n_pairs < 0) return 0;
+    if (mode == GTSFM_MATCH_INT_F16) {
+        const size_t forms = 2 * gtsfm_align_up((size_t)n_img * pack_kpad(kmax) * pack_da(dim) * sizeof(_Float16), 256);
+        const size_t res = 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(uint2), 256);
+        return forms + res;
+    }
+    return 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
+}
+
+int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim, const int* d_pairs,
+                        int n_pairs, double ratio, int mode, void* d_workspace, size_t workspace_bytes,
+                        uint32_t* d_out_idx, int* d_out_count, void* stream_v) {
+    hipStream_t stream = (hipStream_t)stream_v;
+    if (n_pairs == 0) return GTSFM_OK;
+    if (!d_desc || !d_counts || !d_pairs || !d_out_idx || !d_out_count || n_img <= 0 || kmax <= 0 || dim <= 0 ||
+        n_pairs < 0 || kmax > kMaxKmax)
+        return GTSFM_ERR_ARG;
+    if (workspace_bytes < gtsfm_match_workspace_bytes(n_img, kmax, dim, n_pairs, mode)) return GTSFM_ERR_CAPACITY;
+    unsigned char* ws = (unsigned char*)d_workspace;
+
+    if (mode == GTSFM_MATCH_INT_F16) {
+        const int da = pack_da(dim), kpad = pack_kpad(kmax), nk = da / 16, ib = index_bits(kmax);
+        if (dim > 140 || kmax > kMaxKmaxPacked) return GTSFM_ERR_ARG;
+        const size_t form_bytes = gtsfm_align_up((size_t)n_img * kpad * da * sizeof(_Float16), 256);
+        _Float16* a_form = (_Float16*)ws;
+        _Float16* b_form = (_Float16*)(ws + form_bytes);
+        const size_t res_bytes = gtsfm_align_up((size_t)n_pairs * kmax * sizeof(uint2), 256);
+        uint2* rowres = (uint2*)(ws + 2 * form_bytes);
+        uint2* colres = (uint2*)(ws + 2 * form_bytes + res_bytes);
+        hipLaunchKernelGGL(pack_desc_kernel, dim3(kpad / 4, n_img), dim3(64, 4), 0, stream, d_desc, d_counts, kmax,
+                           dim, kpad, da, a_form, b_form);
+        GTSFM_CHECK_HIP(hipGetLastError());
+        int rc;
+        switch (nk) {
+            case 2: rc = launch_mnn<2>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
+            case 5: rc = launch_mnn<5>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
+            case 9: rc = launch_mnn<9>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
+            default: return GTSFM_ERR_ARG;
+        }
+        if (rc != GTSFM_OK) return rc;
+        return launch_finalize<true>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
+                                     d_out_idx, d_out_count, stream);
+    }
+    if (mode != GTSFM_MATCH_EXACT_F32) return GTSFM_ERR_ARG;
+    const size_t res_bytes = gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
+    ExactTop2* rowres = (ExactTop2*)ws;
+    ExactTop2* colres = (ExactTop2*)(ws + res_bytes);
+    const dim3 grid((kmax + 127) / 128, n_pairs);
+    hipLaunchKernelGGL(exact_top2_kernel, grid, dim3(128), 0, stream, d_desc, d_counts, kmax, dim, d_pairs, 0, rowres);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(exact_top2_kernel, grid, dim3(128), 0, stream, d_desc, d_counts, kmax, dim, d_pairs, 1, colres);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    return launch_finalize<false>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, 0, ratio, d_out_idx,
+                                  d_out_count, stream);
+}
+
+}  // extern "C"

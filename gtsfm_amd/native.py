@@ -1,0 +1,91 @@
+"""Loader for libgtsfm_hip.so, the gfx950 C-ABI library behind every gtsfm_amd plugin.
+
+There is no fallback: if the library is missing or cannot be loaded, importing the product path raises.
+torch is imported first so that the process has exactly one HIP runtime (torch's bundled libamdhip64.so.7 and
+ours share the SONAME, so the loader reuses torch's copy).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional
+
+import torch  # noqa: F401  (must precede the CDLL load: one HIP runtime per process)
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG_DIR, "_lib", "libgtsfm_hip.so")
+CSRC_DIR = os.path.join(_PKG_DIR, "csrc")
+
+_lib: Optional[ctypes.CDLL] = None
+
+c_void_p = ctypes.c_void_p
+c_int = ctypes.c_int
+c_double = ctypes.c_double
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+c_uint64 = ctypes.c_uint64
+
+# Mirrors include/gtsfm_hip.h
+GTSFM_OK = 0
+GTSFM_ERR_ARG = -1
+GTSFM_ERR_HIP = -2
+GTSFM_ERR_CAPACITY = -3
+GTSFM_MATCH_EXACT_F32 = 0
+GTSFM_MATCH_INT_F16 = 1
+
+# (name, restype, argtypes) of every symbol declared in include/gtsfm_hip.h
+SIGNATURES = {
+    "gtsfm_hip_abi_version": (c_int, []),
+    "gtsfm_hip_target": (ctypes.c_char_p, []),
+    "gtsfm_match_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    "gtsfm_match_batched": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_double, c_int, c_void_p, c_size_t, c_void_p,
+         c_void_p, c_void_p],
+    ),
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def build(jobs: int = 8) -> str:
+    """Compiles every HIP source under gtsfm_amd/csrc for gfx950 into gtsfm_amd/_lib/libgtsfm_hip.so."""
+    subprocess.run(["make", "-s", f"-j{jobs}", "-C", CSRC_DIR], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(the gtsfm_amd product path has no CPU fallback)"
+            )
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (restype, argtypes) in SIGNATURES.items():
+            fn = getattr(handle, name, None)
+            if fn is None:
+                raise NativeError(f"{LIB_PATH} does not export {name}")
+            fn.restype = restype
+            fn.argtypes = argtypes
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != GTSFM_OK:
+        raise NativeError(f"{what} failed with status {rc}")
+
+
+def stream_handle(stream: Optional["torch.cuda.Stream"] = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def require_gpu() -> None:
+    if not torch.cuda.is_available():
+        raise NativeError("gtsfm_amd needs an MI355X (gfx950) GPU: torch.cuda.is_available() is False")

@@ -1,0 +1,73 @@
+/*
+ * gtsfm_hip.h — C ABI of the MI355X-native GTSfM two-view front-end (libgtsfm_hip.so, gfx950).
+ *
+ * Every entry point takes plain pointers and sizes. Pointers named d_* are DEVICE pointers (HBM);
+ * `stream` is a hipStream_t passed as void* (NULL = default stream). No entry point allocates,
+ * synchronises or copies to the host: callers own every buffer and size workspaces with the
+ * matching *_workspace_bytes() query, so a call can be captured into a hipGraph.
+ * Return value: GTSFM_OK (0) or a negative GTSFM_ERR_* code. Degenerate DATA (too few matches,
+ * no model) is never an error: it is reported per pair, as the reference reports a failure tuple.
+ *
+ * Reference interfaces replaced (file:line in alphonse-CHEN/gtsfm @ 2025-01-17):
+ *   gtsfm_match_*           <- gtsfm/frontend/matcher/twoway_matcher.py:42-144 TwoWayMatcher.match
+ *                              (cv.BFMatcher(NORM_L2).knnMatch(k=2) x 2 directions + ratio + mutual + sort)
+ *   gtsfm_ransac_*          <- gtsfm/frontend/verifier/opencv_verifier_base.py:45-109 verify +
+ *                              gtsfm/frontend/verifier/ransac.py:52-82 estimate_E +
+ *                              gtsfm/utils/verification.py:52-94 recover_relative_pose_from_essential_matrix +
+ *                              gtsfm/frontend/inlier_support_processor.py:39-95 run_inlier_support
+ *   gtsfm_sift_*            <- gtsfm/frontend/detector_descriptor/sift.py:27-56 detect_and_describe
+ *                              (cv.cvtColor RGB2GRAY + cv.SIFT_create().detectAndCompute + Keypoints.get_top_k)
+ */
+#ifndef GTSFM_HIP_H_
+#define GTSFM_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GTSFM_OK 0
+#define GTSFM_ERR_ARG (-1)      /* invalid argument (shape, null pointer, unsupported mode) */
+#define GTSFM_ERR_HIP (-2)      /* a HIP runtime call failed */
+#define GTSFM_ERR_CAPACITY (-3) /* workspace too small */
+
+/* ----------------------------------------------------------------------------------------------
+ * Library
+ * ---------------------------------------------------------------------------------------------- */
+/* ABI version (major*100 + minor). */
+int gtsfm_hip_abi_version(void);
+/* Name of the offload target the kernels were compiled for (e.g. "gfx950"). */
+const char* gtsfm_hip_target(void);
+
+/* ----------------------------------------------------------------------------------------------
+ * Matcher: mutual nearest neighbour + Lowe ratio test over a batch of image pairs.
+ *
+ * Descriptors of all images live in one padded array d_desc[n_img][kmax][dim] float32 with
+ * d_counts[n_img] valid rows per image. d_pairs[n_pairs][2] holds (i1, i2) image indices.
+ * Output: d_out_idx[n_pairs][kmax][2] uint32 (i1 keypoint, i2 keypoint) and d_out_count[n_pairs];
+ * rows 0..count-1 of each pair are ordered exactly like TwoWayMatcher.match's result
+ * (ascending 1->2 distance, ties by i1 index). ratio < 0 disables the ratio test.
+ *
+ * mode GTSFM_MATCH_EXACT_F32: any float descriptors; distances are sum_k (a_k-b_k)^2 in float32,
+ *      sequential k (bit-exact with the oracle; equals OpenCV for integer data or dim == 1).
+ * mode GTSFM_MATCH_INT_F16:   integer-valued descriptors in [0, 1023] with squared norm < 2^19
+ *      (every SIFT descriptor). One fp16 MFMA distance GEMM per pair with the norms folded into
+ *      extra K columns, fused row/column top-2. Exact integer arithmetic: bit-identical to EXACT_F32.
+ *      kmax <= 8192, dim <= 140. (EXACT_F32: kmax <= 65535.)
+ * ---------------------------------------------------------------------------------------------- */
+#define GTSFM_MATCH_EXACT_F32 0
+#define GTSFM_MATCH_INT_F16 1
+
+size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, int mode);
+
+int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim,
+                        const int* d_pairs, int n_pairs, double ratio, int mode, void* d_workspace,
+                        size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GTSFM_HIP_H_ */

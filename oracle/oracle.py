@@ -1,0 +1,81 @@
+"""ORACLE — test infrastructure only (CPU restatement of the reference hot path).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and only as the
+checker / CPU baseline. The product package (gtsfm_amd) never imports it.
+
+Loads oracle/liboracle.so (built by oracle/Makefile, see __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib: Optional[ctypes.CDLL] = None
+
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_u32p = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+
+
+def build() -> str:
+    """Compiles the oracle restatement (gcc, no reference sources involved)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.oracle_twoway_match.restype = ctypes.c_int
+        _lib.oracle_twoway_match.argtypes = [_f32p, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_double, _u32p]
+        _lib.oracle_oneway_top2.restype = None
+        _lib.oracle_oneway_top2.argtypes = [_f32p, ctypes.c_int, _f32p, ctypes.c_int, ctypes.c_int,
+                                            _f32p, _f32p, _i32p]
+        _register_optional(_lib)
+    return _lib
+
+
+def _register_optional(l: ctypes.CDLL) -> None:
+    """Registers symbols of the restatements that exist in this build (ransac / sift)."""
+    if hasattr(l, "oracle_ransac_E"):
+        l.oracle_ransac_E.restype = ctypes.c_int
+    if hasattr(l, "oracle_sift_detect_describe"):
+        l.oracle_sift_detect_describe.restype = ctypes.c_int
+
+
+def twoway_match(d1: np.ndarray, d2: np.ndarray, ratio: Optional[float]) -> np.ndarray:
+    """Mutual NN + ratio matching; returns (M,2) uint32 ordered like the reference."""
+    d1 = np.ascontiguousarray(d1, dtype=np.float32)
+    d2 = np.ascontiguousarray(d2, dtype=np.float32)
+    if d1.ndim == 1:
+        d1 = d1.reshape(-1, 1)
+    if d2.ndim == 1:
+        d2 = d2.reshape(-1, 1)
+    n1, D = d1.shape
+    n2 = d2.shape[0]
+    out = np.zeros((max(1, min(n1, n2)), 2), dtype=np.uint32)
+    m = lib().oracle_twoway_match(d1, n1, d2, n2, D, -1.0 if ratio is None else float(ratio), out)
+    return out[:m].copy()
+
+
+def oneway_top2(q: np.ndarray, t: np.ndarray):
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    t = np.ascontiguousarray(t, dtype=np.float32)
+    nq, D = q.shape
+    d1 = np.zeros(nq, np.float32)
+    d2 = np.zeros(nq, np.float32)
+    j1 = np.zeros(nq, np.int32)
+    lib().oracle_oneway_top2(q, nq, t, t.shape[0], D, d1, d2, j1)
+    return d1, d2, j1

@@ -1,0 +1,36 @@
+"""The C-ABI library loads on the CPU host and exports every symbol include/gtsfm_hip.h declares."""
+import os
+import re
+
+from tests.conftest import REPO
+
+
+def _declared_functions():
+    text = open(os.path.join(REPO, "include", "gtsfm_hip.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gtsfm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    names = _declared_functions()
+    assert "gtsfm_match_batched" in names and "gtsfm_hip_abi_version" in names
+
+
+def test_library_exports_every_declared_symbol():
+    from gtsfm_amd import native
+
+    lib = native.lib()
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+        assert name in native.SIGNATURES, f"{name} has no ctypes signature in gtsfm_amd/native.py"
+    assert lib.gtsfm_hip_abi_version() >= 100
+    assert lib.gtsfm_hip_target() == b"gfx950"
+
+
+def test_workspace_queries_without_gpu():
+    from gtsfm_amd import native
+
+    lib = native.lib()
+    ws = lib.gtsfm_match_workspace_bytes(100, 2048, 128, 4950, native.GTSFM_MATCH_INT_F16)
+    assert ws > 2 * 4950 * 2048 * 8
+    assert lib.gtsfm_match_workspace_bytes(0, 2048, 128, 10, 1) == 0
