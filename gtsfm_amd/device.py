@@ -54,3 +54,49 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
                                _ptr(cnt), native.stream_handle(stream))
     native.check(rc, "gtsfm_match_batched")
     return idx, cnt
+
+
+class RansacResult:
+    """Per-pair verifier outputs (device tensors): E, R (i2Ri1), t (i2ti1), n_inliers, status, n_hyp, mask."""
+
+    def __init__(self, E, R, t, n_inliers, status, n_hyp, mask):
+        self.E, self.R, self.t = E, R, t
+        self.n_inliers, self.status, self.n_hyp, self.mask = n_inliers, status, n_hyp, mask
+
+
+def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
+                     match_count: torch.Tensor, thr_px: float, prob: float = 0.999999, max_iters: int = 1000,
+                     seed: int = native.RANSAC_DEFAULT_SEED, pair_id_base: int = 0,
+                     stream: Optional[torch.cuda.Stream] = None) -> RansacResult:
+    """Batched 5-point RANSAC + LO + recoverPose for every pair (gtsfm_ransac_E_batched).
+
+    Args:
+        kp_xy: (n_img, kmax, 2) float32 keypoint pixels; intrinsics: (n_img, 3) float64 (f, u0, v0).
+        pairs: (P, 2) int32; match_idx: (P, mcap, 2) int32 (uint32 values); match_count: (P,) int32.
+    """
+    assert kp_xy.is_cuda and kp_xy.dtype == torch.float32 and kp_xy.dim() == 3 and kp_xy.is_contiguous()
+    assert intrinsics.dtype == torch.float64 and intrinsics.is_contiguous()
+    assert match_idx.dtype == torch.int32 and match_idx.is_contiguous() and match_count.dtype == torch.int32
+    n_img, kmax, _ = kp_xy.shape
+    P = pairs.shape[0]
+    mcap = match_idx.shape[1]
+    dev = kp_xy.device
+    L = native.lib()
+    E = torch.zeros((max(P, 1), 3, 3), dtype=torch.float64, device=dev)
+    R = torch.zeros_like(E)
+    t = torch.zeros((max(P, 1), 3), dtype=torch.float64, device=dev)
+    n_inl = torch.zeros((max(P, 1),), dtype=torch.int32, device=dev)
+    status = torch.zeros_like(n_inl)
+    n_hyp = torch.zeros_like(n_inl)
+    mask = torch.zeros((max(P, 1), max(mcap, 1)), dtype=torch.uint8, device=dev)
+    if P > 0:
+        ws = _workspace(L.gtsfm_ransac_workspace_bytes(P, mcap), dev)
+        if stream is not None:
+            ws.record_stream(stream)
+        rc = L.gtsfm_ransac_E_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
+                                      _ptr(match_count), mcap, float(thr_px), float(prob), int(max_iters), int(seed),
+                                      int(pair_id_base), _ptr(ws), ws.numel(), _ptr(E), _ptr(R), _ptr(t),
+                                      _ptr(n_inl), _ptr(status), _ptr(n_hyp), _ptr(mask),
+                                      native.stream_handle(stream))
+        native.check(rc, "gtsfm_ransac_E_batched")
+    return RansacResult(E[:P], R[:P], t[:P], n_inl[:P], status[:P], n_hyp[:P], mask[:P])

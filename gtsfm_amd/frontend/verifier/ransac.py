@@ -1,0 +1,72 @@
+"""RANSAC essential-matrix verifier on the MI355X.
+
+Drop-in for gtsfm/frontend/verifier/ransac.py:50-111 (Ransac) with the verify() flow of
+gtsfm/frontend/verifier/opencv_verifier_base.py:45-109: fewer than 5 (E) / 6 putatives -> failure tuple; putatives
+normalised with K; threshold estimation_threshold_px / max(fx1, fx2); inlier mask; inlier ratio = mean(mask);
+relative pose from the essential matrix and the verified correspondences (utils/verification.py:52-94).
+
+The estimation runs in libgtsfm_hip.so (gtsfm_ransac_E_batched): 5-point RANSAC with deterministic sampling,
+iterative local optimisation and the recoverPose cheirality vote, one wavefront per pair.
+"""
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from gtsfm_amd import device, native
+from gtsfm_amd.common import geometry
+from gtsfm_amd.common.keypoints import Keypoints
+from gtsfm_amd.frontend.verifier.verifier_base import VerifierBase
+
+RANSAC_SUCCESS_PROB = 0.999999
+RANSAC_MAX_ITERS = 1000  # cv2.findEssentialMat default maxIters
+
+
+class Ransac(VerifierBase):
+    """5-point RANSAC verifier (E path) computed by HIP kernels."""
+
+    def __init__(self, use_intrinsics_in_verification: bool, estimation_threshold_px: float,
+                 seed: int = native.RANSAC_DEFAULT_SEED) -> None:
+        super().__init__(use_intrinsics_in_verification, estimation_threshold_px)
+        self._seed = seed
+
+    def verify(
+        self,
+        keypoints_i1: Keypoints,
+        keypoints_i2: Keypoints,
+        match_indices: np.ndarray,
+        camera_intrinsics_i1,
+        camera_intrinsics_i2,
+    ) -> Tuple[Optional[object], Optional[object], np.ndarray, float]:
+        if not self._use_intrinsics_in_verification:
+            raise NotImplementedError(
+                "The fundamental-matrix (8-point, use_intrinsics_in_verification=False) path is not on the MI355X "
+                "verifier yet; use use_intrinsics_in_verification=True")
+        if match_indices.shape[0] < self._min_matches or match_indices.shape[0] < 6:
+            return self._failure_result
+        native.require_gpu()
+        M = match_indices.shape[0]
+        dev = torch.device("cuda")
+        c1 = keypoints_i1.coordinates.astype(np.float32)
+        c2 = keypoints_i2.coordinates.astype(np.float32)
+        kmax = max(len(c1), len(c2))
+        kp = np.zeros((2, kmax, 2), np.float32)
+        kp[0, : len(c1)] = c1
+        kp[1, : len(c2)] = c2
+        intr = np.stack([geometry.calibration_params(camera_intrinsics_i1),
+                         geometry.calibration_params(camera_intrinsics_i2)])
+        mi = np.ascontiguousarray(match_indices, dtype=np.int64).astype(np.int32).reshape(1, M, 2)
+        res = device.ransac_essential(
+            torch.from_numpy(kp).to(dev), torch.from_numpy(intr).to(dev),
+            torch.tensor([[0, 1]], dtype=torch.int32, device=dev), torch.from_numpy(mi).to(dev),
+            torch.tensor([M], dtype=torch.int32, device=dev), self._estimation_threshold_px,
+            RANSAC_SUCCESS_PROB, RANSAC_MAX_ITERS, self._seed)
+        status = int(res.status[0].item())
+        if status != native.RANSAC_STATUS_OK:
+            return self._failure_result
+        mask = res.mask[0, :M].cpu().numpy().astype(bool)
+        v_corr_idxs = match_indices[np.flatnonzero(mask)]
+        inlier_ratio = float(np.mean(mask))
+        R = res.R[0].cpu().numpy()
+        t = res.t[0].cpu().numpy()
+        return geometry.Rot3(R), geometry.Unit3(t), v_corr_idxs, inlier_ratio

@@ -33,6 +33,10 @@ GTSFM_ERR_HIP = -2
 GTSFM_ERR_CAPACITY = -3
 GTSFM_MATCH_EXACT_F32 = 0
 GTSFM_MATCH_INT_F16 = 1
+RANSAC_STATUS_OK = 0
+RANSAC_STATUS_TOO_FEW = 1
+RANSAC_STATUS_NO_MODEL = 2
+RANSAC_DEFAULT_SEED = 0x5EED5EED
 
 # (name, restype, argtypes) of every symbol declared in include/gtsfm_hip.h
 SIGNATURES = {
@@ -43,6 +47,13 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_double, c_int, c_void_p, c_size_t, c_void_p,
          c_void_p, c_void_p],
+    ),
+    "gtsfm_ransac_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "gtsfm_ransac_E_batched": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_int,
+         c_uint64, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p],
     ),
 }
 

@@ -66,6 +66,27 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
                         const int* d_pairs, int n_pairs, double ratio, int mode, void* d_workspace,
                         size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count, void* stream);
 
+/* ----------------------------------------------------------------------------------------------
+ * Verifier: essential-matrix RANSAC over a batch of image pairs (use_intrinsics_in_verification=True path).
+ *
+ * Keypoints of all images: d_kp_xy[n_img][kmax][2] float32 pixels; d_intrinsics[n_img][3] = (f, u0, v0)
+ * (Cal3Bundler with k1 = k2 = 0). Putatives per pair: d_match_idx[n_pairs][mcap][2] uint32 keypoint indices
+ * and d_match_count[n_pairs] (exactly the matcher's output). Threshold thr_px / max(f1, f2) in normalized
+ * coordinates on the squared Sampson distance, success probability `prob`, at most `max_iters` hypotheses
+ * (checked per batch of 64); `seed` and pair_id_base + p key the deterministic sampling of pair p.
+ * Outputs per pair: E, R (i2Ri1) row-major 3x3, unit t (i2ti1), inlier count, status (0 ok, 1 fewer than
+ * 6 putatives, 2 no model), number of hypotheses evaluated (d_n_hyp may be NULL) and the inlier mask
+ * d_inlier_mask[n_pairs][mcap] over the putatives in matcher order.
+ * ---------------------------------------------------------------------------------------------- */
+size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap);
+
+int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax,
+                           const int* d_pairs, int n_pairs, const uint32_t* d_match_idx,
+                           const int* d_match_count, int mcap, double thr_px, double prob, int max_iters,
+                           uint64_t seed, int pair_id_base, void* d_workspace, size_t workspace_bytes,
+                           double* d_E, double* d_R, double* d_t, int* d_n_inliers, int* d_status,
+                           int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,15 @@ def _register_optional(l: ctypes.CDLL) -> None:
     """Registers symbols of the restatements that exist in this build (ransac / sift)."""
     if hasattr(l, "oracle_ransac_E"):
         l.oracle_ransac_E.restype = ctypes.c_int
+        l.oracle_ransac_E.argtypes = [_f64p, _f64p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                      ctypes.c_uint64, ctypes.c_int, _f64p, _u8p, _f64p, _f64p,
+                                      ctypes.POINTER(ctypes.c_int)]
+        l.oracle_five_point.restype = ctypes.c_int
+        l.oracle_five_point.argtypes = [_f64p, _f64p, _f64p]
+        l.oracle_sample5.restype = ctypes.c_int
+        l.oracle_sample5.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p]
+        l.oracle_recover_pose.restype = ctypes.c_int
+        l.oracle_recover_pose.argtypes = [_f64p, _f64p, _f64p, ctypes.c_void_p, ctypes.c_int, _f64p, _f64p]
     if hasattr(l, "oracle_sift_detect_describe"):
         l.oracle_sift_detect_describe.restype = ctypes.c_int
 
@@ -79,3 +88,47 @@ def oneway_top2(q: np.ndarray, t: np.ndarray):
     j1 = np.zeros(nq, np.int32)
     lib().oracle_oneway_top2(q, nq, t, t.shape[0], D, d1, d2, j1)
     return d1, d2, j1
+
+
+RANSAC_SEED = 0x5EED5EED
+
+
+def five_point(x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
+    """All essential matrices (k,3,3) from 5 normalized correspondences (Nister)."""
+    Es = np.zeros(90, np.float64)
+    n = lib().oracle_five_point(np.ascontiguousarray(x1, np.float64).ravel(),
+                                np.ascontiguousarray(x2, np.float64).ravel(), Es)
+    return Es[: 9 * n].reshape(n, 3, 3)
+
+
+def sample5(pair: int, h: int, M: int, seed: int = RANSAC_SEED) -> Optional[np.ndarray]:
+    idx = np.zeros(5, np.int32)
+    return idx if lib().oracle_sample5(seed, pair, h, M, idx) else None
+
+
+def ransac_E(x1n: np.ndarray, x2n: np.ndarray, thr: float, prob: float = 0.999999, max_iters: int = 1000,
+             seed: int = RANSAC_SEED, pair_id: int = 0):
+    """Returns (E (3,3), inlier mask (M,) uint8, R (3,3), t (3,), n_inliers, n_hypotheses) or None."""
+    x1n = np.ascontiguousarray(x1n, np.float64)
+    x2n = np.ascontiguousarray(x2n, np.float64)
+    M = x1n.shape[0]
+    E = np.zeros(9)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    mask = np.zeros(max(M, 1), np.uint8)
+    nh = ctypes.c_int(0)
+    n = lib().oracle_ransac_E(x1n.ravel(), x2n.ravel(), M, thr, prob, max_iters, seed, pair_id, E, mask, R, t,
+                              ctypes.byref(nh))
+    if n < 0:
+        return None
+    return E.reshape(3, 3), mask[:M].copy(), R.reshape(3, 3), t, n, nh.value
+
+
+def recover_pose(E: np.ndarray, x1n: np.ndarray, x2n: np.ndarray):
+    R = np.zeros(9)
+    t = np.zeros(3)
+    x1n = np.ascontiguousarray(x1n, np.float64)
+    x2n = np.ascontiguousarray(x2n, np.float64)
+    good = lib().oracle_recover_pose(np.ascontiguousarray(E, np.float64).ravel(), x1n.ravel(), x2n.ravel(), None,
+                                     x1n.shape[0], R, t)
+    return R.reshape(3, 3), t, good

@@ -52,6 +52,57 @@ def lund_door_descriptors():
     print("lund matches: ratio", len(m_full_ratio), "no ratio", len(m_full_noratio), "sub", len(m_sub))
 
 
+def argoverse_known_answer():
+    """tests/frontend/verifier/test_verifier_argoverse.py:41-104: 20 hand-labelled correspondences + intrinsics and
+    the expected relative pose. The .pkl is decoded by walking its opcodes with pickletools.genops (nothing in the
+    file is executed or imported): it is a dict of four lists of numpy float64 scalars, each carried as 8 raw
+    little-endian bytes."""
+    import pickletools
+    import struct
+
+    path = os.path.join(REF, "tests/data/argoverse/labeled_correspondences/"
+                             "argoverse_315975640448534784__315975643412234000.pkl")
+    data = open(path, "rb").read()
+    vals, cur = {}, None
+    for op, arg, _ in pickletools.genops(data):
+        if op.name == "SHORT_BINUNICODE" and arg in ("x1", "y1", "x2", "y2"):
+            cur = arg
+            vals[cur] = []
+        elif op.name == "SHORT_BINBYTES" and len(arg) == 8 and cur is not None:
+            vals[cur].append(struct.unpack("<d", arg)[0])
+    assert all(len(vals[k]) == 20 for k in ("x1", "y1", "x2", "y2"))
+    out = dict(vals)
+    out.update({
+        "fx": 1392.1069298937407, "px": 980.1759848618066, "py": 604.3534182680304,
+        "estimation_threshold_px": 0.5,
+        "expected_euler_zyx_deg_i1Ri2": [-0.37, 32.47, -0.42], "euler_tol_deg": 1.0,
+        "expected_i1ti2": [0.21, -0.0024, 0.976], "translation_tol": 0.01,
+        "source": "tests/frontend/verifier/test_verifier_argoverse.py + tests/data/argoverse/labeled_correspondences",
+    })
+    with open(os.path.join(HERE, "argoverse_known_answer.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+def sampson_known_answers():
+    """tests/utils/test_verification_utils.py:49-111 (Sampson / SED closed-form and real-world values)."""
+    F_real = [[7.41572822e-09, 4.26005557e-07, -2.61114657e-04], [-4.92270651e-07, 4.29568438e-09, 6.95083578e-04],
+              [2.89444929e-04, -1.49345006e-05, -4.01395060e-01]]
+    out = {
+        "cases": [
+            {"F": [[0, 1, 1], [1, 0, 0], [1, 0, 0]], "x1": [[1.0, 3.5], [-2.0, 2.0]], "x2": [[2.0, -1.0], [1.0, 0.0]],
+             "sampson": [81 / (21.25 + 4.0), 1 / (13.0 + 2.0)]},
+            {"F": F_real, "x1": [[1553, 622], [1553, 622]], "x2": [[357, 662], [818, 517]],
+             "sampson": [6.744895e-01, 2.397196e03]},
+        ],
+        "rtol": 1e-3,
+        "source": "tests/utils/test_verification_utils.py:70-111",
+    }
+    with open(os.path.join(HERE, "sampson_known_answers.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     twoway_known_answers()
     lund_door_descriptors()
+    argoverse_known_answer()
+    sampson_known_answers()
