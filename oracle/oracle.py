@@ -62,6 +62,13 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_recover_pose.argtypes = [_f64p, _f64p, _f64p, ctypes.c_void_p, ctypes.c_int, _f64p, _f64p]
     if hasattr(l, "oracle_sift_detect_describe"):
         l.oracle_sift_detect_describe.restype = ctypes.c_int
+        l.oracle_sift_detect_describe.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
+                                                  ctypes.POINTER(ctypes.c_int)]
+        l.oracle_rgb_to_gray.restype = None
+        l.oracle_rgb_to_gray.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, _u8p]
+        l.oracle_sift_pyramid_level.restype = ctypes.c_int
+        l.oracle_sift_pyramid_level.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,
+                                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
 
 
 def twoway_match(d1: np.ndarray, d2: np.ndarray, ratio: Optional[float]) -> np.ndarray:
@@ -132,3 +139,31 @@ def recover_pose(E: np.ndarray, x1n: np.ndarray, x2n: np.ndarray):
     good = lib().oracle_recover_pose(np.ascontiguousarray(E, np.float64).ravel(), x1n.ravel(), x2n.ravel(), None,
                                      x1n.shape[0], R, t)
     return R.reshape(3, 3), t, good
+
+
+def rgb_to_gray(rgb: np.ndarray) -> np.ndarray:
+    rgb = np.ascontiguousarray(rgb, np.uint8)
+    H, W, _ = rgb.shape
+    g = np.zeros((H, W), np.uint8)
+    lib().oracle_rgb_to_gray(rgb.ravel(), H, W, g.ravel())
+    return g
+
+
+def sift(gray: np.ndarray, max_kpts: int = 5000, with_desc: bool = True):
+    """SIFT restatement on a u8 gray image: (kp (N,5) [x, y, size, angle, response], desc (N,128), n_detected)."""
+    gray = np.ascontiguousarray(gray, np.uint8)
+    H, W = gray.shape
+    kp = np.zeros((max_kpts, 5), np.float32)
+    desc = np.zeros((max_kpts, 128), np.float32)
+    nd = ctypes.c_int(0)
+    n = lib().oracle_sift_detect_describe(gray.ravel(), H, W, max_kpts, kp.ravel(), desc.ravel(), ctypes.byref(nd))
+    return kp[:n].copy(), desc[:n].copy(), nd.value
+
+
+def sift_level(gray: np.ndarray, o: int, i: int) -> np.ndarray:
+    gray = np.ascontiguousarray(gray, np.uint8)
+    H, W = gray.shape
+    out = np.zeros((2 * H) * (2 * W), np.float32)
+    Ho, Wo = ctypes.c_int(0), ctypes.c_int(0)
+    lib().oracle_sift_pyramid_level(gray.ravel(), H, W, o, i, out, ctypes.byref(Ho), ctypes.byref(Wo))
+    return out[: Ho.value * Wo.value].reshape(Ho.value, Wo.value).copy()

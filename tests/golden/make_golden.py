@@ -101,8 +101,33 @@ def sampson_known_answers():
         json.dump(out, f, indent=1)
 
 
+def lund_door_sift_fixture():
+    """DSC_0001.JPG of set1_lund_door as u8 gray (cv.cvtColor RGB2GRAY fixed point, applied by the oracle) and the
+    reference's OpenCV SIFT fixture for it (tests/data/set1_lund_door/features/keypoints_0.pkl: coordinates, scales,
+    responses of 5000 keypoints; descriptors_0.npy). The .pkl is decoded by walking its opcodes (pickletools.genops):
+    the three arrays are the three raw BINBYTES blobs (little-endian float64); nothing in the file is executed."""
+    import pickletools
+
+    from PIL import Image
+
+    from oracle import oracle
+
+    data = open(os.path.join(REF, "tests/data/set1_lund_door/features/keypoints_0.pkl"), "rb").read()
+    blobs = [arg for op, arg, _ in pickletools.genops(data) if op.name in ("BINBYTES", "BINBYTES8")]
+    xy = np.frombuffer(blobs[0], "<f8").reshape(-1, 2)
+    scales = np.frombuffer(blobs[1], "<f8")
+    responses = np.frombuffer(blobs[2], "<f8")
+    assert xy.shape == (5000, 2) and scales.shape == (5000,) and responses.shape == (5000,)
+    rgb = np.asarray(Image.open(os.path.join(REF, "tests/data/set1_lund_door/images/DSC_0001.JPG")).convert("RGB"))
+    gray = oracle.rgb_to_gray(rgb)
+    Image.fromarray(gray).save(os.path.join(HERE, "lund_door_DSC_0001_gray.png"), optimize=True)
+    np.savez_compressed(os.path.join(HERE, "lund_door_sift_fixture_0.npz"), xy=xy, scales=scales,
+                        responses=responses)
+
+
 if __name__ == "__main__":
     twoway_known_answers()
     lund_door_descriptors()
     argoverse_known_answer()
     sampson_known_answers()
+    lund_door_sift_fixture()
