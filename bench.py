@@ -1,0 +1,252 @@
+#!/usr/bin/env python
+"""bench.py — verified image-pairs/sec of the all-pairs two-view front-end on MI355X (BASELINE.json `metric`).
+
+One step = the whole front-end over one synthetic scene already resident in HBM:
+    SIFT (2048 kpts/img) on this rank's images -> [N>1: one all-gather of keypoints+descriptors over RCCL]
+    -> mutual-NN + ratio matching of this rank's pairs (fp16 MFMA distance GEMM) -> 5-point RANSAC + LO +
+    recoverPose of the same pairs -> inlier-support filter (>= 15 inliers, ratio >= 0.1), all on device.
+value = all pairs pushed through match + verify (every rank) / max-over-ranks step time.
+
+Workload (configs[1] of BASELINE.json): 100 rendered 1920x1080 images, all 4950 pairs, at N=1. For N GPUs the scene
+grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work constant: "scaling": "weak"); pairs are
+dealt round-robin, images round-robin for extraction.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--images n] [--kpts 2048] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from gtsfm_amd import device as hip  # noqa: E402
+from gtsfm_amd import native, synthetic  # noqa: E402
+
+MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+RATIO = 0.8
+THRESH_PX = 4.0
+MIN_INLIERS = 15
+MIN_INLIER_RATIO = 0.1
+
+
+def images_for(n_gpus: int, base: int = 100) -> int:
+    target = base * (base - 1) // 2 * n_gpus
+    n = base
+    while n * (n - 1) // 2 < target:
+        n += 1
+    return n
+
+
+class FrontEnd:
+    """Device-resident all-pairs front-end for one rank."""
+
+    def __init__(self, scene_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, kpts: int, rank: int,
+                 world: int):
+        self.rank, self.world, self.kpts, self.n_img = rank, world, kpts, n_img
+        self.dev = scene_images.device
+        self.n_per = int(math.ceil(n_img / world))
+        self.local_images = scene_images  # (n_local, H, W, 3): images rank, rank + world, ...
+        # global slot of original image i: (i % world) * n_per + i // world  (rank-major after the all-gather)
+        slot = np.array([(i % world) * self.n_per + i // world for i in range(n_img)], dtype=np.int64)
+        pairs = synthetic.all_pairs(n_img)
+        self.total_pairs = len(pairs)
+        mine = pairs[rank::world]
+        self.my_pairs_orig = mine
+        self.pairs = torch.from_numpy(slot[mine].astype(np.int32)).to(self.dev)
+        intr = np.zeros((world * self.n_per, 3))
+        intr[slot] = intrinsics
+        self.intr = torch.from_numpy(intr).to(self.dev)
+        self.sift_ws = None
+
+    def step(self, events=None):
+        ev = events or {}
+        if "t0" in ev:
+            ev["t0"].record()
+        feats = hip.sift_extract(self.local_images, self.kpts)
+        if "t1" in ev:
+            ev["t1"].record()
+        n_local = self.local_images.shape[0]
+        if self.world > 1:
+            pad = self.n_per - n_local
+            xy, desc, cnt = feats.xy, feats.desc, feats.count
+            if pad:
+                xy = torch.cat([xy, xy.new_zeros((pad,) + xy.shape[1:])])
+                desc = torch.cat([desc, desc.new_zeros((pad,) + desc.shape[1:])])
+                cnt = torch.cat([cnt, cnt.new_zeros((pad,))])
+            xy_all = torch.empty((self.world * self.n_per,) + xy.shape[1:], dtype=xy.dtype, device=self.dev)
+            desc_all = torch.empty((self.world * self.n_per,) + desc.shape[1:], dtype=desc.dtype, device=self.dev)
+            cnt_all = torch.empty((self.world * self.n_per,), dtype=cnt.dtype, device=self.dev)
+            torch.distributed.all_gather_into_tensor(desc_all, desc.contiguous())
+            torch.distributed.all_gather_into_tensor(xy_all, xy.contiguous())
+            torch.distributed.all_gather_into_tensor(cnt_all, cnt.contiguous())
+        else:
+            xy_all, desc_all, cnt_all = feats.xy, feats.desc, feats.count
+        if "t2" in ev:
+            ev["t2"].record()
+        idx, mcnt = hip.match_pairs(desc_all, cnt_all, self.pairs, RATIO, native.GTSFM_MATCH_INT_F16)
+        if "t3" in ev:
+            ev["t3"].record()
+        res = hip.ransac_essential(xy_all, self.intr, self.pairs, idx, mcnt, THRESH_PX)
+        if "t4" in ev:
+            ev["t4"].record()
+        # inlier-support processor (frontend/inlier_support_processor.py:73-87), on device
+        m = mcnt.clamp(min=1).to(torch.float64)
+        ratio = res.n_inliers.to(torch.float64) / m
+        ok = (res.status == native.RANSAC_STATUS_OK) & (ratio >= MIN_INLIER_RATIO) & (res.n_inliers >= MIN_INLIERS)
+        n_ok = ok.sum()
+        return n_ok, (feats, idx, mcnt, res)
+
+
+def cpu_baseline(scene, kpts: int) -> dict:
+    """Oracle restatement timed on host cores (1 thread) on a bounded sample, scaled to the full workload."""
+    from oracle import oracle
+
+    imgs = scene.images[:2].cpu().numpy()
+    t0 = time.time()
+    feats = []
+    for im in imgs:
+        g = oracle.rgb_to_gray(im)
+        feats.append(oracle.sift(g, kpts))
+    t_sift = (time.time() - t0) / len(imgs)
+    K = scene.K
+    t0 = time.time()
+    n_pairs = 2
+    for _ in range(n_pairs):
+        m = oracle.twoway_match(feats[0][1], feats[1][1], RATIO)
+        if len(m) >= 6:
+            x1 = ((feats[0][0][m[:, 0], :2] - K[:2, 2]) / K[0, 0]).astype(np.float64)
+            x2 = ((feats[1][0][m[:, 1], :2] - K[:2, 2]) / K[0, 0]).astype(np.float64)
+            oracle.ransac_E(x1, x2, THRESH_PX / K[0, 0])
+    t_pair = (time.time() - t0) / n_pairs
+    n_img = scene.images.shape[0]
+    P = n_img * (n_img - 1) // 2
+    total = n_img * t_sift + P * t_pair
+    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": 1, "kind": "port",
+            "sample": f"oracle (oracle/*.c, 1 thread): SIFT of 2 of the {n_img} images ({t_sift:.2f} s/img) + match+verify "
+                      f"of {n_pairs} pairs ({t_pair:.2f} s/pair), scaled to {n_img} images / {P} pairs"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--images", type=int, default=0)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--kpts", type=int, default=2048)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    native.lib()
+    n_img = args.images or images_for(world)
+
+    # every rank renders the same seeded scene but keeps only its own images resident
+    scene = synthetic.render_scene(n_img, args.height, args.width, device=str(dev))
+    local = scene.images[rank::world].contiguous()
+    fe = FrontEnd(local, scene.intrinsics, n_img, args.kpts, rank, world)
+    if rank != 0 or world > 1 or args.no_cpu_baseline:
+        keep_for_cpu = None
+    else:
+        keep_for_cpu = scene
+    del scene
+    torch.cuda.empty_cache()
+
+    for _ in range(args.warmup):
+        fe.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n_ok = None
+    for _ in range(args.steps):
+        n_ok, _ = fe.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    ok = n_ok.to(torch.float64).reshape(1)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.SUM)
+    elapsed = float(el.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = fe.total_pairs / (elapsed / args.steps)
+
+    # stage split + roofline of the dominant kernels (HIP events on the stream the kernels run on)
+    names = ["t0", "t1", "t2", "t3", "t4"]
+    stage_ms = {"extract": [], "allgather": [], "match": [], "verify": []}
+    for _ in range(2):
+        evs = {k: torch.cuda.Event(enable_timing=True) for k in names}
+        _, (feats, idx, mcnt, res) = fe.step(evs)
+        torch.cuda.synchronize()
+        stage_ms["extract"].append(evs["t0"].elapsed_time(evs["t1"]))
+        stage_ms["allgather"].append(evs["t1"].elapsed_time(evs["t2"]))
+        stage_ms["match"].append(evs["t2"].elapsed_time(evs["t3"]))
+        stage_ms["verify"].append(evs["t3"].elapsed_time(evs["t4"]))
+    stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    counts = feats.count
+    if world > 1:
+        counts_all = torch.empty((world * fe.n_per,), dtype=counts.dtype, device=dev)
+        cnt_local = torch.cat([counts, counts.new_zeros((fe.n_per - counts.shape[0],))])
+        torch.distributed.all_gather_into_tensor(counts_all, cnt_local)
+    else:
+        counts_all = counts
+    c = counts_all.to(torch.float64)
+    pairs = fe.pairs.long()
+    match_flops = float((2.0 * c[pairs[:, 0]] * c[pairs[:, 1]] * 128).sum().item())
+    match_tflops = match_flops / (stage["match"] * 1e-3) / 1e12
+    roof = {"bound": "mfma", "achieved": round(match_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(match_tflops / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": "mnn_mfma_kernel (+pack, finalize) per batched match launch",
+            "work": "2*K1*K2*128 flop per pair, summed over the launch's pairs"}
+
+    out = {
+        "metric": "verified image-pairs/sec (all-pairs front-end), N images @ 2048 kpts/img",
+        "value": round(value, 2),
+        "unit": "image-pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8 image / fp32 pyramid / fp16-MFMA exact-int distances / fp64 RANSAC solver",
+        "data": "synthetic (rendered textured room, seeds 0/1/2)",
+        "config": {"workload": f"C2: {n_img} synthetic {args.width}x{args.height} images, all "
+                               f"{fe.total_pairs} pairs, SIFT {args.kpts} kpts/img, ratio {RATIO}, "
+                               f"5-pt RANSAC {THRESH_PX}px", "images": n_img, "pairs": fe.total_pairs,
+                   "kpts": args.kpts, "parallelism": f"pairs round-robin x{world}"},
+        "pairs_passing_isp": int(ok.item()),
+        "stage_ms": {k: round(v, 3) for k, v in stage.items()},
+        "roofline": roof,
+    }
+    if keep_for_cpu is not None:
+        out["cpu_baseline"] = cpu_baseline(keep_for_cpu, args.kpts)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

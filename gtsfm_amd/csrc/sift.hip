@@ -1,0 +1,843 @@
+// SIFT detector-descriptor for batches of same-sized images (gfx950).
+//
+// Replaces gtsfm/frontend/detector_descriptor/sift.py:27-56: rgb_to_gray_cv (utils/images.py:14-41),
+// cv.SIFT_create().detectAndCompute with OpenCV's defaults, cast_to_gtsfm_keypoints (utils/features.py:16-37) and
+// Keypoints.get_top_k (keypoints.py:89-110). Arithmetic is the one restated in oracle/sift.c (pinned to the reference's
+// OpenCV fixture), including its deterministic exp/sin/cos polynomials and fixed-point histograms, so the HIP path
+// and the oracle agree bit for bit; FMA contraction is off for this file (explicit fmaf only).
+//
+// Pipeline per batch (every launch covers all images of the batch):
+//   gray+2x upsample -> per octave: [decimate] + 5 x (row blur -> column blur fused with the DoG difference)
+//   -> extrema (26-neighbourhood) -> refinement (thread per candidate, location dedup by atomic bitmap)
+//   -> orientation (wave per location, fixed-point LDS histogram) ; then per image top-k by response
+//   (radix select + bitonic sort in LDS) -> descriptors only for the kept keypoints (wave per keypoint,
+//   fixed-point 360-bin LDS histogram).
+// The blur passes are the HBM-bound part: each level is read once per pass through an LDS tile and written once
+// (+ the DoG level).
+#pragma clang fp contract(off)
+#include <float.h>
+#include <math.h>
+
+#include "common.hpp"
+
+namespace {
+
+constexpr int kLayers = 3;
+constexpr int kLevels = kLayers + 3;
+constexpr int kDogs = kLayers + 2;
+constexpr int kMaxOct = 16;
+constexpr int kMaxR = 31;
+constexpr float kSigma = 1.6f;
+constexpr float kInitSigma = 0.5f;
+constexpr int kBorder = 5;
+constexpr int kMaxInterp = 5;
+constexpr int kOriBins = 36;
+constexpr float kOriSigFctr = 1.5f;
+constexpr float kOriRadius = 3 * kOriSigFctr;
+constexpr float kOriPeakRatio = 0.8f;
+constexpr float kDescrSclFctr = 3.f;
+constexpr float kDescrMagThr = 0.2f;
+constexpr float kIntDescrFctr = 512.f;
+constexpr float kContrast = 0.04f;
+constexpr float kEdge = 10.f;
+constexpr float kFixScale = 16777216.0f;  // 2^24
+
+struct Taps {
+    float k[kMaxR + 1];
+    int r;
+};
+
+// ------------------------------------------------------------------ deterministic math (== oracle/sift.c)
+__device__ __forceinline__ float exp2_det(float t) {
+    if (t < -126.f) return 0.f;
+    const float n = floorf(t);
+    const float f = t - n;
+    float q = fmaf(1.32154867901443053e-06f, f, 1.52527338040598377e-05f);
+    q = fmaf(q, f, 1.54035303933816061e-04f);
+    q = fmaf(q, f, 1.33335581464284411e-03f);
+    q = fmaf(q, f, 9.61812910762847688e-03f);
+    q = fmaf(q, f, 5.55041086648215762e-02f);
+    q = fmaf(q, f, 2.40226506959100694e-01f);
+    q = fmaf(q, f, 6.93147180559945286e-01f);
+    q = fmaf(q, f, 1.0f);
+    return ldexpf(q, (int)n);
+}
+
+__device__ __forceinline__ float exp_det(float x) { return exp2_det(x * 1.4426950408889634f); }
+
+__device__ __forceinline__ void sincos_det(float a, float* s, float* c) {
+    const float k = rintf(a * 0.63661977236758134f);
+    float r = fmaf(-k, 1.5707963705062866f, a);
+    r = fmaf(-k, -4.3711388286737929e-08f, r);
+    const float r2 = r * r;
+    const float sp =
+        fmaf(fmaf(fmaf(-1.9841269841269841e-04f, r2, 8.3333333333333333e-03f), r2, -1.6666666666666667e-01f), r2 * r, r);
+    const float cp = fmaf(fmaf(fmaf(fmaf(2.4801587301587302e-05f, r2, -1.3888888888888889e-03f), r2,
+                                    4.1666666666666667e-02f), r2, -0.5f), r2, 1.0f);
+    const int q = ((int)k) & 3;
+    if (q == 0) { *s = sp; *c = cp; }
+    else if (q == 1) { *s = cp; *c = -sp; }
+    else if (q == 2) { *s = -sp; *c = -cp; }
+    else { *s = -cp; *c = sp; }
+}
+
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * 57.29577951308232f, p3 = -0.3258083974640975f * 57.29577951308232f,
+                p5 = 0.1555786518463281f * 57.29577951308232f, p7 = -0.04432655554792128f * 57.29577951308232f;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__device__ __forceinline__ unsigned long long to_fix(float v) { return (unsigned long long)(long long)(v * kFixScale); }
+__device__ __forceinline__ float from_fix(unsigned long long v) { return (float)(long long)v * (1.0f / kFixScale); }
+
+__device__ __forceinline__ int reflect101(int i, int n) {
+    if (n == 1) return 0;
+    while (i < 0 || i >= n) {
+        if (i < 0) i = -i;
+        if (i >= n) i = 2 * n - 2 - i;
+    }
+    return i;
+}
+
+// ------------------------------------------------------------------ records
+struct Cand {
+    int img, layer, r, c;
+};
+struct Refined {
+    int img, layer, r, c;
+    float xc, xr, xi, contr;
+};
+struct KeyRec {
+    float x, y, size, angle, response, xc, xr, scl;
+    int o, layer, r, c;
+};
+
+struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
+    const float* g[kMaxOct][kLayers];
+    int H[kMaxOct], W[kMaxOct];
+    size_t img_stride[kMaxOct];
+};
+
+// ------------------------------------------------------------------ kernels: pyramid
+__global__ void gray_upsample_kernel(const uint8_t* __restrict__ src, int C, int H, int W, float* __restrict__ up) {
+    const int W2 = 2 * W, H2 = 2 * H;
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    const int b = blockIdx.z;
+    if (x >= W2) return;
+    const uint8_t* s = src + (size_t)b * H * W * C;
+    auto gray = [&](int yy, int xx) -> float {
+        const uint8_t* p = s + ((size_t)yy * W + xx) * C;
+        if (C == 1) return (float)p[0];
+        return (float)((p[0] * 4899 + p[1] * 9617 + p[2] * 1868 + (1 << 13)) >> 14);
+    };
+    float fy = (float)((y + 0.5) * 0.5 - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= sy;
+    if (sy < 0) { sy = 0; fy = 0; }
+    if (sy >= H - 1) { sy = H - 1; fy = 0; }
+    const int sy1 = sy + 1 < H ? sy + 1 : H - 1;
+    float fx = (float)((x + 0.5) * 0.5 - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    if (sx < 0) { sx = 0; fx = 0; }
+    if (sx >= W - 1) { sx = W - 1; fx = 0; }
+    const int sx1 = sx + 1 < W ? sx + 1 : W - 1;
+    const float r0 = gray(sy, sx) * (1.f - fx) + gray(sy, sx1) * fx;
+    const float r1 = gray(sy1, sx) * (1.f - fx) + gray(sy1, sx1) * fx;
+    up[(size_t)b * H2 * W2 + (size_t)y * W2 + x] = r0 * (1.f - fy) + r1 * fy;
+}
+
+constexpr int kRowTile = 256;
+
+__global__ __launch_bounds__(kRowTile) void row_blur_kernel(const float* __restrict__ src, float* __restrict__ dst,
+                                                            int H, int W, Taps t) {
+    __shared__ float buf[kRowTile + 2 * kMaxR];
+    const int y = blockIdx.y, b = blockIdx.z, x0 = blockIdx.x * kRowTile, tid = threadIdx.x;
+    const float* s = src + (size_t)b * H * W + (size_t)y * W;
+    const int r = t.r;
+    for (int i = tid; i < kRowTile + 2 * r; i += kRowTile) buf[i] = s[reflect101(x0 - r + i, W)];
+    __syncthreads();
+    const int x = x0 + tid;
+    if (x >= W) return;
+    float acc = t.k[0] * buf[r + tid];
+    for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], buf[r + tid - j] + buf[r + tid + j], acc);
+    dst[(size_t)b * H * W + (size_t)y * W + x] = acc;
+}
+
+constexpr int kColTileX = 64, kColTileY = 64, kColThreadsY = 4;
+
+__global__ __launch_bounds__(kColTileX* kColThreadsY) void col_blur_kernel(const float* __restrict__ tmp,
+                                                                           float* __restrict__ dst,
+                                                                           const float* __restrict__ prev,
+                                                                           float* __restrict__ dog, int H, int W,
+                                                                           Taps t) {
+    __shared__ float tile[kColTileY + 2 * kMaxR][kColTileX];
+    const int tx = threadIdx.x, ty = threadIdx.y, b = blockIdx.z;
+    const int x0 = blockIdx.x * kColTileX, y0 = blockIdx.y * kColTileY;
+    const int r = t.r;
+    const size_t base = (size_t)b * H * W;
+    const int x = x0 + tx;
+    for (int i = ty; i < kColTileY + 2 * r; i += kColThreadsY) {
+        const int yy = reflect101(y0 - r + i, H);
+        tile[i][tx] = (x < W) ? tmp[base + (size_t)yy * W + x] : 0.f;
+    }
+    __syncthreads();
+    if (x >= W) return;
+    for (int k = 0; k < kColTileY / kColThreadsY; ++k) {
+        const int ly = ty + kColThreadsY * k;
+        const int y = y0 + ly;
+        if (y >= H) break;
+        float acc = t.k[0] * tile[r + ly][tx];
+        for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], tile[r + ly - j][tx] + tile[r + ly + j][tx], acc);
+        const size_t o = base + (size_t)y * W + x;
+        dst[o] = acc;
+        if (dog) dog[o] = acc - prev[o];
+    }
+}
+
+__global__ void decimate_kernel(const float* __restrict__ src, int Hs, int Ws, float* __restrict__ dst, int H,
+                                int W) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, b = blockIdx.z;
+    if (x >= W) return;
+    dst[(size_t)b * H * W + (size_t)y * W + x] = src[(size_t)b * Hs * Ws + (size_t)(2 * y) * Ws + 2 * x];
+}
+
+// ------------------------------------------------------------------ kernels: detection
+struct DogSet {
+    const float* d[kDogs];
+};
+
+__global__ void extrema_kernel(DogSet D, int H, int W, Cand* __restrict__ cands, int* __restrict__ n_cand, int cap) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.y;
+    const int img = blockIdx.z / kLayers, layer = blockIdx.z % kLayers + 1;
+    if (c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) return;
+    const size_t base = (size_t)img * H * W;
+    const float* cur = D.d[layer] + base;
+    const float val = cur[(size_t)r * W + c];
+    const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
+    if (!(fabsf(val) > threshold)) return;
+    const float* prv = D.d[layer - 1] + base;
+    const float* nxt = D.d[layer + 1] + base;
+    bool ismax = val > 0, ismin = val < 0;
+    for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+            const size_t o = (size_t)(r + dy) * W + (c + dx);
+            const float a = prv[o], bb = nxt[o], m = cur[o];
+            if (ismax && !(val >= a && val >= bb && val >= m)) ismax = false;
+            if (ismin && !(val <= a && val <= bb && val <= m)) ismin = false;
+        }
+    if (!ismax && !ismin) return;
+    const int slot = atomicAdd(n_cand, 1);
+    if (slot < cap) cands[slot] = Cand{img, layer, r, c};
+}
+
+#define DAT(p, r, c) ((p)[(size_t)(r) * W + (c)])
+
+__global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restrict__ n_cand_p, int cap, DogSet D, int H,
+                              int W, int n_img, uint32_t* __restrict__ seen, Refined* __restrict__ out,
+                              int* __restrict__ n_out, int out_cap) {
+    const int n_cand = min(*n_cand_p, cap);
+    const float img_scale = 1.f / 255.f;
+    const float deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale, cross_deriv_scale = img_scale * 0.25f;
+    for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < n_cand; id += gridDim.x * blockDim.x) {
+        const Cand cd = cands[id];
+        const size_t base = (size_t)cd.img * H * W;
+        int layer = cd.layer, r = cd.r, c = cd.c;
+        float xi = 0, xr = 0, xc = 0;
+        int i = 0;
+        bool ok = true;
+        for (; i < kMaxInterp; i++) {
+            const float* img = D.d[layer] + base;
+            const float* prev = D.d[layer - 1] + base;
+            const float* next = D.d[layer + 1] + base;
+            const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
+            const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
+            const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
+            const float v2 = DAT(img, r, c) * 2;
+            const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
+            const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
+            const float dss = (DAT(next, r, c) + DAT(prev, r, c) - v2) * second_deriv_scale;
+            const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
+                               DAT(img, r - 1, c - 1)) * cross_deriv_scale;
+            const float dxs = (DAT(next, r, c + 1) - DAT(next, r, c - 1) - DAT(prev, r, c + 1) +
+                               DAT(prev, r, c - 1)) * cross_deriv_scale;
+            const float dys = (DAT(next, r + 1, c) - DAT(next, r - 1, c) - DAT(prev, r + 1, c) +
+                               DAT(prev, r - 1, c)) * cross_deriv_scale;
+            const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
+                        a22 = dss;
+            float det = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+            float X0 = 0, X1 = 0, X2 = 0;
+            if (det != 0) {
+                det = 1 / det;
+                X0 = det * (dD0 * (a11 * a22 - a12 * a21) - a01 * (dD1 * a22 - a12 * dD2) + a02 * (dD1 * a21 - a11 * dD2));
+                X1 = det * (a00 * (dD1 * a22 - a12 * dD2) - dD0 * (a10 * a22 - a12 * a20) + a02 * (a10 * dD2 - dD1 * a20));
+                X2 = det * (a00 * (a11 * dD2 - dD1 * a21) - a01 * (a10 * dD2 - dD1 * a20) + dD0 * (a10 * a21 - a11 * a20));
+            }
+            xi = -X2;
+            xr = -X1;
+            xc = -X0;
+            if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+            if (fabsf(xi) > (float)(INT32_MAX / 3) || fabsf(xr) > (float)(INT32_MAX / 3) ||
+                fabsf(xc) > (float)(INT32_MAX / 3)) {
+                ok = false;
+                break;
+            }
+            c += (int)rintf(xc);
+            r += (int)rintf(xr);
+            layer += (int)rintf(xi);
+            if (layer < 1 || layer > kLayers || c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) {
+                ok = false;
+                break;
+            }
+        }
+        if (!ok || i >= kMaxInterp) continue;
+        const float* img = D.d[layer] + base;
+        const float* prev = D.d[layer - 1] + base;
+        const float* next = D.d[layer + 1] + base;
+        const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
+        const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
+        const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
+        const float tt = dD0 * xc + dD1 * xr + dD2 * xi;
+        const float contr = DAT(img, r, c) * img_scale + tt * 0.5f;
+        if (fabsf(contr) * kLayers < kContrast) continue;
+        const float v2 = DAT(img, r, c) * 2.f;
+        const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
+        const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
+        const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
+                           DAT(img, r - 1, c - 1)) * cross_deriv_scale;
+        const float tr = dxx + dyy;
+        const float det = dxx * dyy - dxy * dxy;
+        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) continue;
+        // duplicates (same refined location) are identical keypoints: keep the first claimant
+        const size_t bit = (((size_t)cd.img * kLayers + (layer - 1)) * H + r) * W + c;
+        const uint32_t m = 1u << (bit & 31);
+        if (atomicOr(&seen[bit >> 5], m) & m) continue;
+        const int slot = atomicAdd(n_out, 1);
+        if (slot < out_cap) out[slot] = Refined{cd.img, layer, r, c, xc, xr, xi, contr};
+    }
+}
+
+struct GaussSet {
+    const float* g[kLevels];
+};
+
+// One wave per refined location: orientation histogram (fixed point, LDS u64 atomics), peaks -> keypoints.
+__global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restrict__ refs,
+                                                         const int* __restrict__ n_ref_p, int ref_cap, GaussSet G,
+                                                         int H, int W, int o, KeyRec* __restrict__ kps,
+                                                         int* __restrict__ kp_counts, int kp_cap) {
+    __shared__ unsigned long long hist[kOriBins];
+    const int lane = threadIdx.x;
+    const int n_ref = min(*n_ref_p, ref_cap);
+    for (int id = blockIdx.x; id < n_ref; id += gridDim.x) {
+        if (lane < kOriBins) hist[lane] = 0ull;
+        __syncthreads();
+        const Refined rf = refs[id];
+        const float size_oct = kSigma * exp2_det(((float)rf.layer + rf.xi) / kLayers);
+        const float scl = size_oct;
+        const int radius = (int)rintf(kOriRadius * scl);
+        const float sigma = kOriSigFctr * scl;
+        const float expf_scale = -1.f / (2.f * sigma * sigma);
+        const float* img = G.g[rf.layer] + (size_t)rf.img * H * W;
+        const int side = 2 * radius + 1;
+        for (int k = lane; k < side * side; k += 64) {
+            const int i = k / side - radius, j = k % side - radius;
+            const int y = rf.r + i, x = rf.c + j;
+            if (y <= 0 || y >= H - 1 || x <= 0 || x >= W - 1) continue;
+            const float dx = img[(size_t)y * W + x + 1] - img[(size_t)y * W + x - 1];
+            const float dy = img[(size_t)(y - 1) * W + x] - img[(size_t)(y + 1) * W + x];
+            const float w = exp_det((float)(i * i + j * j) * expf_scale);
+            const float ori = fast_atan2(dy, dx);
+            const float mag = sqrtf(fmaf(dx, dx, dy * dy));
+            int bin = (int)rintf((kOriBins / 360.f) * ori);
+            if (bin >= kOriBins) bin -= kOriBins;
+            if (bin < 0) bin += kOriBins;
+            atomicAdd(&hist[bin], to_fix(w * mag));
+        }
+        __syncthreads();
+        if (lane == 0) {
+            const int n = kOriBins;
+            float t[kOriBins + 4], h[kOriBins];
+            for (int i = 0; i < n; ++i) t[i + 2] = from_fix(hist[i]);
+            t[1] = t[n + 1];
+            t[0] = t[n];
+            t[n + 2] = t[2];
+            t[n + 3] = t[3];
+            float maxval = 0.f;
+            for (int i = 0; i < n; i++) {
+                h[i] = (t[i] + t[i + 4]) * (1.f / 16.f) + (t[i + 1] + t[i + 3]) * (4.f / 16.f) + t[i + 2] * (6.f / 16.f);
+                maxval = i == 0 ? h[0] : fmaxf(maxval, h[i]);
+            }
+            const float mag_thr = maxval * kOriPeakRatio;
+            for (int j = 0; j < n; j++) {
+                const int l = j > 0 ? j - 1 : n - 1;
+                const int r2 = j < n - 1 ? j + 1 : 0;
+                if (h[j] > h[l] && h[j] > h[r2] && h[j] >= mag_thr) {
+                    float bin = j + 0.5f * (h[l] - h[r2]) / (h[l] - 2 * h[j] + h[r2]);
+                    bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+                    float angle = 360.f - (360.f / n) * bin;
+                    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+                    const int slot = atomicAdd(&kp_counts[rf.img], 1);
+                    if (slot < kp_cap) {
+                        const float sc = (float)(1 << o) * 0.5f;
+                        KeyRec kr;
+                        kr.x = ((float)rf.c + rf.xc) * sc;
+                        kr.y = ((float)rf.r + rf.xr) * sc;
+                        kr.size = size_oct * (float)(1 << o) * 2.f * 0.5f;
+                        kr.angle = angle;
+                        kr.response = fabsf(rf.contr);
+                        kr.xc = rf.xc;
+                        kr.xr = rf.xr;
+                        kr.scl = scl;
+                        kr.o = o;
+                        kr.layer = rf.layer;
+                        kr.r = rf.r;
+                        kr.c = rf.c;
+                        kps[(size_t)rf.img * kp_cap + slot] = kr;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ top-k per image
+constexpr int kTopkThreads = 1024;
+
+struct SortRec {
+    unsigned long long key;  // (~response bits) << 32 | location code
+    uint32_t angle;          // angle bits (non-negative float)
+    int idx;
+};
+
+__device__ __forceinline__ bool rec_less(const SortRec& a, const SortRec& b) {
+    if (a.key != b.key) return a.key < b.key;
+    if (a.angle != b.angle) return a.angle < b.angle;
+    return a.idx < b.idx;
+}
+
+__device__ __forceinline__ SortRec make_rec(const KeyRec& k, int idx) {
+    const uint32_t hi = ~__float_as_uint(k.response);
+    const uint32_t lo = ((uint32_t)k.o << 28) | ((uint32_t)k.layer << 26) | ((uint32_t)k.r << 13) | (uint32_t)k.c;
+    return SortRec{((unsigned long long)hi << 32) | lo, __float_as_uint(k.angle), idx};
+}
+
+__device__ void bitonic_sort(SortRec* a, int n_pow2) {
+    for (int size = 2; size <= n_pow2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int k = threadIdx.x; k < n_pow2; k += blockDim.x) {
+                const int o = k ^ stride;
+                if (o > k) {
+                    const SortRec x = a[k], y = a[o];
+                    const bool up = ((k & size) == 0);
+                    if (rec_less(y, x) == up) {
+                        a[k] = y;
+                        a[o] = x;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+}
+
+// Selects the max_kpts keypoints of largest response (ties: octave, layer, row, col, angle) and orders them.
+__global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __restrict__ kps,
+                                                            const int* __restrict__ kp_counts, int kp_cap,
+                                                            int max_kpts, int* __restrict__ sel, int* __restrict__ n_sel) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int* hdr = (int*)smem;                         // [0] n_less, [1] n_eq, [2] scratch
+    int* histo = (int*)(smem + 16);                // [256]
+    SortRec* recs = (SortRec*)(smem + 16 + 1024);  // [pow2(max_kpts)]
+    const int img = blockIdx.x, tid = threadIdx.x;
+    const int N = min(kp_counts[img], kp_cap);
+    const KeyRec* K = kps + (size_t)img * kp_cap;
+    const int k = min(N, max_kpts);
+    int np2 = 1;
+    while (np2 < k) np2 <<= 1;
+    uint32_t T = 0xFFFFFFFFu;  // threshold on the hi word: take all hi < T, then the smallest ties hi == T
+    if (N > max_kpts) {
+        uint32_t prefix = 0;
+        int need = k;
+        for (int pass = 0; pass < 4; ++pass) {
+            const int shift = 24 - 8 * pass;
+            const uint32_t pmask = pass == 0 ? 0u : (0xFFFFFFFFu << (shift + 8));
+            for (int i = tid; i < 256; i += kTopkThreads) histo[i] = 0;
+            __syncthreads();
+            for (int i = tid; i < N; i += kTopkThreads) {
+                const uint32_t hi = ~__float_as_uint(K[i].response);
+                if ((hi & pmask) == (prefix & pmask)) atomicAdd(&histo[(hi >> shift) & 255], 1);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                int acc = 0, d = 0;
+                for (; d < 256; ++d) {
+                    if (acc + histo[d] >= need) break;
+                    acc += histo[d];
+                }
+                hdr[2] = d;
+                hdr[3] = need - acc;
+            }
+            __syncthreads();
+            prefix |= (uint32_t)hdr[2] << shift;
+            need = hdr[3];
+            __syncthreads();
+        }
+        T = prefix;
+    }
+    // gather: all with hi < T (count k - need_eq), then ties hi == T sorted, truncated
+    if (tid == 0) { hdr[0] = 0; hdr[1] = 0; }
+    __syncthreads();
+    for (int i = tid; i < N; i += kTopkThreads) {
+        const uint32_t hi = ~__float_as_uint(K[i].response);
+        if (N <= max_kpts || hi < T) recs[atomicAdd(&hdr[0], 1)] = make_rec(K[i], i);
+    }
+    __syncthreads();
+    const int n_less = hdr[0];
+    if (N > max_kpts) {
+        // ties at the threshold (rare, few): collect after the strict set, sort them, keep the first (k - n_less)
+        for (int i = tid; i < N; i += kTopkThreads) {
+            const uint32_t hi = ~__float_as_uint(K[i].response);
+            if (hi == T) {
+                const int s = atomicAdd(&hdr[1], 1);
+                if (n_less + s < np2) recs[n_less + s] = make_rec(K[i], i);
+            }
+        }
+        __syncthreads();
+        const int n_eq = min(hdr[1], np2 - n_less);
+        // selection sort of the tie group by (key, angle) is enough: ties are a handful of keypoints
+        if (tid == 0) {
+            for (int a = 0; a < n_eq; ++a) {
+                int m = a;
+                for (int b = a + 1; b < n_eq; ++b)
+                    if (rec_less(recs[n_less + b], recs[n_less + m])) m = b;
+                const SortRec t = recs[n_less + a];
+                recs[n_less + a] = recs[n_less + m];
+                recs[n_less + m] = t;
+            }
+        }
+        __syncthreads();
+    }
+    for (int i = k + tid; i < np2; i += kTopkThreads) recs[i] = SortRec{~0ull, ~0u, 0x7FFFFFFF};
+    __syncthreads();
+    bitonic_sort(recs, np2);
+    for (int i = tid; i < k; i += kTopkThreads) sel[(size_t)img * max_kpts + i] = recs[i].idx;
+    if (tid == 0) n_sel[img] = k;
+}
+
+// ------------------------------------------------------------------ descriptors: one wave per kept keypoint
+__global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict__ kps, int kp_cap,
+                                                        const int* __restrict__ sel, const int* __restrict__ n_sel,
+                                                        int n_img, int max_kpts, LevelTable L,
+                                                        float* __restrict__ out_xy, float* __restrict__ out_attr,
+                                                        float* __restrict__ out_desc) {
+    constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
+    __shared__ unsigned long long hist[HB];
+    __shared__ float dst[128];
+    const int lane = threadIdx.x;
+    for (int slot = blockIdx.x; slot < n_img * max_kpts; slot += gridDim.x) {
+        const int img = slot / max_kpts, q = slot % max_kpts;
+        if (q >= n_sel[img]) continue;  // uniform per block
+        const KeyRec kp = kps[(size_t)img * kp_cap + sel[(size_t)img * max_kpts + q]];
+        for (int i = lane; i < HB; i += 64) hist[i] = 0ull;
+        __syncthreads();
+        const int H = L.H[kp.o], W = L.W[kp.o];
+        const float* img_p = L.g[kp.o][kp.layer - 1] + (size_t)img * L.img_stride[kp.o];
+        const float ptx = (float)kp.c + kp.xc, pty = (float)kp.r + kp.xr;
+        float ori = 360.f - kp.angle;
+        if (fabsf(ori - 360.f) < FLT_EPSILON) ori = 0.f;
+        const float scl = kp.scl;
+        const int px = (int)rintf(ptx), py = (int)rintf(pty);
+        float sin_t, cos_t;
+        sincos_det(ori * (float)(3.14159265358979323846 / 180), &sin_t, &cos_t);
+        const float bins_per_rad = n / 360.f;
+        const float exp_scale = -1.f / (d * d * 0.5f);
+        const float hist_width = kDescrSclFctr * scl;
+        int radius = (int)rintf(hist_width * 1.4142135623730951f * (d + 1) * 0.5f);
+        const int diag = (int)sqrt(((double)W) * W + ((double)H) * H);
+        if (radius > diag) radius = diag;
+        cos_t /= hist_width;
+        sin_t /= hist_width;
+        const int side = 2 * radius + 1;
+        for (int k = lane; k < side * side; k += 64) {
+            const int i = k / side - radius, j = k % side - radius;
+            const float c_rot = j * cos_t - i * sin_t;
+            const float r_rot = j * sin_t + i * cos_t;
+            float rbin = r_rot + d / 2 - 0.5f;
+            float cbin = c_rot + d / 2 - 0.5f;
+            const int r = py + i, c = px + j;
+            if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < H - 1 && c > 0 && c < W - 1))
+                continue;
+            const float dx = img_p[(size_t)r * W + c + 1] - img_p[(size_t)r * W + c - 1];
+            const float dy = img_p[(size_t)(r - 1) * W + c] - img_p[(size_t)(r + 1) * W + c];
+            const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
+            const float o = fast_atan2(dy, dx);
+            const float mag0 = sqrtf(fmaf(dx, dx, dy * dy));
+            const float w = exp_det(wexp);
+            float obin = (o - ori) * bins_per_rad;
+            const float mag = mag0 * w;
+            const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
+            int o0 = (int)floorf(obin);
+            rbin -= r0;
+            cbin -= c0;
+            obin -= o0;
+            if (o0 < 0) o0 += n;
+            if (o0 >= n) o0 -= n;
+            const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
+            const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
+            const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
+            const float v_rco101 = v_rc10 * obin, v_rco100 = v_rc10 - v_rco101;
+            const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
+            const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
+            const int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
+            atomicAdd(&hist[idx], to_fix(v_rco000));
+            atomicAdd(&hist[idx + 1], to_fix(v_rco001));
+            atomicAdd(&hist[idx + (n + 2)], to_fix(v_rco010));
+            atomicAdd(&hist[idx + (n + 3)], to_fix(v_rco011));
+            atomicAdd(&hist[idx + (d + 2) * (n + 2)], to_fix(v_rco100));
+            atomicAdd(&hist[idx + (d + 2) * (n + 2) + 1], to_fix(v_rco101));
+            atomicAdd(&hist[idx + (d + 3) * (n + 2)], to_fix(v_rco110));
+            atomicAdd(&hist[idx + (d + 3) * (n + 2) + 1], to_fix(v_rco111));
+        }
+        __syncthreads();
+        if (lane == 0) {
+            for (int i = 0; i < d; i++)
+                for (int j = 0; j < d; j++) {
+                    const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
+                    float h[10];
+                    for (int k = 0; k < n + 2; ++k) h[k] = from_fix(hist[idx + k]);
+                    h[0] += h[n];
+                    h[1] += h[n + 1];
+                    for (int k = 0; k < n; k++) dst[(i * d + j) * n + k] = h[k];
+                }
+            float nrm2 = 0;
+            for (int k = 0; k < 128; k++) nrm2 += dst[k] * dst[k];
+            const float thr = sqrtf(nrm2) * kDescrMagThr;
+            nrm2 = 0;
+            for (int i = 0; i < 128; i++) {
+                const float val = fminf(dst[i], thr);
+                dst[i] = val;
+                nrm2 += val * val;
+            }
+            nrm2 = kIntDescrFctr / fmaxf(sqrtf(nrm2), FLT_EPSILON);
+            for (int k = 0; k < 128; k++) {
+                const int v = (int)rintf(dst[k] * nrm2);
+                dst[k] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
+            }
+        }
+        __syncthreads();
+        float* od = out_desc + ((size_t)img * max_kpts + q) * 128;
+        for (int k = lane; k < 128; k += 64) od[k] = dst[k];
+        if (lane == 0) {
+            out_xy[((size_t)img * max_kpts + q) * 2] = kp.x;
+            out_xy[((size_t)img * max_kpts + q) * 2 + 1] = kp.y;
+            out_attr[((size_t)img * max_kpts + q) * 3] = kp.size;
+            out_attr[((size_t)img * max_kpts + q) * 3 + 1] = kp.angle;
+            out_attr[((size_t)img * max_kpts + q) * 3 + 2] = kp.response;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ host-side layout
+int gauss_taps(double sigma, Taps* t) {
+    int n = (int)lrint(sigma * 4 * 2 + 1) | 1;
+    if (n > 2 * kMaxR + 1) return -1;
+    float full[2 * kMaxR + 1];
+    const double scale2X = -0.5 / (sigma * sigma);
+    double sum = 0;
+    for (int i = 0; i < n; ++i) {
+        const double x = i - (n - 1) * 0.5;
+        full[i] = (float)exp(scale2X * x * x);
+        sum += full[i];
+    }
+    sum = 1. / sum;
+    for (int i = 0; i < n; ++i) full[i] = (float)(full[i] * sum);
+    t->r = n / 2;
+    for (int j = 0; j <= t->r; ++j) t->k[j] = full[t->r + j];
+    for (int j = t->r + 1; j <= kMaxR; ++j) t->k[j] = 0.f;
+    return 0;
+}
+
+constexpr int kCandCapPerImg = 1 << 19;
+constexpr int kKpCapPerImg = 1 << 16;
+
+struct Layout {
+    int B, H, W, n_oct, max_kpts;
+    int Ho[kMaxOct], Wo[kMaxOct];
+    size_t g[kMaxOct][kLevels], dg[kMaxOct][kDogs];  // byte offsets
+    size_t up, tmp, seen, seen_bytes, cand, ref, kps, kp_counts, counters, sel, n_sel, total;
+};
+
+int num_octaves(int H, int W) {
+    const int m = 2 * (H < W ? H : W);
+    int n = (int)lrint(log((double)m) / log(2.) - 2) + 1;
+    return n > kMaxOct ? kMaxOct : n;
+}
+
+Layout make_layout(int B, int H, int W, int max_kpts) {
+    Layout L{};
+    L.B = B;
+    L.H = H;
+    L.W = W;
+    L.max_kpts = max_kpts;
+    L.n_oct = num_octaves(H, W);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += gtsfm_align_up(bytes, 256);
+        return o;
+    };
+    int h = 2 * H, w = 2 * W;
+    for (int o = 0; o < L.n_oct; ++o) {
+        L.Ho[o] = h;
+        L.Wo[o] = w;
+        const size_t lvl = (size_t)B * h * w * sizeof(float);
+        for (int i = 0; i < kLevels; ++i) L.g[o][i] = take(lvl);
+        for (int i = 0; i < kDogs; ++i) L.dg[o][i] = take(lvl);
+        h /= 2;
+        w /= 2;
+    }
+    const size_t lvl0 = (size_t)B * (2 * H) * (2 * W) * sizeof(float);
+    L.up = take(lvl0);
+    L.tmp = take(lvl0);
+    L.seen_bytes = gtsfm_align_up(((size_t)B * kLayers * (2 * H) * (2 * W) + 31) / 32 * 4, 256);
+    L.seen = take(L.seen_bytes);
+    L.cand = take((size_t)B * kCandCapPerImg * sizeof(Cand));
+    L.ref = take((size_t)B * kCandCapPerImg * sizeof(Refined));
+    L.kps = take((size_t)B * kKpCapPerImg * sizeof(KeyRec));
+    L.kp_counts = take((size_t)B * sizeof(int));
+    L.counters = take(16);
+    L.sel = take((size_t)B * max_kpts * sizeof(int));
+    L.n_sel = take((size_t)B * sizeof(int));
+    L.total = off;
+    return L;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gtsfm_sift_workspace_bytes(int n_img, int H, int W, int max_kpts) {
+    if (n_img <= 0 || H < 16 || W < 16 || max_kpts <= 0) return 0;
+    return make_layout(n_img, H, W, max_kpts).total;
+}
+
+int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int channels, int max_kpts, void* d_workspace,
+                       size_t workspace_bytes, float* d_xy, float* d_attr, float* d_desc, int* d_counts,
+                       int* d_n_detected, void* stream_v) {
+    hipStream_t stream = (hipStream_t)stream_v;
+    if (n_img == 0) return GTSFM_OK;
+    if (!d_images || !d_workspace || !d_xy || !d_attr || !d_desc || !d_counts || n_img < 0 || H < 16 || W < 16 ||
+        (channels != 1 && channels != 3) || max_kpts <= 0 || max_kpts > 8192 || 2 * H >= 8192 || 2 * W >= 8192)
+        return GTSFM_ERR_ARG;
+    const Layout L = make_layout(n_img, H, W, max_kpts);
+    if (workspace_bytes < L.total) return GTSFM_ERR_CAPACITY;
+    unsigned char* ws = (unsigned char*)d_workspace;
+    auto F = [&](size_t off) { return (float*)(ws + off); };
+    int* counters = (int*)(ws + L.counters);
+    int* kp_counts = (int*)(ws + L.kp_counts);
+    const int B = n_img;
+
+    Taps taps[kLevels];
+    {
+        double sig[kLevels];
+        sig[0] = kSigma;
+        const double k = pow(2., 1. / kLayers);
+        for (int i = 1; i < kLevels; ++i) {
+            const double sig_prev = pow(k, (double)(i - 1)) * kSigma;
+            const double sig_total = sig_prev * k;
+            sig[i] = sqrt(sig_total * sig_total - sig_prev * sig_prev);
+        }
+        const double sig_diff = sqrt(fmax(kSigma * kSigma - kInitSigma * kInitSigma * 4, 0.01));
+        if (gauss_taps((double)(float)sig_diff, &taps[0])) return GTSFM_ERR_ARG;
+        for (int i = 1; i < kLevels; ++i)
+            if (gauss_taps(sig[i], &taps[i])) return GTSFM_ERR_ARG;
+    }
+    GTSFM_CHECK_HIP(hipMemsetAsync(kp_counts, 0, (size_t)B * sizeof(int), stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(d_counts, 0, (size_t)B * sizeof(int), stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(d_xy, 0, (size_t)B * max_kpts * 2 * sizeof(float), stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(d_attr, 0, (size_t)B * max_kpts * 3 * sizeof(float), stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(d_desc, 0, (size_t)B * max_kpts * 128 * sizeof(float), stream));
+
+    auto blur = [&](const float* src, float* dst, const float* prev, float* dog, int h, int w, const Taps& t) {
+        hipLaunchKernelGGL(row_blur_kernel, dim3((w + kRowTile - 1) / kRowTile, h, B), dim3(kRowTile), 0, stream, src,
+                           F(L.tmp), h, w, t);
+        hipLaunchKernelGGL(col_blur_kernel, dim3((w + kColTileX - 1) / kColTileX, (h + kColTileY - 1) / kColTileY, B),
+                           dim3(kColTileX, kColThreadsY), 0, stream, F(L.tmp), dst, prev, dog, h, w, t);
+    };
+    hipLaunchKernelGGL(gray_upsample_kernel, dim3((2 * W + 255) / 256, 2 * H, B), dim3(256), 0, stream, d_images,
+                       channels, H, W, F(L.up));
+    GTSFM_CHECK_HIP(hipGetLastError());
+    for (int o = 0; o < L.n_oct; ++o) {
+        const int h = L.Ho[o], w = L.Wo[o];
+        if (o == 0) {
+            blur(F(L.up), F(L.g[0][0]), nullptr, nullptr, h, w, taps[0]);
+        } else {
+            hipLaunchKernelGGL(decimate_kernel, dim3((w + 255) / 256, h, B), dim3(256), 0, stream,
+                               F(L.g[o - 1][kLayers]), L.Ho[o - 1], L.Wo[o - 1], F(L.g[o][0]), h, w);
+        }
+        for (int i = 1; i < kLevels; ++i) blur(F(L.g[o][i - 1]), F(L.g[o][i]), F(L.g[o][i - 1]), F(L.dg[o][i - 1]), h, w,
+                                               taps[i]);
+        GTSFM_CHECK_HIP(hipGetLastError());
+        if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
+        GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, 16, stream));
+        GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.seen, 0,
+                                       gtsfm_align_up(((size_t)B * kLayers * h * w + 31) / 32 * 4, 4), stream));
+        DogSet D;
+        for (int i = 0; i < kDogs; ++i) D.d[i] = F(L.dg[o][i]);
+        hipLaunchKernelGGL(extrema_kernel, dim3((w + 255) / 256, h, B * kLayers), dim3(256), 0, stream, D, h, w,
+                           (Cand*)(ws + L.cand), counters + 0, B * kCandCapPerImg);
+        hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters + 0,
+                           B * kCandCapPerImg, D, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
+                           counters + 1, B * kCandCapPerImg);
+        GaussSet G;
+        for (int i = 0; i < kLevels; ++i) G.g[i] = F(L.g[o][i]);
+        hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),
+                           counters + 1, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps), kp_counts,
+                           kKpCapPerImg);
+        GTSFM_CHECK_HIP(hipGetLastError());
+    }
+    int np2 = 1;
+    while (np2 < max_kpts) np2 <<= 1;
+    const size_t topk_lds = 16 + 1024 + (size_t)np2 * sizeof(SortRec);
+    if (topk_lds > 160 * 1024) return GTSFM_ERR_ARG;
+    if (topk_lds > 65536)
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)topk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            (int)topk_lds));
+    hipLaunchKernelGGL(topk_kernel, dim3(B), dim3(kTopkThreads), topk_lds, stream, (const KeyRec*)(ws + L.kps),
+                       kp_counts, kKpCapPerImg, max_kpts, (int*)(ws + L.sel), d_counts);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    LevelTable T{};
+    for (int o = 0; o < L.n_oct; ++o) {
+        for (int i = 0; i < kLayers; ++i) T.g[o][i] = F(L.g[o][i + 1]);
+        T.H[o] = L.Ho[o];
+        T.W[o] = L.Wo[o];
+        T.img_stride[o] = (size_t)L.Ho[o] * L.Wo[o];
+    }
+    hipLaunchKernelGGL(descriptor_kernel, dim3(min(B * max_kpts, 16384)), dim3(64), 0, stream,
+                       (const KeyRec*)(ws + L.kps), kKpCapPerImg, (const int*)(ws + L.sel), d_counts, B, max_kpts, T,
+                       d_xy, d_attr, d_desc);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    if (d_n_detected) GTSFM_CHECK_HIP(hipMemcpyAsync(d_n_detected, kp_counts, (size_t)B * sizeof(int),
+                                                     hipMemcpyDeviceToDevice, stream));
+    return GTSFM_OK;
+}
+
+}  // extern "C"

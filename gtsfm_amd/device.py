@@ -100,3 +100,36 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
                                       native.stream_handle(stream))
         native.check(rc, "gtsfm_ransac_E_batched")
     return RansacResult(E[:P], R[:P], t[:P], n_inl[:P], status[:P], n_hyp[:P], mask[:P])
+
+
+class SiftResult:
+    """Per-image SIFT outputs (device tensors): xy (n,k,2), attr (n,k,3) size/angle/response, desc (n,k,128),
+    count (n,), n_detected (n,)."""
+
+    def __init__(self, xy, attr, desc, count, n_detected):
+        self.xy, self.attr, self.desc, self.count, self.n_detected = xy, attr, desc, count, n_detected
+
+
+def sift_extract(images: torch.Tensor, max_kpts: int, stream: Optional[torch.cuda.Stream] = None,
+                 out: Optional[SiftResult] = None, workspace: Optional[torch.Tensor] = None) -> SiftResult:
+    """SIFT + top-k on a batch of same-sized uint8 images (n, H, W) gray or (n, H, W, 3) RGB (gtsfm_sift_batched)."""
+    assert images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous()
+    n = images.shape[0]
+    H, W = images.shape[1], images.shape[2]
+    C = 1 if images.dim() == 3 else images.shape[3]
+    dev = images.device
+    L = native.lib()
+    if out is None:
+        out = SiftResult(torch.empty((n, max_kpts, 2), dtype=torch.float32, device=dev),
+                         torch.empty((n, max_kpts, 3), dtype=torch.float32, device=dev),
+                         torch.empty((n, max_kpts, 128), dtype=torch.float32, device=dev),
+                         torch.empty((n,), dtype=torch.int32, device=dev),
+                         torch.empty((n,), dtype=torch.int32, device=dev))
+    nbytes = L.gtsfm_sift_workspace_bytes(n, H, W, max_kpts)
+    ws = workspace if workspace is not None and workspace.numel() >= nbytes else _workspace(nbytes, dev)
+    if stream is not None:
+        ws.record_stream(stream)
+    rc = L.gtsfm_sift_batched(_ptr(images), n, H, W, C, max_kpts, _ptr(ws), ws.numel(), _ptr(out.xy), _ptr(out.attr),
+                              _ptr(out.desc), _ptr(out.count), _ptr(out.n_detected), native.stream_handle(stream))
+    native.check(rc, "gtsfm_sift_batched")
+    return out

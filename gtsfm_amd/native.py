@@ -55,6 +55,12 @@ SIGNATURES = {
          c_uint64, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p],
     ),
+    "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "gtsfm_sift_batched": (
+        c_int,
+        [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p],
+    ),
 }
 
 

@@ -87,6 +87,23 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            double* d_E, double* d_R, double* d_t, int* d_n_inliers, int* d_status,
                            int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
 
+/* ----------------------------------------------------------------------------------------------
+ * Detector-descriptor: SIFT (OpenCV defaults) + top-k by response over a batch of same-sized images.
+ *
+ * d_images[n_img][H][W][channels] uint8, channels 1 (gray) or 3 (RGB, converted like cv.COLOR_RGB2GRAY).
+ * Outputs per image, rows 0..count-1 valid, ordered by descending response:
+ *   d_xy[n_img][max_kpts][2]   keypoint (x, y) in pixels (x right, y down, origin top-left corner)
+ *   d_attr[n_img][max_kpts][3] (size, angle in degrees, response) as cv.KeyPoint
+ *   d_desc[n_img][max_kpts][128] float32 descriptors with integer values in [0, 255]
+ *   d_counts[n_img] = min(#keypoints, max_kpts); d_n_detected[n_img] (may be NULL) = #keypoints before top-k.
+ * Limits: 16 <= H, W < 4096, max_kpts <= 8192.
+ * ---------------------------------------------------------------------------------------------- */
+size_t gtsfm_sift_workspace_bytes(int n_img, int H, int W, int max_kpts);
+
+int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int channels, int max_kpts,
+                       void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_attr, float* d_desc,
+                       int* d_counts, int* d_n_detected, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
