@@ -74,14 +74,31 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
         for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += s * (q[i] * l[j]);
 }
 
-__device__ __forceinline__ double peval(const double* p, int deg, double x) {
+// ------------------------------------------------------------------ lane-private arrays in LDS
+// The solver's dynamically indexed arrays (the 5x9 and 10x20 eliminations, the Sturm chain, the isolation stack)
+// live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit consecutive 8-byte words, so every
+// access is bank-conflict free, and nothing spills to scratch. One 64-lane workgroup owns 102 KB + 16 KB.
+constexpr int kLanes = 64;
+constexpr int kUnion = 200;   // doubles per lane: Q (45) | A (200) | Sturm (121) + t (11) + stack (2 x 24)
+constexpr int kInts = 112;    // ints per lane: col perm (9) | stack va/vb (2 x 48) + chain degrees (11)
+constexpr int kStack = 48;  // == oracle/ransac.c isolation stack
+constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double) + (size_t)kInts * kLanes * sizeof(int);
+
+template <typename T>
+struct LaneArr {
+    T* p;
+    __device__ __forceinline__ T& operator[](int i) const { return p[i * kLanes]; }
+    __device__ __forceinline__ LaneArr at(int off) const { return LaneArr{p + off * kLanes}; }
+};
+
+__device__ __forceinline__ double peval(LaneArr<double> p, int deg, double x) {
     double v = p[deg];
     for (int i = deg - 1; i >= 0; --i) v = v * x + p[i];
     return v;
 }
 
-__device__ int prem(const double* a, int da, const double* b, int db, double* r) {
-    double t[11];
+// r = a mod b (deg_a >= deg_b) using scratch t (11 entries); returns degree of r (-1 if zero)
+__device__ int prem(LaneArr<double> a, int da, LaneArr<double> b, int db, LaneArr<double> r, LaneArr<double> t) {
     for (int i = 0; i <= da; ++i) t[i] = a[i];
     for (int k = da; k >= db; --k) {
         const double f = t[k] / b[db];
@@ -96,54 +113,93 @@ __device__ int prem(const double* a, int da, const double* b, int db, double* r)
     return dr;
 }
 
-struct Sturm {
-    double p[11][11];
-    int deg[11];
-    int n;
+struct SolverMem {
+    LaneArr<double> u;  // kUnion doubles
+    LaneArr<int> iv;    // kInts ints
 };
 
-__device__ int sign_changes(const Sturm& s, double x) {
+__device__ __forceinline__ SolverMem solver_mem(unsigned char* smem, int lane) {
+    double* d = (double*)smem;
+    int* iv = (int*)(smem + (size_t)kUnion * kLanes * sizeof(double));
+    return SolverMem{LaneArr<double>{d + lane}, LaneArr<int>{iv + lane}};
+}
+
+// Register-resident Sturm chain: row k (degree <= 10 - k) at kRowOff[k], zero-padded to length 11 - k. Horner over
+// the padded row equals Horner from the row's true degree bit for bit (leading zeros contribute exact zeros), and
+// rows past the chain length evaluate to 0 and are skipped exactly like the oracle's loop bound.
+constexpr int kChain = 66;
+__device__ __forceinline__ constexpr int row_off(int k) { return 11 * k - k * (k - 1) / 2; }
+
+__device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], double x) {
+    double v[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+        const int len = 11 - k, o = row_off(k);
+        double a = R[o + len - 1];
+#pragma unroll
+        for (int i = len - 2; i >= 0; --i) a = a * x + R[o + i];
+        v[k] = a;
+    }
     int c = 0;
     double prev = 0.0;
-    for (int k = 0; k < s.n; ++k) {
-        const double v = peval(s.p[k], s.deg[k], x);
-        if (v == 0.0) continue;
-        if (prev != 0.0 && ((v < 0.0) != (prev < 0.0))) ++c;
-        prev = v;
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+        if (v[k] != 0.0) {
+            if (prev != 0.0 && ((v[k] < 0.0) != (prev < 0.0))) ++c;
+            prev = v[k];
+        }
     }
     return c;
 }
 
-// Real roots (ascending) of a degree <= 10 polynomial: Sturm isolation + bisection.
-__device__ int real_roots(const double* pin, int deg, double* roots) {
-    double p[11];
+__device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
+    double a = R[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) a = a * x + R[i];
+    return a;
+}
+
+// Real roots (ascending) of a degree <= 10 polynomial: Sturm isolation + 80-step bisection, arithmetic identical to
+// oracle/ransac.c real_roots. Isolation runs first and records the isolating intervals; all intervals are then
+// bisected together (10 independent chains), so a wave never serialises one lane's bisection behind another's
+// isolation step.
+template <typename RootFn>
+__device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_root) {
+    LaneArr<double> S = m.u;  // chain rows at 11*k during construction
+    LaneArr<double> t = m.u.at(121);
+    LaneArr<int> sdeg = m.iv.at(2 * kStack);
     while (deg > 0 && fabs(pin[deg]) <= 1e-300) --deg;
     if (deg <= 0) return 0;
-    for (int i = 0; i <= deg; ++i) p[i] = pin[i] / pin[deg];
-    Sturm s;
-    for (int i = 0; i <= deg; ++i) s.p[0][i] = p[i];
-    s.deg[0] = deg;
-    for (int i = 1; i <= deg; ++i) s.p[1][i - 1] = (double)i * p[i];
-    s.deg[1] = deg - 1;
-    s.n = 2;
-    while (s.n < 11 && s.deg[s.n - 1] > 0) {
-        double r[11];
-        const int dr = prem(s.p[s.n - 2], s.deg[s.n - 2], s.p[s.n - 1], s.deg[s.n - 1], r);
+    for (int i = 0; i <= deg; ++i) S[i] = pin[i] / pin[deg];
+    sdeg[0] = deg;
+    for (int i = 1; i <= deg; ++i) S[11 + i - 1] = (double)i * S[i];
+    sdeg[1] = deg - 1;
+    int n = 2;
+    while (n < 11 && sdeg[n - 1] > 0) {
+        const int dr = prem(S.at(11 * (n - 2)), sdeg[n - 2], S.at(11 * (n - 1)), sdeg[n - 1], S.at(11 * n), t);
         if (dr < 0) break;
-        for (int i = 0; i <= dr; ++i) s.p[s.n][i] = -r[i];
-        s.deg[s.n] = dr;
-        s.n++;
+        for (int i = 0; i <= dr; ++i) S[11 * n + i] = -S[11 * n + i];
+        sdeg[n] = dr;
+        n++;
+    }
+    double R[kChain];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) {
+        const int dk = k < n ? sdeg[k] : -1;
+#pragma unroll
+        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dk ? S[11 * k + i] : 0.0;
     }
     double bound = 0.0;
-    for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(p[i]));
+    for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(S[i]));
     bound += 1.0;
-    double st_a[48], st_b[48];
-    int st_va[48], st_vb[48];
+    // isolation (stack and the interval list reuse the chain's LDS)
+    LaneArr<double> st_a = m.u, st_b = m.u.at(kStack), iv_a = m.u.at(2 * kStack), iv_b = m.u.at(2 * kStack + kMaxSol);
+    LaneArr<int> st_va = m.iv, st_vb = m.iv.at(kStack);
     int ns = 1, nr = 0, guard = 0;
     st_a[0] = -bound;
     st_b[0] = bound;
-    st_va[0] = sign_changes(s, -bound);
-    st_vb[0] = sign_changes(s, bound);
+    st_va[0] = sign_changes_reg(R, -bound);
+    st_vb[0] = sign_changes_reg(R, bound);
     while (ns > 0 && nr < kMaxSol && guard < 2000) {
         ++guard;
         --ns;
@@ -152,168 +208,219 @@ __device__ int real_roots(const double* pin, int deg, double* roots) {
         const int cnt = va - vb;
         if (cnt <= 0) continue;
         if (cnt == 1 || b - a < 1e-10 * fmax(1.0, fabs(a))) {
-            double lo = a, hi = b;
-            double flo = peval(p, deg, lo);
-            for (int it = 0; it < 80; ++it) {
-                const double mid = 0.5 * (lo + hi);
-                const double fm = peval(p, deg, mid);
-                if ((fm < 0.0) == (flo < 0.0) && fm != 0.0) {
-                    lo = mid;
-                    flo = fm;
-                } else {
-                    hi = mid;
-                }
-            }
-            roots[nr++] = 0.5 * (lo + hi);
+            iv_a[nr] = a;
+            iv_b[nr] = b;
+            ++nr;
             continue;
         }
         const double mid = 0.5 * (a + b);
-        const int vm = sign_changes(s, mid);
-        if (ns + 2 <= 48) {
+        const int vm = sign_changes_reg(R, mid);
+        if (ns + 2 <= kStack) {
             st_a[ns] = mid; st_b[ns] = b; st_va[ns] = vm; st_vb[ns] = vb; ++ns;
             st_a[ns] = a; st_b[ns] = mid; st_va[ns] = va; st_vb[ns] = vm; ++ns;
         }
     }
+    double lo[kMaxSol], hi[kMaxSol], flo[kMaxSol];
+#pragma unroll
+    for (int k = 0; k < kMaxSol; ++k) {
+        lo[k] = k < nr ? iv_a[k] : 0.0;
+        hi[k] = k < nr ? iv_b[k] : 0.0;
+        flo[k] = peval0(R, lo[k]);
+    }
+    for (int it = 0; it < 80; ++it) {
+#pragma unroll
+        for (int k = 0; k < kMaxSol; ++k) {
+            const double mid = 0.5 * (lo[k] + hi[k]);
+            const double fm = peval0(R, mid);
+            const bool left = (fm < 0.0) == (flo[k] < 0.0) && fm != 0.0;
+            lo[k] = left ? mid : lo[k];
+            flo[k] = left ? fm : flo[k];
+            hi[k] = left ? hi[k] : mid;
+        }
+    }
+    LaneArr<double> roots = iv_a;
+#pragma unroll
+    for (int k = 0; k < kMaxSol; ++k)
+        if (k < nr) roots[k] = 0.5 * (lo[k] + hi[k]);
+    for (int k = 0; k < nr; ++k) on_root(roots[k]);
     return nr;
 }
 
-// ------------------------------------------------------------------ Nister 5-point (one lane)
-__device__ bool nullspace_5x9(double q[5][9], double N[4][9]) {
-    int col[9];
+// ------------------------------------------------------------------ Nister 5-point (one lane, arrays in LDS)
+__device__ bool nullspace_5x9(const double* x1, const double* x2, SolverMem m, double N[4][9]) {
+    LaneArr<double> q = m.u;     // [5][9]
+    LaneArr<double> v = m.u.at(45);
+    LaneArr<int> col = m.iv;
+    for (int i = 0; i < 5; ++i) {
+        const double u1 = x1[2 * i], v1 = x1[2 * i + 1], u2 = x2[2 * i], v2 = x2[2 * i + 1];
+        q[9 * i + 0] = u2 * u1; q[9 * i + 1] = u2 * v1; q[9 * i + 2] = u2;
+        q[9 * i + 3] = v2 * u1; q[9 * i + 4] = v2 * v1; q[9 * i + 5] = v2;
+        q[9 * i + 6] = u1; q[9 * i + 7] = v1; q[9 * i + 8] = 1.0;
+    }
     for (int j = 0; j < 9; ++j) col[j] = j;
     for (int r = 0; r < 5; ++r) {
         int pr = r, pc = r;
         double best = -1.0;
         for (int i = r; i < 5; ++i)
             for (int j = r; j < 9; ++j)
-                if (fabs(q[i][j]) > best) { best = fabs(q[i][j]); pr = i; pc = j; }
+                if (fabs(q[9 * i + j]) > best) { best = fabs(q[9 * i + j]); pr = i; pc = j; }
         if (best < 1e-12) return false;
         if (pr != r)
-            for (int j = 0; j < 9; ++j) { const double t = q[r][j]; q[r][j] = q[pr][j]; q[pr][j] = t; }
+            for (int j = 0; j < 9; ++j) { const double tt = q[9 * r + j]; q[9 * r + j] = q[9 * pr + j]; q[9 * pr + j] = tt; }
         if (pc != r) {
-            for (int i = 0; i < 5; ++i) { const double t = q[i][r]; q[i][r] = q[i][pc]; q[i][pc] = t; }
-            const int t = col[r]; col[r] = col[pc]; col[pc] = t;
+            for (int i = 0; i < 5; ++i) { const double tt = q[9 * i + r]; q[9 * i + r] = q[9 * i + pc]; q[9 * i + pc] = tt; }
+            const int tt = col[r]; col[r] = col[pc]; col[pc] = tt;
         }
-        const double inv = 1.0 / q[r][r];
-        for (int j = 0; j < 9; ++j) q[r][j] *= inv;
+        const double inv = 1.0 / q[9 * r + r];
+        for (int j = 0; j < 9; ++j) q[9 * r + j] *= inv;
         for (int i = 0; i < 5; ++i) {
             if (i == r) continue;
-            const double f = q[i][r];
-            for (int j = 0; j < 9; ++j) q[i][j] -= f * q[r][j];
+            const double f = q[9 * i + r];
+            for (int j = 0; j < 9; ++j) q[9 * i + j] -= f * q[9 * r + j];
         }
     }
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
-        double v[9];
         for (int j = 0; j < 9; ++j) v[j] = 0.0;
         v[col[5 + k]] = 1.0;
-        for (int r = 0; r < 5; ++r) v[col[r]] = -q[r][5 + k];
+        for (int r = 0; r < 5; ++r) v[col[r]] = -q[9 * r + 5 + k];
         double nrm = 0.0;
+#pragma unroll
         for (int j = 0; j < 9; ++j) nrm += v[j] * v[j];
         nrm = sqrt(nrm);
+#pragma unroll
         for (int j = 0; j < 9; ++j) N[k][j] = v[j] / nrm;
     }
     return true;
 }
 
-// 5 correspondences (x1[i], x2[i]) -> up to 10 unit-norm E (row-major). Returns the count.
-__device__ int five_point(const double* x1, const double* x2, double* Es) {
-    double Q[5][9];
-    for (int i = 0; i < 5; ++i) {
-        const double u1 = x1[2 * i], v1 = x1[2 * i + 1], u2 = x2[2 * i], v2 = x2[2 * i + 1];
-        Q[i][0] = u2 * u1; Q[i][1] = u2 * v1; Q[i][2] = u2;
-        Q[i][3] = v2 * u1; Q[i][4] = v2 * v1; Q[i][5] = v2;
-        Q[i][6] = u1; Q[i][7] = v1; Q[i][8] = 1.0;
-    }
+__device__ __forceinline__ void addmul_ql_lds(const double* q, const double* l, double s, LaneArr<double> c) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += s * (q[i] * l[j]);
+}
+
+// 5 correspondences -> up to 10 unit-norm E; on_sol(s, E) is called for each solution in root order.
+template <typename SolFn>
+__device__ int five_point(const double* x1, const double* x2, SolverMem m, SolFn&& on_sol) {
     double N[4][9];
-    if (!nullspace_5x9(Q, N)) return 0;
+    if (!nullspace_5x9(x1, x2, m, N)) return 0;
     double E[9][4];
+#pragma unroll
     for (int e = 0; e < 9; ++e) {
         E[e][0] = N[0][e];
         E[e][1] = N[1][e];
         E[e][2] = N[2][e];
         E[e][3] = N[3][e];
     }
-    double A[10][20];
-    for (int r = 0; r < 10; ++r)
-        for (int c = 0; c < 20; ++c) A[r][c] = 0.0;
+    LaneArr<double> A = m.u;  // [10][20]
+    for (int k = 0; k < 200; ++k) A[k] = 0.0;
     {
         double q[10];
-        mul_ll(E[4], E[8], q); addmul_ql(q, E[0], 1.0, A[0]);
-        mul_ll(E[5], E[7], q); addmul_ql(q, E[0], -1.0, A[0]);
-        mul_ll(E[3], E[8], q); addmul_ql(q, E[1], -1.0, A[0]);
-        mul_ll(E[5], E[6], q); addmul_ql(q, E[1], 1.0, A[0]);
-        mul_ll(E[3], E[7], q); addmul_ql(q, E[2], 1.0, A[0]);
-        mul_ll(E[4], E[6], q); addmul_ql(q, E[2], -1.0, A[0]);
+        mul_ll(E[4], E[8], q); addmul_ql_lds(q, E[0], 1.0, A);
+        mul_ll(E[5], E[7], q); addmul_ql_lds(q, E[0], -1.0, A);
+        mul_ll(E[3], E[8], q); addmul_ql_lds(q, E[1], -1.0, A);
+        mul_ll(E[5], E[6], q); addmul_ql_lds(q, E[1], 1.0, A);
+        mul_ll(E[3], E[7], q); addmul_ql_lds(q, E[2], 1.0, A);
+        mul_ll(E[4], E[6], q); addmul_ql_lds(q, E[2], -1.0, A);
     }
     double EEt[3][3][10], tr[10], tmp[10];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = i; j < 3; ++j) {
-            for (int m = 0; m < 10; ++m) EEt[i][j][m] = 0.0;
+#pragma unroll
+            for (int mm = 0; mm < 10; ++mm) EEt[i][j][mm] = 0.0;
+#pragma unroll
             for (int k = 0; k < 3; ++k) {
                 mul_ll(E[3 * i + k], E[3 * j + k], tmp);
-                for (int m = 0; m < 10; ++m) EEt[i][j][m] += tmp[m];
+#pragma unroll
+                for (int mm = 0; mm < 10; ++mm) EEt[i][j][mm] += tmp[mm];
             }
             if (j != i)
-                for (int m = 0; m < 10; ++m) EEt[j][i][m] = EEt[i][j][m];
+#pragma unroll
+                for (int mm = 0; mm < 10; ++mm) EEt[j][i][mm] = EEt[i][j][mm];
         }
-    for (int m = 0; m < 10; ++m) tr[m] = EEt[0][0][m] + EEt[1][1][m] + EEt[2][2][m];
+#pragma unroll
+    for (int mm = 0; mm < 10; ++mm) tr[mm] = EEt[0][0][mm] + EEt[1][1][mm] + EEt[2][2][mm];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < 3; ++j) {
-            double* row = A[1 + 3 * i + j];
-            for (int k = 0; k < 3; ++k) addmul_ql(EEt[i][k], E[3 * k + j], 2.0, row);
-            addmul_ql(tr, E[3 * i + j], -1.0, row);
+            LaneArr<double> row = A.at(20 * (1 + 3 * i + j));
+#pragma unroll
+            for (int k = 0; k < 3; ++k) addmul_ql_lds(EEt[i][k], E[3 * k + j], 2.0, row);
+            addmul_ql_lds(tr, E[3 * i + j], -1.0, row);
         }
     for (int c = 0; c < 10; ++c) {
         int pr = c;
-        double best = fabs(A[c][c]);
+        double best = fabs(A[20 * c + c]);
         for (int r = c + 1; r < 10; ++r)
-            if (fabs(A[r][c]) > best) { best = fabs(A[r][c]); pr = r; }
+            if (fabs(A[20 * r + c]) > best) { best = fabs(A[20 * r + c]); pr = r; }
         if (best < 1e-14) return 0;
         if (pr != c)
-            for (int j = 0; j < 20; ++j) { const double t = A[c][j]; A[c][j] = A[pr][j]; A[pr][j] = t; }
-        const double inv = 1.0 / A[c][c];
-        for (int j = 0; j < 20; ++j) A[c][j] *= inv;
+            for (int j = 0; j < 20; ++j) { const double tt = A[20 * c + j]; A[20 * c + j] = A[20 * pr + j]; A[20 * pr + j] = tt; }
+        const double inv = 1.0 / A[20 * c + c];
+        for (int j = 0; j < 20; ++j) A[20 * c + j] *= inv;
         for (int r = 0; r < 10; ++r) {
             if (r == c) continue;
-            const double f = A[r][c];
-            for (int j = 0; j < 20; ++j) A[r][j] -= f * A[c][j];
+            const double f = A[20 * r + c];
+            for (int j = 0; j < 20; ++j) A[20 * r + j] -= f * A[20 * c + j];
         }
     }
     double B[3][3][5];
+#pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const double* e = A[4 + 2 * r];
-        const double* f = A[5 + 2 * r];
-        B[r][0][0] = e[12]; B[r][0][1] = e[11] - f[12]; B[r][0][2] = e[10] - f[11]; B[r][0][3] = -f[10]; B[r][0][4] = 0.0;
-        B[r][1][0] = e[15]; B[r][1][1] = e[14] - f[15]; B[r][1][2] = e[13] - f[14]; B[r][1][3] = -f[13]; B[r][1][4] = 0.0;
-        B[r][2][0] = e[19]; B[r][2][1] = e[18] - f[19]; B[r][2][2] = e[17] - f[18]; B[r][2][3] = e[16] - f[17];
-        B[r][2][4] = -f[16];
+        const int e = 20 * (4 + 2 * r), f = 20 * (5 + 2 * r);
+        B[r][0][0] = A[e + 12]; B[r][0][1] = A[e + 11] - A[f + 12]; B[r][0][2] = A[e + 10] - A[f + 11];
+        B[r][0][3] = -A[f + 10]; B[r][0][4] = 0.0;
+        B[r][1][0] = A[e + 15]; B[r][1][1] = A[e + 14] - A[f + 15]; B[r][1][2] = A[e + 13] - A[f + 14];
+        B[r][1][3] = -A[f + 13]; B[r][1][4] = 0.0;
+        B[r][2][0] = A[e + 19]; B[r][2][1] = A[e + 18] - A[f + 19]; B[r][2][2] = A[e + 17] - A[f + 18];
+        B[r][2][3] = A[e + 16] - A[f + 17]; B[r][2][4] = -A[f + 16];
     }
     double n[11];
+#pragma unroll
     for (int i = 0; i < 11; ++i) n[i] = 0.0;
     {
         const int deg[3] = {3, 3, 4};
+#pragma unroll
         for (int c = 0; c < 3; ++c) {
             const int c1 = (c + 1) % 3, c2 = (c + 2) % 3;
-            double m[9];
-            for (int i = 0; i < 9; ++i) m[i] = 0.0;
+            double mm[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) mm[i] = 0.0;
+#pragma unroll
             for (int i = 0; i <= deg[c1]; ++i)
-                for (int j = 0; j <= deg[c2]; ++j) m[i + j] += B[1][c1][i] * B[2][c2][j];
+#pragma unroll
+                for (int j = 0; j <= deg[c2]; ++j) mm[i + j] += B[1][c1][i] * B[2][c2][j];
+#pragma unroll
             for (int i = 0; i <= deg[c2]; ++i)
-                for (int j = 0; j <= deg[c1]; ++j) m[i + j] -= B[1][c2][i] * B[2][c1][j];
+#pragma unroll
+                for (int j = 0; j <= deg[c1]; ++j) mm[i + j] -= B[1][c2][i] * B[2][c1][j];
             const int dm = deg[c1] + deg[c2];
+#pragma unroll
             for (int i = 0; i <= deg[c]; ++i)
-                for (int j = 0; j <= dm; ++j) n[i + j] += B[0][c][i] * m[j];
+#pragma unroll
+                for (int j = 0; j <= dm; ++j) n[i + j] += B[0][c][i] * mm[j];
         }
     }
-    double roots[kMaxSol];
-    const int nroots = real_roots(n, 10, roots);
     int nsol = 0;
-    for (int k = 0; k < nroots; ++k) {
-        const double z = roots[k];
+    real_roots(n, 10, m, [&](double z) {
         double Bz[3][3];
+#pragma unroll
         for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) Bz[r][c] = peval(B[r][c], c == 2 ? 4 : 3, z);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int dg = c == 2 ? 4 : 3;
+                double v = B[r][c][dg];
+#pragma unroll
+                for (int i = dg - 1; i >= 0; --i) v = v * z + B[r][c][i];
+                Bz[r][c] = v;
+            }
         double bx = 0, by = 0, bzz = 0, bn = -1.0;
+#pragma unroll
         for (int a = 0; a < 3; ++a) {
             const int b = (a + 1) % 3;
             const double cx = Bz[a][1] * Bz[b][2] - Bz[a][2] * Bz[b][1];
@@ -322,19 +429,21 @@ __device__ int five_point(const double* x1, const double* x2, double* Es) {
             const double nn = cx * cx + cy * cy + cz * cz;
             if (nn > bn) { bn = nn; bx = cx; by = cy; bzz = cz; }
         }
-        if (!(fabs(bzz) > 1e-300)) continue;
+        if (!(fabs(bzz) > 1e-300)) return;
         const double x = bx / bzz, y = by / bzz;
-        double* Eo = Es + 9 * nsol;
-        double nrm = 0.0;
+        double Eo[9], nrm = 0.0;
+#pragma unroll
         for (int e = 0; e < 9; ++e) {
             Eo[e] = x * N[0][e] + y * N[1][e] + z * N[2][e] + N[3][e];
             nrm += Eo[e] * Eo[e];
         }
         nrm = sqrt(nrm);
-        if (!(nrm > 0.0)) continue;
+        if (!(nrm > 0.0)) return;
+#pragma unroll
         for (int e = 0; e < 9; ++e) Eo[e] /= nrm;
+        on_sol(nsol, Eo);
         ++nsol;
-    }
+    });
     return nsol;
 }
 
@@ -578,10 +687,6 @@ __global__ void normalize_putatives_kernel(const float* __restrict__ kp_xy, cons
     pts[o] = make_float4((float)n1.x, (float)n1.y, (float)n2.x, (float)n2.y);
 }
 
-__device__ __forceinline__ float readlane_f(float v, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
-
 struct RansacOutputs {
     double* E;       // [P][9]
     double* R;       // [P][9]
@@ -592,21 +697,121 @@ struct RansacOutputs {
     uint8_t* mask;   // [P][mcap]
 };
 
-__global__ __launch_bounds__(64) void ransac_hypotheses_kernel(const int* __restrict__ pairs, const double* __restrict__ intr,
-                                                      const int* __restrict__ match_count, int mcap,
-                                                      const double2* __restrict__ x1n_all,
-                                                      const double2* __restrict__ x2n_all,
-                                                      const float4* __restrict__ pts_all, double thr_px, double prob,
-                                                      int max_iters, uint64_t seed, int pair_id_base,
-                                                      RansacOutputs out, int4* __restrict__ best_out) {
-    __shared__ double bestE_sh[9];
-    __shared__ float cand[kBatch][kMaxSol * 9 + 1];  // candidates of the batch, one padded row per lane
-    __shared__ int nsol[kBatch];
+struct PairState {
+    int best, best_h, best_s, done;
+    int niters, pad0, pad1, pad2;
+    double bestE[9];
+    double pad3;
+};
+
+__global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int max_iters) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pairs) return;
+    PairState s{};
+    s.best = -1;
+    s.best_h = -1;
+    s.best_s = -1;
+    s.done = 0;
+    s.niters = max_iters;
+    st[p] = s;
+}
+
+// One 64-lane workgroup per active pair: lane l solves hypothesis done + l; candidates (fp64) -> global.
+__global__ __launch_bounds__(64, 1) void ransac_solve_kernel(const int* __restrict__ match_count, int mcap,
+                                                             const double2* __restrict__ x1n_all,
+                                                             const double2* __restrict__ x2n_all, uint64_t seed,
+                                                             int pair_id_base, const PairState* __restrict__ st,
+                                                             double* __restrict__ cand, int* __restrict__ nsol) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int M = match_count[p];
+    if (M < 6) return;
+    const int done = st[p].done;
+    if (done >= st[p].niters) return;
+    const double2* x1 = x1n_all + (size_t)p * mcap;
+    const double2* x2 = x2n_all + (size_t)p * mcap;
+    const SolverMem mem = solver_mem(smem, lane);
+    double* cout = cand + ((size_t)p * kBatch + lane) * (kMaxSol * 9);
+    int ns = 0;
+    int idx[5];
+    if (sample5(seed, pair_id_base + p, done + lane, M, idx)) {
+        double s1[10], s2[10];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const double2 a = x1[idx[k]], b = x2[idx[k]];
+            s1[2 * k] = a.x; s1[2 * k + 1] = a.y;
+            s2[2 * k] = b.x; s2[2 * k + 1] = b.y;
+        }
+        ns = five_point(s1, s2, mem, [&](int s, const double* E) {
+#pragma unroll
+            for (int e = 0; e < 9; ++e) cout[9 * s + e] = E[e];
+        });
+    }
+    nsol[(size_t)p * kBatch + lane] = ns;
+}
+
+// One wave per active pair: scores the batch's candidates in (hypothesis, solution) order, exact early exit,
+// keeps the first best, applies the OpenCV iteration bound after the batch.
+__global__ __launch_bounds__(64) void ransac_score_kernel(const int* __restrict__ pairs,
+                                                          const double* __restrict__ intr,
+                                                          const int* __restrict__ match_count, int mcap,
+                                                          const float4* __restrict__ pts_all, double thr_px,
+                                                          double prob, const double* __restrict__ cand,
+                                                          const int* __restrict__ nsol, PairState* __restrict__ st) {
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int M = match_count[p];
+    if (M < 6) return;
+    PairState s = st[p];
+    if (s.done >= s.niters) return;
+    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+    const double fx = fmax(intr[3 * i1], intr[3 * i2]);  // opencv_verifier_base.py:86
+    const double thr = thr_px / fx;
+    const float thr2 = (float)(thr * thr);
+    const float4* pts = pts_all + (size_t)p * mcap;
+    bool improved = false;
+    int imp_h = 0, imp_s = 0;
+    for (int hl = 0; hl < kBatch; ++hl) {
+        const int nsh = nsol[(size_t)p * kBatch + hl];
+        const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9);
+        for (int sI = 0; sI < nsh; ++sI) {
+            float E[9];
+#pragma unroll
+            for (int e = 0; e < 9; ++e) E[e] = (float)ch[9 * sI + e];
+            const int c = wave_count(E, pts, M, thr2, s.best, lane);
+            if (c > s.best) {
+                s.best = c;
+                s.best_h = s.done + hl;
+                s.best_s = sI;
+                improved = true;
+                imp_h = hl;
+                imp_s = sI;
+            }
+        }
+    }
+    if (improved) {
+        const double* ch = cand + ((size_t)p * kBatch + imp_h) * (kMaxSol * 9);
+        for (int e = 0; e < 9; ++e) s.bestE[e] = ch[9 * imp_s + e];
+    }
+    s.done += kBatch;
+    if (s.best > 0) {
+        const int upd = update_num_iters(prob, (double)(M - s.best) / M, 5, s.niters);
+        if (upd < s.niters) s.niters = upd;
+    }
+    if (lane == 0) st[p] = s;
+}
+
+// Per pair: status, iterative LO from the best hypothesis, final mask, recoverPose.
+__global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict__ pairs,
+                                                           const double* __restrict__ intr,
+                                                           const int* __restrict__ match_count, int mcap,
+                                                           const double2* __restrict__ x1n_all,
+                                                           const double2* __restrict__ x2n_all,
+                                                           const float4* __restrict__ pts_all, double thr_px,
+                                                           RansacOutputs out, const PairState* __restrict__ st) {
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     const int M = match_count[p];
     uint8_t* mask = out.mask + (size_t)p * mcap;
-    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
     if (M < 6) {  // opencv_verifier_base.py:69-78
         if (lane == 0) {
             out.n_inliers[p] = 0;
@@ -614,88 +819,19 @@ __global__ __launch_bounds__(64) void ransac_hypotheses_kernel(const int* __rest
             if (out.n_hyp) out.n_hyp[p] = 0;
         }
         for (int i = lane; i < M; i += 64) mask[i] = 0;
-        if (lane == 0) best_out[p] = make_int4(-1, -1, -1, 0);
         return;
     }
-    const double fx = fmax(intr[3 * i1], intr[3 * i2]);  // opencv_verifier_base.py:86
-    const double thr = thr_px / fx;
-    const float thr2 = (float)(thr * thr);
-    const double2* x1 = x1n_all + (size_t)p * mcap;
-    const double2* x2 = x2n_all + (size_t)p * mcap;
-    const float4* pts = pts_all + (size_t)p * mcap;
-    const int pair_id = pair_id_base + p;
-
-    int best = -1, best_h = -1, best_s = -1;
-    int niters = max_iters, done = 0;
-    while (done < niters) {
-        // lane-per-hypothesis minimal solves; candidates go to this lane's LDS row
-        int ns = 0;
-        {
-            const int h = done + lane;
-            int idx[5];
-            if (sample5(seed, pair_id, h, M, idx)) {
-                double s1[10], s2[10], Es[9 * kMaxSol];
-                for (int k = 0; k < 5; ++k) {
-                    const double2 a = x1[idx[k]], b = x2[idx[k]];
-                    s1[2 * k] = a.x; s1[2 * k + 1] = a.y;
-                    s2[2 * k] = b.x; s2[2 * k + 1] = b.y;
-                }
-                ns = five_point(s1, s2, Es);
-                for (int k = 0; k < 9 * ns; ++k) cand[lane][k] = (float)Es[k];
-            }
-            nsol[lane] = ns;
-        }
-        __syncthreads();
-        // wave-cooperative scoring of every candidate, in (hypothesis, solution) order
-        for (int hl = 0; hl < kBatch; ++hl) {
-            const int nsh = nsol[hl];
-            for (int s = 0; s < nsh; ++s) {
-                float E[9];
-#pragma unroll
-                for (int e = 0; e < 9; ++e) E[e] = cand[hl][9 * s + e];  // LDS broadcast
-                const int c = wave_count(E, pts, M, thr2, best, lane);
-                if (c > best) {
-                    best = c;
-                    best_h = done + hl;
-                    best_s = s;
-                }
-            }
-        }
-        __syncthreads();  // cand/nsol are rewritten by the next batch
-        done += kBatch;
-        if (best > 0) {
-            const int upd = update_num_iters(prob, (double)(M - best) / M, 5, niters);
-            if (upd < niters) niters = upd;
-        }
-    }
-    if (best <= 0) {
+    const PairState ps = st[p];
+    if (ps.best <= 0) {
         if (lane == 0) {
             out.n_inliers[p] = 0;
             out.status[p] = 2;
-            if (out.n_hyp) out.n_hyp[p] = done;
+            if (out.n_hyp) out.n_hyp[p] = ps.done;
         }
         for (int i = lane; i < M; i += 64) mask[i] = 0;
+        return;
     }
-    if (lane == 0) best_out[p] = make_int4(best, best_h, best_s, done);
-}
-
-// Refinement of each pair's winning hypothesis: fp64 re-solve, iterative LO, final mask, recoverPose.
-__global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict__ pairs,
-                                                           const double* __restrict__ intr,
-                                                           const int* __restrict__ match_count, int mcap,
-                                                           const double2* __restrict__ x1n_all,
-                                                           const double2* __restrict__ x2n_all,
-                                                           const float4* __restrict__ pts_all, double thr_px,
-                                                           uint64_t seed, int pair_id_base, RansacOutputs out,
-                                                           const int4* __restrict__ best_in) {
-    __shared__ double bestE_sh[9];
-    const int p = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int M = match_count[p];
-    const int4 bst = best_in[p];
-    if (M < 6 || bst.x <= 0) return;  // status already written by ransac_hypotheses_kernel
-    const int best_h = bst.y, best_s = bst.z, done = bst.w;
-    uint8_t* mask = out.mask + (size_t)p * mcap;
+    const int done = ps.done;
     const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
     const double fx = fmax(intr[3 * i1], intr[3 * i2]);
     const double thr = thr_px / fx;
@@ -703,25 +839,8 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
     const double2* x1 = x1n_all + (size_t)p * mcap;
     const double2* x2 = x2n_all + (size_t)p * mcap;
     const float4* pts = pts_all + (size_t)p * mcap;
-    const int pair_id = pair_id_base + p;
-
-    // re-solve the winning hypothesis in fp64 (deterministic) to recover its double-precision E
-    if (lane == 0) {
-        int idx[5];
-        sample5(seed, pair_id, best_h, M, idx);
-        double s1[10], s2[10], Es[9 * kMaxSol];
-        for (int k = 0; k < 5; ++k) {
-            const double2 a = x1[idx[k]], b = x2[idx[k]];
-            s1[2 * k] = a.x; s1[2 * k + 1] = a.y;
-            s2[2 * k] = b.x; s2[2 * k + 1] = b.y;
-        }
-        five_point(s1, s2, Es);
-        for (int e = 0; e < 9; ++e) bestE_sh[e] = Es[9 * best_s + e];
-    }
-    __syncthreads();
     double bestE[9];
-    for (int e = 0; e < 9; ++e) bestE[e] = bestE_sh[e];
-
+    for (int e = 0; e < 9; ++e) bestE[e] = ps.bestE[e];
     // iterative LO (oracle/ransac.c): thresholds kLoMult*thr -> thr, Sampson-weighted refits
     auto count_d = [&](const double* Ed) {
         float Ef[9];
@@ -809,11 +928,28 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
 
 extern "C" {
 
+static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_pts, size_t* off_st, size_t* off_cand,
+                            size_t* off_nsol) {
+    const size_t n = (size_t)n_pairs * mcap;
+    size_t o = 0;
+    o += gtsfm_align_up(n * sizeof(double2), 256);
+    *off_x2 = o;
+    o += gtsfm_align_up(n * sizeof(double2), 256);
+    *off_pts = o;
+    o += gtsfm_align_up(n * sizeof(float4), 256);
+    *off_st = o;
+    o += gtsfm_align_up((size_t)n_pairs * sizeof(PairState), 256);
+    *off_cand = o;
+    o += gtsfm_align_up((size_t)n_pairs * kBatch * kMaxSol * 9 * sizeof(double), 256);
+    *off_nsol = o;
+    o += gtsfm_align_up((size_t)n_pairs * kBatch * sizeof(int), 256);
+    return o;
+}
+
 size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap) {
     if (n_pairs <= 0 || mcap <= 0) return 0;
-    const size_t n = (size_t)n_pairs * mcap;
-    return gtsfm_align_up(n * sizeof(double2), 256) * 2 + gtsfm_align_up(n * sizeof(float4), 256) +
-           gtsfm_align_up((size_t)n_pairs * sizeof(int4), 256);
+    size_t a, b, c, d, e;
+    return ransac_layout(n_pairs, mcap, &a, &b, &c, &d, &e);
 }
 
 int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
@@ -827,22 +963,37 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
         !d_n_inliers || !d_status || !d_inlier_mask || n_img <= 0 || kmax <= 0 || n_pairs < 0 || mcap <= 0 ||
         max_iters <= 0 || !(thr_px > 0.0))
         return GTSFM_ERR_ARG;
-    if (workspace_bytes < gtsfm_ransac_workspace_bytes(n_pairs, mcap)) return GTSFM_ERR_CAPACITY;
+    size_t o_x2, o_pts, o_st, o_cand, o_nsol;
+    const size_t need = ransac_layout(n_pairs, mcap, &o_x2, &o_pts, &o_st, &o_cand, &o_nsol);
+    if (workspace_bytes < need) return GTSFM_ERR_CAPACITY;
     unsigned char* ws = (unsigned char*)d_workspace;
-    const size_t n = (size_t)n_pairs * mcap;
     double2* x1n = (double2*)ws;
-    double2* x2n = (double2*)(ws + gtsfm_align_up(n * sizeof(double2), 256));
-    float4* pts = (float4*)(ws + 2 * gtsfm_align_up(n * sizeof(double2), 256));
+    double2* x2n = (double2*)(ws + o_x2);
+    float4* pts = (float4*)(ws + o_pts);
+    PairState* st = (PairState*)(ws + o_st);
+    double* cand = (double*)(ws + o_cand);
+    int* nsol = (int*)(ws + o_nsol);
     hipLaunchKernelGGL(normalize_putatives_kernel, dim3((mcap + 255) / 256, n_pairs), dim3(256), 0, stream, d_kp_xy,
                        d_intrinsics, kmax, d_pairs, d_match_idx, d_match_count, mcap, x1n, x2n, pts);
+    hipLaunchKernelGGL(ransac_init_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, stream, st, n_pairs, max_iters);
     GTSFM_CHECK_HIP(hipGetLastError());
-    int4* best = (int4*)(ws + 2 * gtsfm_align_up(n * sizeof(double2), 256) + gtsfm_align_up(n * sizeof(float4), 256));
+    static bool lds_set = false;
+    if (!lds_set) {
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)ransac_solve_kernel,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSolveLds));
+        lds_set = true;
+    }
+    const int n_batches = (max_iters + kBatch - 1) / kBatch;
+    for (int b = 0; b < n_batches; ++b) {
+        hipLaunchKernelGGL(ransac_solve_kernel, dim3(n_pairs), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
+                           x2n, seed, pair_id_base, st, cand, nsol);
+        hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics,
+                           d_match_count, mcap, pts, thr_px, prob, cand, nsol, st);
+    }
+    GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask};
-    hipLaunchKernelGGL(ransac_hypotheses_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics,
-                       d_match_count, mcap, x1n, x2n, pts, thr_px, prob, max_iters, seed, pair_id_base, o, best);
-    GTSFM_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(ransac_refine_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics, d_match_count,
-                       mcap, x1n, x2n, pts, thr_px, seed, pair_id_base, o, best);
+                       mcap, x1n, x2n, pts, thr_px, o, st);
     GTSFM_CHECK_HIP(hipGetLastError());
     return GTSFM_OK;
 }
