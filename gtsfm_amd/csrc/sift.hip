@@ -132,13 +132,9 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 };
 
 // ------------------------------------------------------------------ kernels: pyramid
-__global__ void gray_upsample_kernel(const uint8_t* __restrict__ src, int C, int H, int W, float* __restrict__ up) {
-    const int W2 = 2 * W, H2 = 2 * H;
-    const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
-    const int b = blockIdx.z;
-    if (x >= W2) return;
-    const uint8_t* s = src + (size_t)b * H * W * C;
+// Octave-0 base sample: gray conversion (cv::cvtColor fixed point) + 2x INTER_LINEAR upsampling, evaluated on the fly
+// by the first blur (sift.py's cv2 path via gtsfm/frontend/detector_descriptor/sift.py:44-66).
+__device__ __forceinline__ float up_pixel(const uint8_t* __restrict__ s, int C, int H, int W, int y, int x) {
     auto gray = [&](int yy, int xx) -> float {
         const uint8_t* p = s + ((size_t)yy * W + xx) * C;
         if (C == 1) return (float)p[0];
@@ -158,54 +154,56 @@ __global__ void gray_upsample_kernel(const uint8_t* __restrict__ src, int C, int
     const int sx1 = sx + 1 < W ? sx + 1 : W - 1;
     const float r0 = gray(sy, sx) * (1.f - fx) + gray(sy, sx1) * fx;
     const float r1 = gray(sy1, sx) * (1.f - fx) + gray(sy1, sx1) * fx;
-    up[(size_t)b * H2 * W2 + (size_t)y * W2 + x] = r0 * (1.f - fy) + r1 * fy;
+    return r0 * (1.f - fy) + r1 * fy;
 }
 
-constexpr int kRowTile = 256;
+// Separable Gaussian (cv::GaussianBlur, BORDER_REFLECT_101: rows then columns) fused in one pass: the input tile
+// and its halo are staged once in LDS, the row pass writes an LDS buffer, the column pass writes the level.
+// kFromU8: the input is the upsampled gray image computed from the u8 source (octave 0, level 0).
+constexpr int kBlurTX = 64, kBlurTY = 32, kBlurTYT = 4;
 
-__global__ __launch_bounds__(kRowTile) void row_blur_kernel(const float* __restrict__ src, float* __restrict__ dst,
-                                                            int H, int W, Taps t) {
-    __shared__ float buf[kRowTile + 2 * kMaxR];
-    const int y = blockIdx.y, b = blockIdx.z, x0 = blockIdx.x * kRowTile, tid = threadIdx.x;
-    const float* s = src + (size_t)b * H * W + (size_t)y * W;
+__host__ __device__ constexpr size_t blur_lds_bytes(int r) {
+    return (size_t)((kBlurTY + 2 * r) * (kBlurTX + 2 * r) + (kBlurTY + 2 * r) * kBlurTX) * sizeof(float);
+}
+
+template <bool kFromU8>
+__global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* __restrict__ src,
+                                                                  const uint8_t* __restrict__ img8, int C, int H0,
+                                                                  int W0, float* __restrict__ dst, int H, int W,
+                                                                  Taps t) {
+    extern __shared__ float lds[];
     const int r = t.r;
-    for (int i = tid; i < kRowTile + 2 * r; i += kRowTile) buf[i] = s[reflect101(x0 - r + i, W)];
-    __syncthreads();
-    const int x = x0 + tid;
-    if (x >= W) return;
-    float acc = t.k[0] * buf[r + tid];
-    for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], buf[r + tid - j] + buf[r + tid + j], acc);
-    dst[(size_t)b * H * W + (size_t)y * W + x] = acc;
-}
-
-constexpr int kColTileX = 64, kColTileY = 64, kColThreadsY = 4;
-
-__global__ __launch_bounds__(kColTileX* kColThreadsY) void col_blur_kernel(const float* __restrict__ tmp,
-                                                                           float* __restrict__ dst,
-                                                                           const float* __restrict__ prev,
-                                                                           float* __restrict__ dog, int H, int W,
-                                                                           Taps t) {
-    __shared__ float tile[kColTileY + 2 * kMaxR][kColTileX];
+    const int IW = kBlurTX + 2 * r, IH = kBlurTY + 2 * r;
+    float* in = lds;             // IH x IW
+    float* rb = lds + IH * IW;   // IH x kBlurTX (row-blurred)
     const int tx = threadIdx.x, ty = threadIdx.y, b = blockIdx.z;
-    const int x0 = blockIdx.x * kColTileX, y0 = blockIdx.y * kColTileY;
-    const int r = t.r;
+    const int x0 = blockIdx.x * kBlurTX, y0 = blockIdx.y * kBlurTY;
     const size_t base = (size_t)b * H * W;
-    const int x = x0 + tx;
-    for (int i = ty; i < kColTileY + 2 * r; i += kColThreadsY) {
-        const int yy = reflect101(y0 - r + i, H);
-        tile[i][tx] = (x < W) ? tmp[base + (size_t)yy * W + x] : 0.f;
+    const uint8_t* s8 = kFromU8 ? img8 + (size_t)b * H0 * W0 * C : nullptr;
+    for (int iy = ty; iy < IH; iy += kBlurTYT) {
+        const int yy = reflect101(y0 - r + iy, H);
+        for (int ix = tx; ix < IW; ix += kBlurTX) {
+            const int xx = reflect101(x0 - r + ix, W);
+            in[iy * IW + ix] = kFromU8 ? up_pixel(s8, C, H0, W0, yy, xx) : src[base + (size_t)yy * W + xx];
+        }
     }
     __syncthreads();
+    for (int iy = ty; iy < IH; iy += kBlurTYT) {
+        const float* row = in + iy * IW + r + tx;
+        float acc = t.k[0] * row[0];
+        for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], row[-j] + row[j], acc);
+        rb[iy * kBlurTX + tx] = acc;
+    }
+    __syncthreads();
+    const int x = x0 + tx;
     if (x >= W) return;
-    for (int k = 0; k < kColTileY / kColThreadsY; ++k) {
-        const int ly = ty + kColThreadsY * k;
+    for (int ly = ty; ly < kBlurTY; ly += kBlurTYT) {
         const int y = y0 + ly;
         if (y >= H) break;
-        float acc = t.k[0] * tile[r + ly][tx];
-        for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], tile[r + ly - j][tx] + tile[r + ly + j][tx], acc);
-        const size_t o = base + (size_t)y * W + x;
-        dst[o] = acc;
-        if (dog) dog[o] = acc - prev[o];
+        const float* col = rb + (ly + r) * kBlurTX + tx;
+        float acc = t.k[0] * col[0];
+        for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], col[-j * kBlurTX] + col[j * kBlurTX], acc);
+        dst[base + (size_t)y * W + x] = acc;
     }
 }
 
@@ -217,38 +215,77 @@ __global__ void decimate_kernel(const float* __restrict__ src, int Hs, int Ws, f
 }
 
 // ------------------------------------------------------------------ kernels: detection
-struct DogSet {
-    const float* d[kDogs];
+struct GaussSet {
+    const float* g[kLevels];
 };
 
-__global__ void extrema_kernel(DogSet D, int H, int W, Cand* __restrict__ cands, int* __restrict__ n_cand, int cap) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    const int r = blockIdx.y;
-    const int img = blockIdx.z / kLayers, layer = blockIdx.z % kLayers + 1;
-    if (c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) return;
-    const size_t base = (size_t)img * H * W;
-    const float* cur = D.d[layer] + base;
-    const float val = cur[(size_t)r * W + c];
-    const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
-    if (!(fabsf(val) > threshold)) return;
-    const float* prv = D.d[layer - 1] + base;
-    const float* nxt = D.d[layer + 1] + base;
-    bool ismax = val > 0, ismin = val < 0;
-    for (int dy = -1; dy <= 1; ++dy)
-        for (int dx = -1; dx <= 1; ++dx) {
-            const size_t o = (size_t)(r + dy) * W + (c + dx);
-            const float a = prv[o], bb = nxt[o], m = cur[o];
-            if (ismax && !(val >= a && val >= bb && val >= m)) ismax = false;
-            if (ismin && !(val <= a && val <= bb && val <= m)) ismin = false;
+// DoG levels are never stored: DoG_l = G_{l+1} - G_l is recomputed from the Gaussian levels (the same fp32
+// subtraction cv::subtract performs), which removes 5 level writes per octave.
+constexpr int kExTX = 64, kExTY = 16, kExTYT = 4;
+
+__global__ __launch_bounds__(kExTX* kExTYT) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
+                                                                int* __restrict__ n_cand, int cap) {
+    __shared__ float D[kDogs][kExTY + 2][kExTX + 2];
+    __shared__ Cand list[kExTX * kExTY * kLayers / 4];
+    __shared__ int n_list, gbase;
+    const int tx = threadIdx.x, ty = threadIdx.y, b = blockIdx.z;
+    const int x0 = blockIdx.x * kExTX, y0 = blockIdx.y * kExTY;
+    const size_t base = (size_t)b * H * W;
+    if (tx == 0 && ty == 0) n_list = 0;
+    for (int iy = ty; iy < kExTY + 2; iy += kExTYT)
+        for (int ix = tx; ix < kExTX + 2; ix += kExTX) {
+            const int y = min(max(y0 - 1 + iy, 0), H - 1), x = min(max(x0 - 1 + ix, 0), W - 1);
+            const size_t o = base + (size_t)y * W + x;
+            float g0 = G.g[0][o];
+#pragma unroll
+            for (int l = 0; l < kDogs; ++l) {
+                const float g1 = G.g[l + 1][o];
+                D[l][iy][ix] = g1 - g0;
+                g0 = g1;
+            }
         }
-    if (!ismax && !ismin) return;
-    const int slot = atomicAdd(n_cand, 1);
-    if (slot < cap) cands[slot] = Cand{img, layer, r, c};
+    __syncthreads();
+    const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
+    const int c = x0 + tx;
+    for (int ly = ty; ly < kExTY; ly += kExTYT) {
+        const int r = y0 + ly;
+        if (c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) continue;
+#pragma unroll
+        for (int layer = 1; layer <= kLayers; ++layer) {
+            const float val = D[layer][ly + 1][tx + 1];
+            if (!(fabsf(val) > threshold)) continue;
+            bool ismax = val > 0, ismin = val < 0;
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    const float a = D[layer - 1][ly + dy][tx + dx], bb = D[layer + 1][ly + dy][tx + dx],
+                                m = D[layer][ly + dy][tx + dx];
+                    if (ismax && !(val >= a && val >= bb && val >= m)) ismax = false;
+                    if (ismin && !(val <= a && val <= bb && val <= m)) ismin = false;
+                }
+            if (!ismax && !ismin) continue;
+            const int slot = atomicAdd(&n_list, 1);
+            if (slot < (int)(sizeof(list) / sizeof(Cand))) {
+                list[slot] = Cand{b, layer, r, c};
+            } else {  // plateau-heavy tile: spill straight to the global list
+                const int g = atomicAdd(n_cand, 1);
+                if (g < cap) cands[g] = Cand{b, layer, r, c};
+            }
+        }
+    }
+    __syncthreads();
+    const int n = min(n_list, (int)(sizeof(list) / sizeof(Cand)));
+    const int t = ty * kExTX + tx;
+    if (t == 0) gbase = n ? atomicAdd(n_cand, n) : 0;
+    __syncthreads();
+    for (int i = t; i < n; i += kExTX * kExTYT)
+        if (gbase + i < cap) cands[gbase + i] = list[i];
 }
 
-#define DAT(p, r, c) ((p)[(size_t)(r) * W + (c)])
+#define DAT(l, r, c) (G.g[(l) + 1][base + (size_t)(r) * W + (c)] - G.g[(l)][base + (size_t)(r) * W + (c)])
 
-__global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restrict__ n_cand_p, int cap, DogSet D, int H,
+__global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restrict__ n_cand_p, int cap, GaussSet G, int H,
                               int W, int n_img, uint32_t* __restrict__ seen, Refined* __restrict__ out,
                               int* __restrict__ n_out, int out_cap) {
     const int n_cand = min(*n_cand_p, cap);
@@ -262,9 +299,7 @@ __global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restr
         int i = 0;
         bool ok = true;
         for (; i < kMaxInterp; i++) {
-            const float* img = D.d[layer] + base;
-            const float* prev = D.d[layer - 1] + base;
-            const float* next = D.d[layer + 1] + base;
+            const int img = layer, prev = layer - 1, next = layer + 1;
             const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
             const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
             const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
@@ -306,9 +341,7 @@ __global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restr
             }
         }
         if (!ok || i >= kMaxInterp) continue;
-        const float* img = D.d[layer] + base;
-        const float* prev = D.d[layer - 1] + base;
-        const float* next = D.d[layer + 1] + base;
+        const int img = layer, prev = layer - 1, next = layer + 1;
         const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
         const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
         const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
@@ -331,10 +364,6 @@ __global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restr
         if (slot < out_cap) out[slot] = Refined{cd.img, layer, r, c, xc, xr, xi, contr};
     }
 }
-
-struct GaussSet {
-    const float* g[kLevels];
-};
 
 // One wave per refined location: orientation histogram (fixed point, LDS u64 atomics), peaks -> keypoints.
 __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restrict__ refs,
@@ -681,8 +710,8 @@ constexpr int kKpCapPerImg = 1 << 16;
 struct Layout {
     int B, H, W, n_oct, max_kpts;
     int Ho[kMaxOct], Wo[kMaxOct];
-    size_t g[kMaxOct][kLevels], dg[kMaxOct][kDogs];  // byte offsets
-    size_t up, tmp, seen, seen_bytes, cand, ref, kps, kp_counts, counters, sel, n_sel, total;
+    size_t g[kMaxOct][kLevels];  // byte offsets
+    size_t seen, seen_bytes, cand, ref, kps, kp_counts, counters, sel, n_sel, total;
 };
 
 int num_octaves(int H, int W) {
@@ -710,13 +739,9 @@ Layout make_layout(int B, int H, int W, int max_kpts) {
         L.Wo[o] = w;
         const size_t lvl = (size_t)B * h * w * sizeof(float);
         for (int i = 0; i < kLevels; ++i) L.g[o][i] = take(lvl);
-        for (int i = 0; i < kDogs; ++i) L.dg[o][i] = take(lvl);
         h /= 2;
         w /= 2;
     }
-    const size_t lvl0 = (size_t)B * (2 * H) * (2 * W) * sizeof(float);
-    L.up = take(lvl0);
-    L.tmp = take(lvl0);
     L.seen_bytes = gtsfm_align_up(((size_t)B * kLayers * (2 * H) * (2 * W) + 31) / 32 * 4, 256);
     L.seen = take(L.seen_bytes);
     L.cand = take((size_t)B * kCandCapPerImg * sizeof(Cand));
@@ -776,39 +801,45 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
     GTSFM_CHECK_HIP(hipMemsetAsync(d_attr, 0, (size_t)B * max_kpts * 3 * sizeof(float), stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(d_desc, 0, (size_t)B * max_kpts * 128 * sizeof(float), stream));
 
-    auto blur = [&](const float* src, float* dst, const float* prev, float* dog, int h, int w, const Taps& t) {
-        hipLaunchKernelGGL(row_blur_kernel, dim3((w + kRowTile - 1) / kRowTile, h, B), dim3(kRowTile), 0, stream, src,
-                           F(L.tmp), h, w, t);
-        hipLaunchKernelGGL(col_blur_kernel, dim3((w + kColTileX - 1) / kColTileX, (h + kColTileY - 1) / kColTileY, B),
-                           dim3(kColTileX, kColThreadsY), 0, stream, F(L.tmp), dst, prev, dog, h, w, t);
+    static bool lds_set = false;
+    if (!lds_set) {
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)blur2d_kernel<false>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)blur_lds_bytes(kMaxR)));
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)blur2d_kernel<true>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)blur_lds_bytes(kMaxR)));
+        lds_set = true;
+    }
+    auto blur = [&](const float* src, float* dst, int h, int w, const Taps& t) {
+        const dim3 grid((w + kBlurTX - 1) / kBlurTX, (h + kBlurTY - 1) / kBlurTY, B);
+        if (src)
+            hipLaunchKernelGGL(blur2d_kernel<false>, grid, dim3(kBlurTX, kBlurTYT), blur_lds_bytes(t.r), stream, src,
+                               nullptr, 0, 0, 0, dst, h, w, t);
+        else
+            hipLaunchKernelGGL(blur2d_kernel<true>, grid, dim3(kBlurTX, kBlurTYT), blur_lds_bytes(t.r), stream,
+                               nullptr, d_images, channels, H, W, dst, h, w, t);
     };
-    hipLaunchKernelGGL(gray_upsample_kernel, dim3((2 * W + 255) / 256, 2 * H, B), dim3(256), 0, stream, d_images,
-                       channels, H, W, F(L.up));
-    GTSFM_CHECK_HIP(hipGetLastError());
     for (int o = 0; o < L.n_oct; ++o) {
         const int h = L.Ho[o], w = L.Wo[o];
         if (o == 0) {
-            blur(F(L.up), F(L.g[0][0]), nullptr, nullptr, h, w, taps[0]);
+            blur(nullptr, F(L.g[0][0]), h, w, taps[0]);
         } else {
             hipLaunchKernelGGL(decimate_kernel, dim3((w + 255) / 256, h, B), dim3(256), 0, stream,
                                F(L.g[o - 1][kLayers]), L.Ho[o - 1], L.Wo[o - 1], F(L.g[o][0]), h, w);
         }
-        for (int i = 1; i < kLevels; ++i) blur(F(L.g[o][i - 1]), F(L.g[o][i]), F(L.g[o][i - 1]), F(L.dg[o][i - 1]), h, w,
-                                               taps[i]);
+        for (int i = 1; i < kLevels; ++i) blur(F(L.g[o][i - 1]), F(L.g[o][i]), h, w, taps[i]);
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
         GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, 16, stream));
         GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.seen, 0,
                                        gtsfm_align_up(((size_t)B * kLayers * h * w + 31) / 32 * 4, 4), stream));
-        DogSet D;
-        for (int i = 0; i < kDogs; ++i) D.d[i] = F(L.dg[o][i]);
-        hipLaunchKernelGGL(extrema_kernel, dim3((w + 255) / 256, h, B * kLayers), dim3(256), 0, stream, D, h, w,
-                           (Cand*)(ws + L.cand), counters + 0, B * kCandCapPerImg);
-        hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters + 0,
-                           B * kCandCapPerImg, D, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
-                           counters + 1, B * kCandCapPerImg);
         GaussSet G;
         for (int i = 0; i < kLevels; ++i) G.g[i] = F(L.g[o][i]);
+        hipLaunchKernelGGL(extrema_kernel, dim3((w + kExTX - 1) / kExTX, (h + kExTY - 1) / kExTY, B),
+                           dim3(kExTX, kExTYT), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters + 0,
+                           B * kCandCapPerImg);
+        hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters + 0,
+                           B * kCandCapPerImg, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
+                           counters + 1, B * kCandCapPerImg);
         hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),
                            counters + 1, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps), kp_counts,
                            kKpCapPerImg);
