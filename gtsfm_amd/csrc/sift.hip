@@ -133,13 +133,34 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 
 // ------------------------------------------------------------------ kernels: pyramid
 // Octave-0 base sample: gray conversion (cv::cvtColor fixed point) + 2x INTER_LINEAR upsampling, evaluated on the fly
-// by the first blur (sift.py's cv2 path via gtsfm/frontend/detector_descriptor/sift.py:44-66).
-__device__ __forceinline__ float up_pixel(const uint8_t* __restrict__ s, int C, int H, int W, int y, int x) {
-    auto gray = [&](int yy, int xx) -> float {
-        const uint8_t* p = s + ((size_t)yy * W + xx) * C;
-        if (C == 1) return (float)p[0];
-        return (float)((p[0] * 4899 + p[1] * 9617 + p[2] * 1868 + (1 << 13)) >> 14);
-    };
+// by the first blur (gtsfm/frontend/detector_descriptor/sift.py:44-66 -> cv2 SIFT_create().detectAndCompute).
+// Separable Gaussian (cv::GaussianBlur, BORDER_REFLECT_101: rows then columns) fused in one pass: the input tile
+// and its halo are staged once in LDS, the row pass (4 outputs per thread from ds_read_b128 windows) writes an LDS
+// buffer, the column pass (8 outputs per thread from one register window) writes the level. Every output is the
+// same fmaf chain as the oracle (acc = k0*c; acc = fmaf(kj, l + r, acc)), so the pyramid stays bit-exact.
+// kFromU8: the input is the 2x-upsampled gray image, computed from a gray tile of the u8 source staged in LDS.
+// Tiles are mapped XCD-contiguously (consecutive workgroups land on different XCDs; each XCD gets a contiguous run
+// of tiles so halos are shared through its own L2).
+constexpr int kBlurTX = 64, kBlurTY = 32, kBlurTYT = 4, kBlurColRows = kBlurTY / kBlurTYT;
+constexpr int kBlurMaxR = 16;
+
+__host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 3 + 3) / 4 * 4; }
+__host__ __device__ constexpr int blur_gh(int r) { return (kBlurTY + 2 * r) / 2 + 4; }
+__host__ __device__ constexpr int blur_gw(int r) { return (kBlurTX + 2 * r) / 2 + 4; }
+__host__ __device__ constexpr size_t blur_lds_bytes(int r, bool u8) {
+    return (size_t)((kBlurTY + 2 * r) * blur_iwp(r) + (kBlurTY + 2 * r) * kBlurTX + (u8 ? blur_gh(r) * blur_gw(r) : 0)) *
+           sizeof(float);
+}
+
+__device__ __forceinline__ float gray_at(const uint8_t* __restrict__ s, int C, int W, int yy, int xx) {
+    const uint8_t* p = s + ((size_t)yy * W + xx) * C;
+    if (C == 1) return (float)p[0];
+    return (float)((p[0] * 4899 + p[1] * 9617 + p[2] * 1868 + (1 << 13)) >> 14);
+}
+
+// up_pixel with the gray samples read from an LDS tile whose origin is (gy0, gx0)
+__device__ __forceinline__ float up_pixel_lds(const float* __restrict__ g, int gw, int gy0, int gx0, int H, int W, int y,
+                                              int x) {
     float fy = (float)((y + 0.5) * 0.5 - 0.5);
     int sy = (int)floorf(fy);
     fy -= sy;
@@ -152,60 +173,147 @@ __device__ __forceinline__ float up_pixel(const uint8_t* __restrict__ s, int C, 
     if (sx < 0) { sx = 0; fx = 0; }
     if (sx >= W - 1) { sx = W - 1; fx = 0; }
     const int sx1 = sx + 1 < W ? sx + 1 : W - 1;
-    const float r0 = gray(sy, sx) * (1.f - fx) + gray(sy, sx1) * fx;
-    const float r1 = gray(sy1, sx) * (1.f - fx) + gray(sy1, sx1) * fx;
+    const float* r0p = g + (sy - gy0) * gw;
+    const float* r1p = g + (sy1 - gy0) * gw;
+    const float r0 = r0p[sx - gx0] * (1.f - fx) + r0p[sx1 - gx0] * fx;
+    const float r1 = r1p[sx - gx0] * (1.f - fx) + r1p[sx1 - gx0] * fx;
     return r0 * (1.f - fy) + r1 * fy;
 }
 
-// Separable Gaussian (cv::GaussianBlur, BORDER_REFLECT_101: rows then columns) fused in one pass: the input tile
-// and its halo are staged once in LDS, the row pass writes an LDS buffer, the column pass writes the level.
-// kFromU8: the input is the upsampled gray image computed from the u8 source (octave 0, level 0).
-constexpr int kBlurTX = 64, kBlurTY = 32, kBlurTYT = 4;
-
-__host__ __device__ constexpr size_t blur_lds_bytes(int r) {
-    return (size_t)((kBlurTY + 2 * r) * (kBlurTX + 2 * r) + (kBlurTY + 2 * r) * kBlurTX) * sizeof(float);
-}
-
-template <bool kFromU8>
+template <int R, bool kFromU8>
 __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* __restrict__ src,
                                                                   const uint8_t* __restrict__ img8, int C, int H0,
                                                                   int W0, float* __restrict__ dst, int H, int W,
-                                                                  Taps t) {
-    extern __shared__ float lds[];
-    const int r = t.r;
-    const int IW = kBlurTX + 2 * r, IH = kBlurTY + 2 * r;
-    float* in = lds;             // IH x IW
-    float* rb = lds + IH * IW;   // IH x kBlurTX (row-blurred)
-    const int tx = threadIdx.x, ty = threadIdx.y, b = blockIdx.z;
-    const int x0 = blockIdx.x * kBlurTX, y0 = blockIdx.y * kBlurTY;
+                                                                  int n_tx, int n_ty, int n_img, Taps t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int IW = kBlurTX + 2 * R, IH = kBlurTY + 2 * R, IWP = blur_iwp(R);
+    constexpr int NV = (4 + 2 * R + 3) / 4;  // float4 words per row-pass window
+    float* in = lds;                          // IH x IWP
+    float* rb = lds + IH * IWP;               // IH x kBlurTX (row-blurred)
+    const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * kBlurTX + tx;
+    // XCD-contiguous tile order
+    const int total = n_tx * n_ty * n_img;
+    const int per_xcd = (total + 7) / 8;
+    const int tile = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    if (tile >= total) return;
+    const int b = tile / (n_tx * n_ty);
+    const int rem = tile - b * n_tx * n_ty;
+    const int x0 = (rem % n_tx) * kBlurTX, y0 = (rem / n_tx) * kBlurTY;
     const size_t base = (size_t)b * H * W;
-    const uint8_t* s8 = kFromU8 ? img8 + (size_t)b * H0 * W0 * C : nullptr;
-    for (int iy = ty; iy < IH; iy += kBlurTYT) {
-        const int yy = reflect101(y0 - r + iy, H);
-        for (int ix = tx; ix < IW; ix += kBlurTX) {
-            const int xx = reflect101(x0 - r + ix, W);
-            in[iy * IW + ix] = kFromU8 ? up_pixel(s8, C, H0, W0, yy, xx) : src[base + (size_t)yy * W + xx];
+    float k[R + 1];
+#pragma unroll
+    for (int j = 0; j <= R; ++j) k[j] = t.k[j];
+    int xx[(IW + kBlurTX - 1) / kBlurTX];
+#pragma unroll
+    for (int q = 0; q < (IW + kBlurTX - 1) / kBlurTX; ++q) xx[q] = reflect101(x0 - R + tx + q * kBlurTX, W);
+    if constexpr (kFromU8) {
+        float* g = rb + IH * kBlurTX;
+        constexpr int GW = blur_gw(R);
+        const int ylo = max(y0 - R, 0), yhi = min(y0 + kBlurTY + R, H) - 1;
+        const int xlo = max(x0 - R, 0), xhi = min(x0 + kBlurTX + R, W) - 1;
+        const int gy0 = max((ylo - 1) / 2, 0), gy1 = min(yhi / 2 + 1, H0 - 1);
+        const int gx0 = max((xlo - 1) / 2, 0), gx1 = min(xhi / 2 + 1, W0 - 1);
+        const uint8_t* s8 = img8 + (size_t)b * H0 * W0 * C;
+        {
+            constexpr int NGR = (blur_gh(R) + kBlurTYT - 1) / kBlurTYT;
+            float gv[NGR];
+            const int gx = gx0 + tx;
+#pragma unroll
+            for (int i = 0; i < NGR; ++i) {
+                const int gy = gy0 + ty + i * kBlurTYT;
+                gv[i] = (gy <= gy1 && gx <= gx1) ? gray_at(s8, C, W0, gy, gx) : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < NGR; ++i) {
+                const int gy = gy0 + ty + i * kBlurTYT;
+                if (gy <= gy1 && gx <= gx1) g[(gy - gy0) * GW + tx] = gv[i];
+            }
+        }
+        __syncthreads();
+        for (int iy = ty; iy < IH; iy += kBlurTYT) {
+            const int yy = reflect101(y0 - R + iy, H);
+#pragma unroll
+            for (int q = 0; q < (IW + kBlurTX - 1) / kBlurTX; ++q) {
+                const int ix = tx + q * kBlurTX;
+                if (ix < IW) in[iy * IWP + ix] = up_pixel_lds(g, GW, gy0, gx0, H0, W0, yy, xx[q]);
+            }
+        }
+    } else {
+        // every load of the tile issued before any LDS store (memory-level parallelism)
+        constexpr int NR = (IH + kBlurTYT - 1) / kBlurTYT, NQ = (IW + kBlurTX - 1) / kBlurTX;
+        float v[NR][NQ];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const int iy = ty + i * kBlurTYT;
+            const float* srow = src + base + (size_t)reflect101(min(y0 - R + iy, y0 + IH - 1 - R), H) * W;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) v[i][q] = (iy < IH && tx + q * kBlurTX < IW) ? srow[xx[q]] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+            const int iy = ty + i * kBlurTYT;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                if (iy < IH && tx + q * kBlurTX < IW) in[iy * IWP + tx + q * kBlurTX] = v[i][q];
         }
     }
     __syncthreads();
-    for (int iy = ty; iy < IH; iy += kBlurTYT) {
-        const float* row = in + iy * IW + r + tx;
-        float acc = t.k[0] * row[0];
-        for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], row[-j] + row[j], acc);
-        rb[iy * kBlurTX + tx] = acc;
+    // row pass: 16 threads per row, 4 consecutive outputs each
+    for (int iy = tid >> 4; iy < IH; iy += kBlurTX * kBlurTYT / 16) {
+        const int g4 = (tid & 15) * 4;
+        const float4* wp = (const float4*)(in + iy * IWP + g4);
+        float v[4 * NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const float4 w4 = wp[q];
+            v[4 * q] = w4.x; v[4 * q + 1] = w4.y; v[4 * q + 2] = w4.z; v[4 * q + 3] = w4.w;
+        }
+        float o[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float acc = k[0] * v[R + q];
+#pragma unroll
+            for (int j = 1; j <= R; ++j) acc = fmaf(k[j], v[R + q - j] + v[R + q + j], acc);
+            o[q] = acc;
+        }
+        *(float4*)(rb + iy * kBlurTX + g4) = make_float4(o[0], o[1], o[2], o[3]);
     }
     __syncthreads();
+    // column pass: kBlurColRows consecutive outputs per thread
     const int x = x0 + tx;
     if (x >= W) return;
-    for (int ly = ty; ly < kBlurTY; ly += kBlurTYT) {
-        const int y = y0 + ly;
-        if (y >= H) break;
-        const float* col = rb + (ly + r) * kBlurTX + tx;
-        float acc = t.k[0] * col[0];
-        for (int j = 1; j <= r; ++j) acc = fmaf(t.k[j], col[-j * kBlurTX] + col[j * kBlurTX], acc);
-        dst[base + (size_t)y * W + x] = acc;
+    const int ly0 = ty * kBlurColRows;
+    float c[kBlurColRows + 2 * R];
+#pragma unroll
+    for (int i = 0; i < kBlurColRows + 2 * R; ++i) c[i] = rb[(ly0 + i) * kBlurTX + tx];
+#pragma unroll
+    for (int q = 0; q < kBlurColRows; ++q) {
+        const int y = y0 + ly0 + q;
+        float acc = k[0] * c[R + q];
+#pragma unroll
+        for (int j = 1; j <= R; ++j) acc = fmaf(k[j], c[R + q - j] + c[R + q + j], acc);
+        if (y < H) dst[base + (size_t)y * W + x] = acc;
     }
 }
+
+template <bool kFromU8>
+struct BlurTable {
+    using Fn = void (*)(const float*, const uint8_t*, int, int, int, float*, int, int, int, int, int, Taps);
+    static Fn get(int r) {
+        switch (r) {
+#define GTSFM_BLUR_CASE(RR) \
+    case RR:                \
+        return blur2d_kernel<RR, kFromU8>;
+            GTSFM_BLUR_CASE(1) GTSFM_BLUR_CASE(2) GTSFM_BLUR_CASE(3) GTSFM_BLUR_CASE(4) GTSFM_BLUR_CASE(5)
+            GTSFM_BLUR_CASE(6) GTSFM_BLUR_CASE(7) GTSFM_BLUR_CASE(8) GTSFM_BLUR_CASE(9) GTSFM_BLUR_CASE(10)
+            GTSFM_BLUR_CASE(11) GTSFM_BLUR_CASE(12) GTSFM_BLUR_CASE(13) GTSFM_BLUR_CASE(14) GTSFM_BLUR_CASE(15)
+            GTSFM_BLUR_CASE(16)
+#undef GTSFM_BLUR_CASE
+            default:
+                return nullptr;
+        }
+    }
+};
 
 __global__ void decimate_kernel(const float* __restrict__ src, int Hs, int Ws, float* __restrict__ dst, int H,
                                 int W) {
@@ -232,18 +340,30 @@ __global__ __launch_bounds__(kExTX* kExTYT) void extrema_kernel(GaussSet G, int 
     const int x0 = blockIdx.x * kExTX, y0 = blockIdx.y * kExTY;
     const size_t base = (size_t)b * H * W;
     if (tx == 0 && ty == 0) n_list = 0;
-    for (int iy = ty; iy < kExTY + 2; iy += kExTYT)
-        for (int ix = tx; ix < kExTX + 2; ix += kExTX) {
-            const int y = min(max(y0 - 1 + iy, 0), H - 1), x = min(max(x0 - 1 + ix, 0), W - 1);
-            const size_t o = base + (size_t)y * W + x;
-            float g0 = G.g[0][o];
+    {
+        constexpr int NR = (kExTY + 2 + kExTYT - 1) / kExTYT, NQ = 2;
+        float v[NR][NQ][kLevels];
 #pragma unroll
-            for (int l = 0; l < kDogs; ++l) {
-                const float g1 = G.g[l + 1][o];
-                D[l][iy][ix] = g1 - g0;
-                g0 = g1;
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int iy = ty + i * kExTYT, ix = tx + q * kExTX;
+                const int y = min(max(y0 - 1 + iy, 0), H - 1), x = min(max(x0 - 1 + ix, 0), W - 1);
+                const size_t o = base + (size_t)y * W + x;
+                const bool ok = iy < kExTY + 2 && ix < kExTX + 2;
+#pragma unroll
+                for (int l = 0; l < kLevels; ++l) v[i][q][l] = ok ? G.g[l][o] : 0.f;
             }
-        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i)
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                const int iy = ty + i * kExTYT, ix = tx + q * kExTX;
+                if (iy < kExTY + 2 && ix < kExTX + 2)
+#pragma unroll
+                    for (int l = 0; l < kDogs; ++l) D[l][iy][ix] = v[i][q][l + 1] - v[i][q][l];
+            }
+    }
     __syncthreads();
     const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
     const int c = x0 + tx;
@@ -801,32 +921,37 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
     GTSFM_CHECK_HIP(hipMemsetAsync(d_attr, 0, (size_t)B * max_kpts * 3 * sizeof(float), stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(d_desc, 0, (size_t)B * max_kpts * 128 * sizeof(float), stream));
 
-    static bool lds_set = false;
-    if (!lds_set) {
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)blur2d_kernel<false>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)blur_lds_bytes(kMaxR)));
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)blur2d_kernel<true>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)blur_lds_bytes(kMaxR)));
-        lds_set = true;
-    }
-    auto blur = [&](const float* src, float* dst, int h, int w, const Taps& t) {
-        const dim3 grid((w + kBlurTX - 1) / kBlurTX, (h + kBlurTY - 1) / kBlurTY, B);
-        if (src)
-            hipLaunchKernelGGL(blur2d_kernel<false>, grid, dim3(kBlurTX, kBlurTYT), blur_lds_bytes(t.r), stream, src,
-                               nullptr, 0, 0, 0, dst, h, w, t);
+    for (int i = 0; i < kLevels; ++i)
+        if (taps[i].r < 1 || taps[i].r > kBlurMaxR) return GTSFM_ERR_ARG;
+    auto blur = [&](const float* src, float* dst, int h, int w, const Taps& t) -> int {
+        const int n_tx = (w + kBlurTX - 1) / kBlurTX, n_ty = (h + kBlurTY - 1) / kBlurTY;
+        const int total = n_tx * n_ty * B;
+        const dim3 grid((unsigned)((total + 7) / 8 * 8));
+        const bool u8 = src == nullptr;
+        const void* fn = u8 ? (const void*)BlurTable<true>::get(t.r) : (const void*)BlurTable<false>::get(t.r);
+        const size_t lds = blur_lds_bytes(t.r, u8);
+        if (lds > 65536) {
+            const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+            if (e != hipSuccess) return GTSFM_ERR_HIP;
+        }
+        if (u8)
+            hipLaunchKernelGGL(BlurTable<true>::get(t.r), grid, dim3(kBlurTX, kBlurTYT), lds, stream, nullptr,
+                               d_images, channels, H, W, dst, h, w, n_tx, n_ty, B, t);
         else
-            hipLaunchKernelGGL(blur2d_kernel<true>, grid, dim3(kBlurTX, kBlurTYT), blur_lds_bytes(t.r), stream,
-                               nullptr, d_images, channels, H, W, dst, h, w, t);
+            hipLaunchKernelGGL(BlurTable<false>::get(t.r), grid, dim3(kBlurTX, kBlurTYT), lds, stream, src, nullptr, 0,
+                               0, 0, dst, h, w, n_tx, n_ty, B, t);
+        return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
     };
     for (int o = 0; o < L.n_oct; ++o) {
         const int h = L.Ho[o], w = L.Wo[o];
         if (o == 0) {
-            blur(nullptr, F(L.g[0][0]), h, w, taps[0]);
+            if (blur(nullptr, F(L.g[0][0]), h, w, taps[0])) return GTSFM_ERR_HIP;
         } else {
             hipLaunchKernelGGL(decimate_kernel, dim3((w + 255) / 256, h, B), dim3(256), 0, stream,
                                F(L.g[o - 1][kLayers]), L.Ho[o - 1], L.Wo[o - 1], F(L.g[o][0]), h, w);
         }
-        for (int i = 1; i < kLevels; ++i) blur(F(L.g[o][i - 1]), F(L.g[o][i]), h, w, taps[i]);
+        for (int i = 1; i < kLevels; ++i)
+            if (blur(F(L.g[o][i - 1]), F(L.g[o][i]), h, w, taps[i])) return GTSFM_ERR_HIP;
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
         GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, 16, stream));
