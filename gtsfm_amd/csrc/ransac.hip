@@ -152,6 +152,13 @@ __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], doubl
     return c;
 }
 
+__device__ __forceinline__ double peval1(const double (&R)[kChain], double x) {
+    double a = R[row_off(1) + 9];
+#pragma unroll
+    for (int i = 8; i >= 0; --i) a = a * x + R[row_off(1) + i];
+    return a;
+}
+
 __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
     double a = R[10];
 #pragma unroll
@@ -189,9 +196,22 @@ __device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_r
 #pragma unroll
         for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dk ? S[11 * k + i] : 0.0;
     }
-    double bound = 0.0;
-    for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(S[i]));
-    bound += 1.0;
+    // root bound (== oracle root_bound_pow2): exact exponent arithmetic, a power of two
+    double bound;
+    {
+        int emax = -2000;
+        for (int k = 1; k <= deg; ++k) {
+            double mk = fabs(S[deg - k]);
+            if (k == deg) mk *= 0.5;
+            if (mk == 0.0) continue;
+            int x;
+            frexp(mk, &x);
+            const int c = x >= 0 ? (x + k - 1) / k : -((-x) / k);
+            emax = c > emax ? c : emax;
+        }
+        if (emax == -2000) emax = 0;
+        bound = ldexp(1.0, emax + 1);
+    }
     // isolation (stack and the interval list reuse the chain's LDS)
     LaneArr<double> st_a = m.u, st_b = m.u.at(kStack), iv_a = m.u.at(2 * kStack), iv_b = m.u.at(2 * kStack + kMaxSol);
     LaneArr<int> st_va = m.iv, st_vb = m.iv.at(kStack);
@@ -227,21 +247,51 @@ __device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_r
         hi[k] = k < nr ? iv_b[k] : 0.0;
         flo[k] = peval0(R, lo[k]);
     }
+    // all isolating intervals refined together (== oracle): bisection down to a relative width of 2^-20, then 4
+    // safeguarded Newton steps with p' = Sturm row 1
+    unsigned live = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxSol; ++k) live |= (k < nr ? 1u : 0u) << k;
+    const unsigned all_roots = live;
     for (int it = 0; it < 80; ++it) {
+        if (!__any(live != 0)) break;
 #pragma unroll
         for (int k = 0; k < kMaxSol; ++k) {
+            if (!__any((live >> k) & 1u)) continue;
+            const bool go = ((live >> k) & 1u) && hi[k] - lo[k] > 0x1p-20 * fmax(1.0, fmax(fabs(lo[k]), fabs(hi[k])));
+            if (!go) live &= ~(1u << k);
             const double mid = 0.5 * (lo[k] + hi[k]);
             const double fm = peval0(R, mid);
             const bool left = (fm < 0.0) == (flo[k] < 0.0) && fm != 0.0;
-            lo[k] = left ? mid : lo[k];
-            flo[k] = left ? fm : flo[k];
-            hi[k] = left ? hi[k] : mid;
+            lo[k] = go && left ? mid : lo[k];
+            flo[k] = go && left ? fm : flo[k];
+            hi[k] = go && !left ? mid : hi[k];
+        }
+    }
+    double xr[kMaxSol];
+#pragma unroll
+    for (int k = 0; k < kMaxSol; ++k) xr[k] = 0.5 * (lo[k] + hi[k]);
+    live = all_roots;
+    for (int it = 0; it < 4; ++it) {
+#pragma unroll
+        for (int k = 0; k < kMaxSol; ++k) {
+            if (!__any((live >> k) & 1u)) continue;
+            const double fx = peval0(R, xr[k]), dfx = peval1(R, xr[k]);
+            const bool go = ((live >> k) & 1u) && fx != 0.0;
+            if (!go) live &= ~(1u << k);
+            const bool left = (fx < 0.0) == (flo[k] < 0.0);
+            lo[k] = go && left ? xr[k] : lo[k];
+            flo[k] = go && left ? fx : flo[k];
+            hi[k] = go && !left ? xr[k] : hi[k];
+            const double xn = xr[k] - fx / dfx;
+            const double xs = (xn > lo[k] && xn < hi[k]) ? xn : 0.5 * (lo[k] + hi[k]);
+            xr[k] = go ? xs : xr[k];
         }
     }
     LaneArr<double> roots = iv_a;
 #pragma unroll
     for (int k = 0; k < kMaxSol; ++k)
-        if (k < nr) roots[k] = 0.5 * (lo[k] + hi[k]);
+        if (k < nr) roots[k] = xr[k];
     for (int k = 0; k < nr; ++k) on_root(roots[k]);
     return nr;
 }
@@ -314,16 +364,19 @@ __device__ int five_point(const double* x1, const double* x2, SolverMem m, SolFn
         E[e][2] = N[2][e];
         E[e][3] = N[3][e];
     }
-    LaneArr<double> A = m.u;  // [10][20]
-    for (int k = 0; k < 200; ++k) A[k] = 0.0;
+    LaneArr<double> A = m.u;  // [10][20]; each row is accumulated in registers, then stored once
     {
-        double q[10];
-        mul_ll(E[4], E[8], q); addmul_ql_lds(q, E[0], 1.0, A);
-        mul_ll(E[5], E[7], q); addmul_ql_lds(q, E[0], -1.0, A);
-        mul_ll(E[3], E[8], q); addmul_ql_lds(q, E[1], -1.0, A);
-        mul_ll(E[5], E[6], q); addmul_ql_lds(q, E[1], 1.0, A);
-        mul_ll(E[3], E[7], q); addmul_ql_lds(q, E[2], 1.0, A);
-        mul_ll(E[4], E[6], q); addmul_ql_lds(q, E[2], -1.0, A);
+        double row[20], q[10];
+#pragma unroll
+        for (int k = 0; k < 20; ++k) row[k] = 0.0;
+        mul_ll(E[4], E[8], q); addmul_ql(q, E[0], 1.0, row);
+        mul_ll(E[5], E[7], q); addmul_ql(q, E[0], -1.0, row);
+        mul_ll(E[3], E[8], q); addmul_ql(q, E[1], -1.0, row);
+        mul_ll(E[5], E[6], q); addmul_ql(q, E[1], 1.0, row);
+        mul_ll(E[3], E[7], q); addmul_ql(q, E[2], 1.0, row);
+        mul_ll(E[4], E[6], q); addmul_ql(q, E[2], -1.0, row);
+#pragma unroll
+        for (int k = 0; k < 20; ++k) A[k] = row[k];
     }
     double EEt[3][3][10], tr[10], tmp[10];
 #pragma unroll
@@ -348,25 +401,51 @@ __device__ int five_point(const double* x1, const double* x2, SolverMem m, SolFn
     for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            LaneArr<double> row = A.at(20 * (1 + 3 * i + j));
+            double row[20];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) addmul_ql_lds(EEt[i][k], E[3 * k + j], 2.0, row);
-            addmul_ql_lds(tr, E[3 * i + j], -1.0, row);
+            for (int k = 0; k < 20; ++k) row[k] = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) addmul_ql(EEt[i][k], E[3 * k + j], 2.0, row);
+            addmul_ql(tr, E[3 * i + j], -1.0, row);
+            const int r0 = 20 * (1 + 3 * i + j);
+#pragma unroll
+            for (int k = 0; k < 20; ++k) A[r0 + k] = row[k];
         }
+    // Gauss-Jordan with partial pivoting; every row is moved through registers whole (loads issued together)
+#pragma unroll
     for (int c = 0; c < 10; ++c) {
         int pr = c;
         double best = fabs(A[20 * c + c]);
-        for (int r = c + 1; r < 10; ++r)
-            if (fabs(A[20 * r + c]) > best) { best = fabs(A[20 * r + c]); pr = r; }
+        for (int r = c + 1; r < 10; ++r) {
+            const double v = fabs(A[20 * r + c]);
+            if (v > best) { best = v; pr = r; }
+        }
         if (best < 1e-14) return 0;
-        if (pr != c)
-            for (int j = 0; j < 20; ++j) { const double tt = A[20 * c + j]; A[20 * c + j] = A[20 * pr + j]; A[20 * pr + j] = tt; }
-        const double inv = 1.0 / A[20 * c + c];
-        for (int j = 0; j < 20; ++j) A[20 * c + j] *= inv;
+        double prow[20];
+#pragma unroll
+        for (int j = 0; j < 20; ++j) prow[j] = A[20 * pr + j];
+        if (pr != c) {
+            double crow[20];
+#pragma unroll
+            for (int j = 0; j < 20; ++j) crow[j] = A[20 * c + j];
+#pragma unroll
+            for (int j = 0; j < 20; ++j) A[20 * pr + j] = crow[j];
+        }
+        const double inv = 1.0 / prow[c];
+#pragma unroll
+        for (int j = 0; j < 20; ++j) prow[j] *= inv;
+#pragma unroll
+        for (int j = 0; j < 20; ++j) A[20 * c + j] = prow[j];
         for (int r = 0; r < 10; ++r) {
             if (r == c) continue;
-            const double f = A[20 * r + c];
-            for (int j = 0; j < 20; ++j) A[20 * r + j] -= f * A[20 * c + j];
+            double row[20];
+#pragma unroll
+            for (int j = 0; j < 20; ++j) row[j] = A[20 * r + j];
+            const double f = row[c];
+#pragma unroll
+            for (int j = 0; j < 20; ++j) row[j] -= f * prow[j];
+#pragma unroll
+            for (int j = 0; j < 20; ++j) A[20 * r + j] = row[j];
         }
     }
     double B[3][3][5];
@@ -473,67 +552,135 @@ __device__ int wave_count(const float* E, const float4* pts, int M, float thr2, 
     return c;
 }
 
-// ------------------------------------------------------------------ small dense linear algebra (one lane / redundant)
-__device__ void jacobi_eig(double* a, int n, double* w, double* V) {
-    for (int i = 0; i < n; ++i)
-        for (int j = 0; j < n; ++j) V[i * n + j] = (i == j) ? 1.0 : 0.0;
+// ------------------------------------------------------------------ small dense linear algebra
+// Cyclic Jacobi eigen-decomposition, the same rotation sequence as oracle/ransac.c jacobi_eig. N = 3: fully
+// unrolled, register resident (redundant per lane).
+template <int N>
+__device__ __forceinline__ void jacobi_eig_reg(double (&a)[N * N], double (&w)[N], double (&V)[N * N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = 0; j < N; ++j) V[i * N + j] = (i == j) ? 1.0 : 0.0;
     for (int sweep = 0; sweep < 30; ++sweep) {
         double off = 0.0;
-        for (int i = 0; i < n; ++i)
-            for (int j = i + 1; j < n; ++j) off += a[i * n + j] * a[i * n + j];
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+#pragma unroll
+            for (int j = i + 1; j < N; ++j) off += a[i * N + j] * a[i * N + j];
         if (off < 1e-30) break;
-        for (int p = 0; p < n; ++p)
-            for (int q = p + 1; q < n; ++q) {
-                const double apq = a[p * n + q];
+#pragma unroll
+        for (int p = 0; p < N; ++p)
+#pragma unroll
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = a[p * N + q];
                 if (fabs(apq) < 1e-300) continue;
-                const double app = a[p * n + p], aqq = a[q * n + q];
+                const double app = a[p * N + p], aqq = a[q * N + q];
                 const double theta = (aqq - app) / (2.0 * apq);
                 const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < n; ++k) {
-                    const double akp = a[k * n + p], akq = a[k * n + q];
-                    a[k * n + p] = c * akp - s * akq;
-                    a[k * n + q] = s * akp + c * akq;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    const double akp = a[k * N + p], akq = a[k * N + q];
+                    a[k * N + p] = c * akp - s * akq;
+                    a[k * N + q] = s * akp + c * akq;
                 }
-                for (int k = 0; k < n; ++k) {
-                    const double apk = a[p * n + k], aqk = a[q * n + k];
-                    a[p * n + k] = c * apk - s * aqk;
-                    a[q * n + k] = s * apk + c * aqk;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    const double apk = a[p * N + k], aqk = a[q * N + k];
+                    a[p * N + k] = c * apk - s * aqk;
+                    a[q * N + k] = s * apk + c * aqk;
                 }
-                for (int k = 0; k < n; ++k) {
-                    const double vkp = V[k * n + p], vkq = V[k * n + q];
-                    V[k * n + p] = c * vkp - s * vkq;
-                    V[k * n + q] = s * vkp + c * vkq;
+#pragma unroll
+                for (int k = 0; k < N; ++k) {
+                    const double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = c * vkp - s * vkq;
+                    V[k * N + q] = s * vkp + c * vkq;
                 }
             }
     }
-    for (int i = 0; i < n; ++i) w[i] = a[i * n + i];
+#pragma unroll
+    for (int i = 0; i < N; ++i) w[i] = a[i * N + i];
+}
+
+// 9x9 Jacobi on a wave: a and V live in LDS, the rotation angles are computed redundantly by every lane (uniform
+// control flow), the k-loops of one rotation run one k per lane. Element-wise identical to the oracle.
+__device__ void jacobi9_lds(double* a, double* V, int lane) {
+    constexpr int N = 9;
+    for (int i = lane; i < N * N; i += 64) V[i] = (i / N == i % N) ? 1.0 : 0.0;
+    __syncthreads();
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        double off = 0.0;
+        for (int i = 0; i < N; ++i)
+            for (int j = i + 1; j < N; ++j) off += a[i * N + j] * a[i * N + j];
+        if (off < 1e-30) break;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = a[p * N + q];
+                if (fabs(apq) < 1e-300) continue;
+                const double app = a[p * N + p], aqq = a[q * N + q];
+                const double theta = (aqq - app) / (2.0 * apq);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                __syncthreads();
+                if (lane < N) {
+                    const int k = lane;
+                    const double akp = a[k * N + p], akq = a[k * N + q];
+                    a[k * N + p] = c * akp - s * akq;
+                    a[k * N + q] = s * akp + c * akq;
+                }
+                __syncthreads();
+                if (lane < N) {
+                    const int k = lane;
+                    const double apk = a[p * N + k], aqk = a[q * N + k];
+                    a[p * N + k] = c * apk - s * aqk;
+                    a[q * N + k] = s * apk + c * aqk;
+                } else if (lane < 2 * N) {
+                    const int k = lane - N;
+                    const double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = c * vkp - s * vkq;
+                    V[k * N + q] = s * vkp + c * vkq;
+                }
+                __syncthreads();
+            }
+    }
 }
 
 __device__ void svd3(const double* E, double* U, double* s, double* V) {
     double ata[9], w[3], Vt[9];
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
         for (int j = 0; j < 3; ++j) {
             double acc = 0.0;
+#pragma unroll
             for (int k = 0; k < 3; ++k) acc += E[k * 3 + i] * E[k * 3 + j];
             ata[i * 3 + j] = acc;
         }
-    jacobi_eig(ata, 3, w, Vt);
-    int order[3] = {0, 1, 2};
-    for (int i = 0; i < 3; ++i)
-        for (int j = i + 1; j < 3; ++j)
-            if (w[order[j]] > w[order[i]]) { const int t = order[i]; order[i] = order[j]; order[j] = t; }
+    jacobi_eig_reg<3>(ata, w, Vt);
+    // descending order of w (selection by comparisons, same result as the oracle's index sort)
+    int o0 = 0, o1 = 1, o2 = 2;
+    if (w[o1] > w[o0]) { const int t = o0; o0 = o1; o1 = t; }
+    if (w[o2] > w[o0]) { const int t = o0; o0 = o2; o2 = t; }
+    if (w[o2] > w[o1]) { const int t = o1; o1 = o2; o2 = t; }
+    const int order[3] = {o0, o1, o2};
+#pragma unroll
     for (int c = 0; c < 3; ++c) {
-        s[c] = sqrt(fmax(w[order[c]], 0.0));
-        for (int r = 0; r < 3; ++r) V[r * 3 + c] = Vt[r * 3 + order[c]];
+        const int oc = order[c];
+        const double wc = oc == 0 ? w[0] : oc == 1 ? w[1] : w[2];
+        s[c] = sqrt(fmax(wc, 0.0));
+#pragma unroll
+        for (int r = 0; r < 3; ++r) V[r * 3 + c] = oc == 0 ? Vt[r * 3] : oc == 1 ? Vt[r * 3 + 1] : Vt[r * 3 + 2];
     }
+#pragma unroll
     for (int c = 0; c < 2; ++c) {
         double u[3], nrm = 0.0;
+#pragma unroll
         for (int r = 0; r < 3; ++r) {
             u[r] = E[r * 3 + 0] * V[0 * 3 + c] + E[r * 3 + 1] * V[1 * 3 + c] + E[r * 3 + 2] * V[2 * 3 + c];
             nrm += u[r] * u[r];
         }
         nrm = sqrt(nrm);
+#pragma unroll
         for (int r = 0; r < 3; ++r) U[r * 3 + c] = nrm > 0 ? u[r] / nrm : (r == c ? 1.0 : 0.0);
     }
     U[2] = U[3] * U[7] - U[6] * U[4];
@@ -566,7 +713,7 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
 // Wave-cooperative Sampson-weighted 8-point refit (see oracle refit_essential). The 45 unique normal-matrix
 // entries are summed per lane, then butterfly-reduced across the wave (fixed order: deterministic).
 __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const double* Esel, double th2,
-                           const double* Ew, double* Eout, int lane) {
+                           const double* Ew, double* Eout, int lane, double* jac_a, double* jac_v) {
     double acc[45];
 #pragma unroll
     for (int k = 0; k < 45; ++k) acc[k] = 0.0;
@@ -591,25 +738,25 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
 #pragma unroll
     for (int k = 0; k < 45; ++k)
         for (int m = 1; m < 64; m <<= 1) acc[k] += shfl_xor_d(acc[k], m);
-    double ata[81];
-    {
-        int k = 0;
+    if (lane < 45) {
+        int a = 0, k = lane;
+        while (k >= 9 - a) { k -= 9 - a; ++a; }
+        const int b = a + k;
+        double v = acc[0];
 #pragma unroll
-        for (int a = 0; a < 9; ++a)
-#pragma unroll
-            for (int b = a; b < 9; ++b) {
-                ata[a * 9 + b] = acc[k];
-                ata[b * 9 + a] = acc[k];
-                ++k;
-            }
+        for (int q = 1; q < 45; ++q) v = q == lane ? acc[q] : v;
+        jac_a[a * 9 + b] = v;
+        jac_a[b * 9 + a] = v;
     }
-    double w[9], V[81];
-    jacobi_eig(ata, 9, w, V);
+    __syncthreads();
+    jacobi9_lds(jac_a, jac_v, lane);
     int imin = 0;
+    double wmin = jac_a[0];
     for (int i = 1; i < 9; ++i)
-        if (w[i] < w[imin]) imin = i;
+        if (jac_a[i * 9 + i] < wmin) { wmin = jac_a[i * 9 + i]; imin = i; }
     double E[9];
-    for (int k = 0; k < 9; ++k) E[k] = V[k * 9 + imin];
+    for (int k = 0; k < 9; ++k) E[k] = jac_v[k * 9 + imin];
+    __syncthreads();  // every lane has read the result before the LDS is reused
     double U[9], s[3], Vv[9];
     svd3(E, U, s, Vv);
     double nrm = 0.0;
@@ -808,6 +955,7 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
                                                            const double2* __restrict__ x2n_all,
                                                            const float4* __restrict__ pts_all, double thr_px,
                                                            RansacOutputs out, const PairState* __restrict__ st) {
+    __shared__ double jac_a[81], jac_v[81];
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     const int M = match_count[p];
@@ -855,11 +1003,11 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
             const double th = thr * (kLoMult - (kLoMult - 1.0) * k / (kLoSteps - 1));
             double Esel[9], En[9];
             for (int e = 0; e < 9; ++e) Esel[e] = E[e];
-            if (!wave_refit(x1, x2, M, Esel, th * th, Esel, En, lane)) break;
+            if (!wave_refit(x1, x2, M, Esel, th * th, Esel, En, lane, jac_a, jac_v)) break;
             bool ok = true;
             for (int r = 1; r < kLoIrls && ok; ++r) {
                 double Et[9];
-                ok = wave_refit(x1, x2, M, Esel, th * th, En, Et, lane);
+                ok = wave_refit(x1, x2, M, Esel, th * th, En, Et, lane, jac_a, jac_v);
                 if (ok)
                     for (int e = 0; e < 9; ++e) En[e] = Et[e];
             }

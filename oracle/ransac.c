@@ -145,6 +145,23 @@ static int sign_changes(const sturm_t* s, double x) {
 }
 
 /* Real roots of p (degree <= 10) in ascending order. Returns the count. */
+/* Root-magnitude bound of a monic polynomial (Fujiwara: |z| <= 2 max_k |p[deg-k]|^(1/k), the constant term halved),
+   rounded up to a power of two with exact exponent arithmetic (frexp), so CPU and GPU agree bit for bit. */
+static double root_bound_pow2(const double* p, int deg) {
+    int emax = -2000;
+    for (int k = 1; k <= deg; ++k) {
+        double m = fabs(p[deg - k]);
+        if (k == deg) m *= 0.5;
+        if (m == 0.0) continue;
+        int x;
+        frexp(m, &x); /* m < 2^x */
+        const int c = x >= 0 ? (x + k - 1) / k : -((-x) / k); /* ceil(x / k) */
+        if (c > emax) emax = c;
+    }
+    if (emax == -2000) emax = 0;
+    return ldexp(1.0, emax + 1);
+}
+
 static int real_roots(const double* pin, int deg, double* roots) {
     double p[11];
     while (deg > 0 && fabs(pin[deg]) <= 1e-300) --deg;
@@ -164,9 +181,7 @@ static int real_roots(const double* pin, int deg, double* roots) {
         s.deg[s.n] = dr;
         s.n++;
     }
-    double bound = 0.0;
-    for (int i = 0; i < deg; ++i) bound = fmax(bound, fabs(p[i]));
-    bound += 1.0;
+    const double bound = root_bound_pow2(p, deg);
     /* isolation by bisection with Sturm counts */
     double st_a[48], st_b[48];
     int st_va[48], st_vb[48], ns = 0, nr = 0;
@@ -184,10 +199,11 @@ static int real_roots(const double* pin, int deg, double* roots) {
         const int cnt = va - vb;
         if (cnt <= 0) continue;
         if (cnt == 1 || b - a < 1e-10 * fmax(1.0, fabs(a))) {
-            /* refine: bisection on the sign of p */
+            /* refine: bisection down to a relative width of 2^-20, then 4 safeguarded Newton steps (p' is Sturm row 1) */
             double lo = a, hi = b;
             double flo = peval(p, deg, lo);
             for (int it = 0; it < 80; ++it) {
+                if (hi - lo <= 0x1p-20 * fmax(1.0, fmax(fabs(lo), fabs(hi)))) break;
                 const double mid = 0.5 * (lo + hi);
                 const double fm = peval(p, deg, mid);
                 if ((fm < 0.0) == (flo < 0.0) && fm != 0.0) {
@@ -197,7 +213,20 @@ static int real_roots(const double* pin, int deg, double* roots) {
                     hi = mid;
                 }
             }
-            roots[nr++] = 0.5 * (lo + hi);
+            double x = 0.5 * (lo + hi);
+            for (int it = 0; it < 4; ++it) {
+                const double fx = peval(p, deg, x), dfx = peval(s.p[1], s.deg[1], x);
+                if (fx == 0.0) break;
+                if ((fx < 0.0) == (flo < 0.0)) {
+                    lo = x;
+                    flo = fx;
+                } else {
+                    hi = x;
+                }
+                const double xn = x - fx / dfx;
+                x = (xn > lo && xn < hi) ? xn : 0.5 * (lo + hi);
+            }
+            roots[nr++] = x;
             continue;
         }
         const double mid = 0.5 * (a + b);
