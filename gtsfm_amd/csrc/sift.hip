@@ -142,6 +142,7 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 // Tiles are mapped XCD-contiguously (consecutive workgroups land on different XCDs; each XCD gets a contiguous run
 // of tiles so halos are shared through its own L2).
 constexpr int kBlurTX = 64, kBlurTY = 32, kBlurTYT = 4, kBlurColRows = kBlurTY / kBlurTYT;
+typedef float pf2 __attribute__((ext_vector_type(2)));
 constexpr int kBlurMaxR = 16;
 
 __host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 3 + 3) / 4 * 4; }
@@ -158,26 +159,16 @@ __device__ __forceinline__ float gray_at(const uint8_t* __restrict__ s, int C, i
     return (float)((p[0] * 4899 + p[1] * 9617 + p[2] * 1868 + (1 << 13)) >> 14);
 }
 
-// up_pixel with the gray samples read from an LDS tile whose origin is (gy0, gx0)
-__device__ __forceinline__ float up_pixel_lds(const float* __restrict__ g, int gw, int gy0, int gx0, int H, int W, int y,
-                                              int x) {
-    float fy = (float)((y + 0.5) * 0.5 - 0.5);
-    int sy = (int)floorf(fy);
-    fy -= sy;
-    if (sy < 0) { sy = 0; fy = 0; }
-    if (sy >= H - 1) { sy = H - 1; fy = 0; }
-    const int sy1 = sy + 1 < H ? sy + 1 : H - 1;
+// INTER_LINEAR 2x source coordinate of output index x (cv::resize, half-pixel centres, clamped at the border)
+__device__ __forceinline__ void up_coord(int x, int W, int& s0, int& s1, float& f) {
     float fx = (float)((x + 0.5) * 0.5 - 0.5);
     int sx = (int)floorf(fx);
     fx -= sx;
     if (sx < 0) { sx = 0; fx = 0; }
     if (sx >= W - 1) { sx = W - 1; fx = 0; }
-    const int sx1 = sx + 1 < W ? sx + 1 : W - 1;
-    const float* r0p = g + (sy - gy0) * gw;
-    const float* r1p = g + (sy1 - gy0) * gw;
-    const float r0 = r0p[sx - gx0] * (1.f - fx) + r0p[sx1 - gx0] * fx;
-    const float r1 = r1p[sx - gx0] * (1.f - fx) + r1p[sx1 - gx0] * fx;
-    return r0 * (1.f - fy) + r1 * fy;
+    s0 = sx;
+    s1 = sx + 1 < W ? sx + 1 : W - 1;
+    f = fx;
 }
 
 template <int R, bool kFromU8>
@@ -230,12 +221,29 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
             }
         }
         __syncthreads();
-        for (int iy = ty; iy < IH; iy += kBlurTYT) {
-            const int yy = reflect101(y0 - R + iy, H);
+        constexpr int NQ = (IW + kBlurTX - 1) / kBlurTX;
+        int cx0[NQ], cx1[NQ];
+        float cfx[NQ];
 #pragma unroll
-            for (int q = 0; q < (IW + kBlurTX - 1) / kBlurTX; ++q) {
+        for (int q = 0; q < NQ; ++q) {
+            up_coord(xx[q], W0, cx0[q], cx1[q], cfx[q]);
+            cx0[q] -= gx0;
+            cx1[q] -= gx0;
+        }
+        for (int iy = ty; iy < IH; iy += kBlurTYT) {
+            int sy0, sy1;
+            float fy;
+            up_coord(reflect101(y0 - R + iy, H), H0, sy0, sy1, fy);
+            const float* r0p = g + (sy0 - gy0) * GW;
+            const float* r1p = g + (sy1 - gy0) * GW;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
                 const int ix = tx + q * kBlurTX;
-                if (ix < IW) in[iy * IWP + ix] = up_pixel_lds(g, GW, gy0, gx0, H0, W0, yy, xx[q]);
+                if (ix < IW) {
+                    const float r0 = r0p[cx0[q]] * (1.f - cfx[q]) + r0p[cx1[q]] * cfx[q];
+                    const float r1 = r1p[cx0[q]] * (1.f - cfx[q]) + r1p[cx1[q]] * cfx[q];
+                    in[iy * IWP + ix] = r0 * (1.f - fy) + r1 * fy;
+                }
             }
         }
     } else {
@@ -268,15 +276,20 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
             const float4 w4 = wp[q];
             v[4 * q] = w4.x; v[4 * q + 1] = w4.y; v[4 * q + 2] = w4.z; v[4 * q + 3] = w4.w;
         }
-        float o[4];
+        // two outputs per packed-fp32 op (v_pk_add_f32 / v_pk_fma_f32); per-lane rounding unchanged
+        pf2 o[2];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            float acc = k[0] * v[R + q];
+        for (int h = 0; h < 2; ++h) {
+            const int q = 2 * h;
+            pf2 acc = pf2{k[0], k[0]} * pf2{v[R + q], v[R + q + 1]};
 #pragma unroll
-            for (int j = 1; j <= R; ++j) acc = fmaf(k[j], v[R + q - j] + v[R + q + j], acc);
-            o[q] = acc;
+            for (int j = 1; j <= R; ++j)
+                acc = __builtin_elementwise_fma(pf2{k[j], k[j]},
+                                                pf2{v[R + q - j], v[R + q + 1 - j]} + pf2{v[R + q + j], v[R + q + 1 + j]},
+                                                acc);
+            o[h] = acc;
         }
-        *(float4*)(rb + iy * kBlurTX + g4) = make_float4(o[0], o[1], o[2], o[3]);
+        *(float4*)(rb + iy * kBlurTX + g4) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
     }
     __syncthreads();
     // column pass: kBlurColRows consecutive outputs per thread
@@ -287,12 +300,15 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
 #pragma unroll
     for (int i = 0; i < kBlurColRows + 2 * R; ++i) c[i] = rb[(ly0 + i) * kBlurTX + tx];
 #pragma unroll
-    for (int q = 0; q < kBlurColRows; ++q) {
-        const int y = y0 + ly0 + q;
-        float acc = k[0] * c[R + q];
+    for (int q = 0; q < kBlurColRows; q += 2) {
+        pf2 acc = pf2{k[0], k[0]} * pf2{c[R + q], c[R + q + 1]};
 #pragma unroll
-        for (int j = 1; j <= R; ++j) acc = fmaf(k[j], c[R + q - j] + c[R + q + j], acc);
-        if (y < H) dst[base + (size_t)y * W + x] = acc;
+        for (int j = 1; j <= R; ++j)
+            acc = __builtin_elementwise_fma(pf2{k[j], k[j]},
+                                            pf2{c[R + q - j], c[R + q + 1 - j]} + pf2{c[R + q + j], c[R + q + 1 + j]}, acc);
+        const int y = y0 + ly0 + q;
+        if (y < H) dst[base + (size_t)y * W + x] = acc.x;
+        if (y + 1 < H) dst[base + (size_t)(y + 1) * W + x] = acc.y;
     }
 }
 
@@ -330,6 +346,9 @@ struct GaussSet {
 // DoG levels are never stored: DoG_l = G_{l+1} - G_l is recomputed from the Gaussian levels (the same fp32
 // subtraction cv::subtract performs), which removes 5 level writes per octave.
 constexpr int kExTX = 64, kExTY = 16, kExTYT = 4;
+// Candidate list sharded over kCandShards counters/segments: one global atomic per tile on a single counter
+// serialises at ~11 ns each (800k tiles per octave-0 launch); sharding spreads them over independent lines.
+constexpr int kCandShards = 256;
 
 __global__ __launch_bounds__(kExTX* kExTYT) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
                                                                 int* __restrict__ n_cand, int cap) {
@@ -339,6 +358,8 @@ __global__ __launch_bounds__(kExTX* kExTYT) void extrema_kernel(GaussSet G, int 
     const int tx = threadIdx.x, ty = threadIdx.y, b = blockIdx.z;
     const int x0 = blockIdx.x * kExTX, y0 = blockIdx.y * kExTY;
     const size_t base = (size_t)b * H * W;
+    const int shard = (int)((blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z)) %
+                            kCandShards);  // cap is per shard
     if (tx == 0 && ty == 0) n_list = 0;
     {
         constexpr int NR = (kExTY + 2 + kExTYT - 1) / kExTYT, NQ = 2;
@@ -365,54 +386,81 @@ __global__ __launch_bounds__(kExTX* kExTYT) void extrema_kernel(GaussSet G, int 
             }
     }
     __syncthreads();
+    // Each thread owns a strip of kExRows rows of one column. The 27-neighbourhood test "val >= every neighbour"
+    // is val == max over the 3x3x3 block (the centre included), computed with shared max3/min3 partials:
+    // per-row 3-wide extrema -> 3x3 box extrema -> across the three DoG levels.
+    constexpr int kExRows = kExTY / kExTYT;
     const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
     const int c = x0 + tx;
-    for (int ly = ty; ly < kExTY; ly += kExTYT) {
-        const int r = y0 + ly;
-        if (c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) continue;
+    const int ly0 = ty * kExRows;
+    float rmax[kDogs][kExRows + 2], rmin[kDogs][kExRows + 2], ctr[kDogs][kExRows];
+#pragma unroll
+    for (int l = 0; l < kDogs; ++l)
+#pragma unroll
+        for (int i = 0; i < kExRows + 2; ++i) {
+            const float a0 = D[l][ly0 + i][tx], a1 = D[l][ly0 + i][tx + 1], a2 = D[l][ly0 + i][tx + 2];
+            rmax[l][i] = fmaxf(fmaxf(a0, a1), a2);
+            rmin[l][i] = fminf(fminf(a0, a1), a2);
+            if (i >= 1 && i <= kExRows) ctr[l][i - 1] = a1;
+        }
+    const bool col_ok = c >= kBorder && c < W - kBorder;
+#pragma unroll
+    for (int q = 0; q < kExRows; ++q) {
+        const int r = y0 + ly0 + q;
+        if (!col_ok || r < kBorder || r >= H - kBorder) continue;
+        float bmax[kDogs], bmin[kDogs];
+#pragma unroll
+        for (int l = 0; l < kDogs; ++l) {
+            bmax[l] = fmaxf(fmaxf(rmax[l][q], rmax[l][q + 1]), rmax[l][q + 2]);
+            bmin[l] = fminf(fminf(rmin[l][q], rmin[l][q + 1]), rmin[l][q + 2]);
+        }
 #pragma unroll
         for (int layer = 1; layer <= kLayers; ++layer) {
-            const float val = D[layer][ly + 1][tx + 1];
+            const float val = ctr[layer][q];
             if (!(fabsf(val) > threshold)) continue;
-            bool ismax = val > 0, ismin = val < 0;
-#pragma unroll
-            for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    const float a = D[layer - 1][ly + dy][tx + dx], bb = D[layer + 1][ly + dy][tx + dx],
-                                m = D[layer][ly + dy][tx + dx];
-                    if (ismax && !(val >= a && val >= bb && val >= m)) ismax = false;
-                    if (ismin && !(val <= a && val <= bb && val <= m)) ismin = false;
-                }
+            const float mx = fmaxf(fmaxf(bmax[layer - 1], bmax[layer]), bmax[layer + 1]);
+            const float mn = fminf(fminf(bmin[layer - 1], bmin[layer]), bmin[layer + 1]);
+            const bool ismax = val > 0 && val >= mx, ismin = val < 0 && val <= mn;
             if (!ismax && !ismin) continue;
             const int slot = atomicAdd(&n_list, 1);
             if (slot < (int)(sizeof(list) / sizeof(Cand))) {
                 list[slot] = Cand{b, layer, r, c};
             } else {  // plateau-heavy tile: spill straight to the global list
-                const int g = atomicAdd(n_cand, 1);
-                if (g < cap) cands[g] = Cand{b, layer, r, c};
+                const int g = atomicAdd(&n_cand[shard], 1);
+                if (g < cap) cands[(size_t)shard * cap + g] = Cand{b, layer, r, c};
             }
         }
     }
     __syncthreads();
     const int n = min(n_list, (int)(sizeof(list) / sizeof(Cand)));
     const int t = ty * kExTX + tx;
-    if (t == 0) gbase = n ? atomicAdd(n_cand, n) : 0;
+    if (t == 0) gbase = n ? atomicAdd(&n_cand[shard], n) : 0;
     __syncthreads();
     for (int i = t; i < n; i += kExTX * kExTYT)
-        if (gbase + i < cap) cands[gbase + i] = list[i];
+        if (gbase + i < cap) cands[(size_t)shard * cap + gbase + i] = list[i];
 }
 
 #define DAT(l, r, c) (G.g[(l) + 1][base + (size_t)(r) * W + (c)] - G.g[(l)][base + (size_t)(r) * W + (c)])
 
-__global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restrict__ n_cand_p, int cap, GaussSet G, int H,
-                              int W, int n_img, uint32_t* __restrict__ seen, Refined* __restrict__ out,
-                              int* __restrict__ n_out, int out_cap) {
-    const int n_cand = min(*n_cand_p, cap);
+// Sub-pixel refinement (cv::SIFT adjustLocalExtrema). Candidates come from kCandShards segments of `cap` entries;
+// survivors are appended with one atomic per wave (ballot + prefix popcount).
+__global__ __launch_bounds__(256) void refine_kernel(const Cand* __restrict__ cands,
+                                                     const int* __restrict__ shard_counts, int cap, GaussSet G, int H,
+                                                     int W, int n_img, uint32_t* __restrict__ seen,
+                                                     Refined* __restrict__ out, int* __restrict__ n_out, int out_cap) {
+    const int lane = threadIdx.x & 63;
     const float img_scale = 1.f / 255.f;
     const float deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale, cross_deriv_scale = img_scale * 0.25f;
-    for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < n_cand; id += gridDim.x * blockDim.x) {
-        const Cand cd = cands[id];
+    // gridDim.x is a multiple of kCandShards: each shard is worked by gridDim.x / kCandShards blocks
+    {
+    const int sh = blockIdx.x % kCandShards, sub = blockIdx.x / kCandShards, nsub = gridDim.x / kCandShards;
+    const int n_cand = min(shard_counts[sh], cap);
+    for (int base0 = sub * blockDim.x; base0 < n_cand; base0 += nsub * blockDim.x) {
+        const int id = base0 + threadIdx.x;
+        Refined res;
+        bool keep = false;
+        if (id < n_cand) do {
+        const Cand cd = cands[(size_t)sh * cap + id];
         const size_t base = (size_t)cd.img * H * W;
         int layer = cd.layer, r = cd.r, c = cd.c;
         float xi = 0, xr = 0, xc = 0;
@@ -460,14 +508,14 @@ __global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restr
                 break;
             }
         }
-        if (!ok || i >= kMaxInterp) continue;
+        if (!ok || i >= kMaxInterp) break;
         const int img = layer, prev = layer - 1, next = layer + 1;
         const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
         const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
         const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
         const float tt = dD0 * xc + dD1 * xr + dD2 * xi;
         const float contr = DAT(img, r, c) * img_scale + tt * 0.5f;
-        if (fabsf(contr) * kLayers < kContrast) continue;
+        if (fabsf(contr) * kLayers < kContrast) break;
         const float v2 = DAT(img, r, c) * 2.f;
         const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
         const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
@@ -475,13 +523,23 @@ __global__ void refine_kernel(const Cand* __restrict__ cands, const int* __restr
                            DAT(img, r - 1, c - 1)) * cross_deriv_scale;
         const float tr = dxx + dyy;
         const float det = dxx * dyy - dxy * dxy;
-        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) continue;
+        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) break;
         // duplicates (same refined location) are identical keypoints: keep the first claimant
         const size_t bit = (((size_t)cd.img * kLayers + (layer - 1)) * H + r) * W + c;
         const uint32_t m = 1u << (bit & 31);
-        if (atomicOr(&seen[bit >> 5], m) & m) continue;
-        const int slot = atomicAdd(n_out, 1);
-        if (slot < out_cap) out[slot] = Refined{cd.img, layer, r, c, xc, xr, xi, contr};
+        if (atomicOr(&seen[bit >> 5], m) & m) break;
+        res = Refined{cd.img, layer, r, c, xc, xr, xi, contr};
+        keep = true;
+        } while (0);
+        const unsigned long long bal = __ballot(keep);
+        if (bal) {
+            int wbase = 0;
+            if (lane == 0) wbase = atomicAdd(n_out, (int)__popcll(bal));
+            wbase = __shfl(wbase, 0);
+            const int slot = wbase + (int)__popcll(bal & ((1ull << lane) - 1ull));
+            if (keep && slot < out_cap) out[slot] = res;
+        }
+    }
     }
 }
 
@@ -858,7 +916,9 @@ Layout make_layout(int B, int H, int W, int max_kpts) {
         L.Ho[o] = h;
         L.Wo[o] = w;
         const size_t lvl = (size_t)B * h * w * sizeof(float);
-        for (int i = 0; i < kLevels; ++i) L.g[o][i] = take(lvl);
+        // levels are read together (extrema: all six; blur: two); a per-level skew of 1.25 KiB keeps equal pixels of
+        // different levels off the same HBM channel / bank
+        for (int i = 0; i < kLevels; ++i) L.g[o][i] = take(lvl + (size_t)(5 * i + 3) * 256);
         h /= 2;
         w /= 2;
     }
@@ -868,7 +928,7 @@ Layout make_layout(int B, int H, int W, int max_kpts) {
     L.ref = take((size_t)B * kCandCapPerImg * sizeof(Refined));
     L.kps = take((size_t)B * kKpCapPerImg * sizeof(KeyRec));
     L.kp_counts = take((size_t)B * sizeof(int));
-    L.counters = take(16);
+    L.counters = take((size_t)(kCandShards + 16) * sizeof(int));
     L.sel = take((size_t)B * max_kpts * sizeof(int));
     L.n_sel = take((size_t)B * sizeof(int));
     L.total = off;
@@ -954,19 +1014,19 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
             if (blur(F(L.g[o][i - 1]), F(L.g[o][i]), h, w, taps[i])) return GTSFM_ERR_HIP;
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
-        GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, 16, stream));
+        GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, (kCandShards + 16) * sizeof(int), stream));
         GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.seen, 0,
                                        gtsfm_align_up(((size_t)B * kLayers * h * w + 31) / 32 * 4, 4), stream));
         GaussSet G;
         for (int i = 0; i < kLevels; ++i) G.g[i] = F(L.g[o][i]);
+        const int shard_cap = (int)((size_t)B * kCandCapPerImg / kCandShards);
         hipLaunchKernelGGL(extrema_kernel, dim3((w + kExTX - 1) / kExTX, (h + kExTY - 1) / kExTY, B),
-                           dim3(kExTX, kExTYT), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters + 0,
-                           B * kCandCapPerImg);
-        hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters + 0,
-                           B * kCandCapPerImg, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
-                           counters + 1, B * kCandCapPerImg);
+                           dim3(kExTX, kExTYT), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap);
+        hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
+                           shard_cap, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
+                           counters + kCandShards, B * kCandCapPerImg);
         hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),
-                           counters + 1, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps), kp_counts,
+                           counters + kCandShards, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps), kp_counts,
                            kKpCapPerImg);
         GTSFM_CHECK_HIP(hipGetLastError());
     }
