@@ -21,7 +21,16 @@ __host__ __device__ static inline size_t gtsfm_align_up(size_t x, size_t a) { re
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
 __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-    return umax(umin(a, b), umin(umax(a, b), c));  // lowers to v_med3_u32
+    uint32_t r;  // one v_med3_u32 (the generic min/max form is not always matched by the backend)
+    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// (a << s) | b in one v_lshl_or_b32 (keeps the backend from splitting shared shifts into shift + or pairs)
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) {
+    uint32_t r;
+    asm volatile("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(s), "v"(b));
+    return r;
 }
 
 // Insert key k into a running (b1 <= b2) top-2 of packed keys: second = med3(b1, b2, k), first = min(b1, k).

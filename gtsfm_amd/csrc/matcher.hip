@@ -7,11 +7,12 @@
 //
 // Fast path (GTSFM_MATCH_INT_F16): one K1 x K2 distance GEMM per pair on fp16 MFMA
 // (v_mfma_f32_32x32x16_f16). The squared norms are folded into 4 extra K columns, so the accumulator
-// IS the squared L2 distance:   A'_r = [a, |a|^2 mod 2048, |a|^2 div 2048, 1, 2048]
-//                               B'_c = [-2b, 1, 2048, |b|^2 mod 2048, |b|^2 div 2048]
+// IS the squared L2 distance:   A'_r = [a, |a|^2 mod 2048, |a|^2 div 2048, 1, 2048, 2048]
+//                               B'_c = [-2b, 1, 2048, |b|^2 mod 2048, |b|^2 div 2048, 4096]
+// (the last column adds 2^23, see the epilogue)
 // Every factor is an integer exactly representable in fp16 and every partial sum is an integer < 2^24,
 // so the fp32 accumulation is exact in any order: d2 = |a|^2 + |b|^2 - 2 a.b exactly.
-// The epilogue packs key = d2 << 12 | index (d2 < 2^20) and keeps a running top-2 per row in
+// The epilogue packs key = d2 << ib | index (d2 < 2^20, ib = max(11, ceil log2 kmax)) and keeps a running top-2 per row in
 // registers (v_med3_u32 + v_min_u32 per element) and per column through LDS; the K1 x K2 matrix is
 // never written to HBM. Lexicographic (d2, index) order == OpenCV's strict-'<' scan order, and for
 // d2 < 2^22 ordering by d2 equals ordering by sqrtf(d2), so results are bit-identical to the oracle.
@@ -22,6 +23,8 @@
 // Both paths end in match_finalize_kernel: ratio test in double on float32 distances, mutual check,
 // LDS compaction and a bitonic sort on (distance, i1) — the reference's output order.
 #include "common.hpp"
+
+#include <type_traits>
 
 namespace {
 
@@ -75,6 +78,7 @@ __global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __re
         else if (e == 1) { av = hi; bv = 2048.f; }
         else if (e == 2) { av = 1.f; bv = lo; }
         else if (e == 3) { av = 2048.f; bv = hi; }
+        else if (e == 4) { av = 2048.f; bv = 4096.f; }  // + 2^23: accumulator bits = 0x4B000000 | d2
         ar[k] = (_Float16)av;
         br[k] = (_Float16)bv;
     }
@@ -105,7 +109,16 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                      (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
-template <int NK>
+// A fifth folded K column (A' = 2048, B' = 4096) adds 2^23 to every accumulator, so each holds 2^23 + d2 exactly
+// (d2 < 2^20 for non-negative integer descriptors with |a|^2 < 2^19) and its bit pattern is 0x4B000000 | d2.
+// kFast (ib <= 12, i.e. kmax <= 4096): the packed key is one v_lshl_or_b32 of the raw accumulator bits (the shift
+// drops exponent and sign), no conversion and no saturation. ib = 13 converts, subtracts 2^23 and saturates.
+// B streams through LDS in super-chunks of kSub x 32 columns per barrier; the column partials of a super-chunk are
+// merged by one wave with all 64 lanes busy.
+constexpr int kSub = 2;
+constexpr int kSuper = kSub * kChunk;
+
+template <int NK, bool kFast>
 __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* __restrict__ a_form,
                                                                const _Float16* __restrict__ b_form,
                                                                const int* __restrict__ counts,
@@ -113,11 +126,12 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
                                                                int ib, uint2* __restrict__ rowres,
                                                                uint2* __restrict__ colres) {
     using Cfg = MnnCfg<NK>;
+    constexpr int kSupBytes = kSub * Cfg::kBufBytes;
     const uint32_t dsat = (1u << (32 - ib)) - 1u;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* bbuf = smem;                                             // [2][kChunk][kRowBytes]
-    uint32_t* partial = (uint32_t*)(smem + 2 * Cfg::kBufBytes);             // [2][kWaves][kChunk][2]
-    uint2* colstate = (uint2*)(partial + 2 * kWaves * kChunk * 2);          // [kmax]
+    unsigned char* bbuf = smem;                                      // [2][kSuper][kRowBytes]
+    uint32_t* partial = (uint32_t*)(smem + 2 * kSupBytes);           // [2][kWaves][kSuper][2]
+    uint2* colstate = (uint2*)(partial + 2 * kWaves * kSuper * 2);   // [kmax]
 
     const int p = blockIdx.x;
     const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
@@ -132,24 +146,25 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
     uint2* cres = colres + (size_t)p * kmax;
 
     for (int c = tid; c < n2; c += kThreads) colstate[c] = make_uint2(kNoKey, kNoKey);
-    const int nchunks = (n2 + kChunk - 1) / kChunk;
+    const int nsup = (n2 + kSuper - 1) / kSuper;
 
-    // Chunk `ch` of B (32 consecutive B-form rows = one contiguous block) -> LDS buffer `buf`.
-    auto issue_chunk = [&](int ch, int buf) {
-        const unsigned char* src = Bbytes + (size_t)ch * Cfg::kBufBytes + lane * 16;
-        unsigned char* dst = bbuf + buf * Cfg::kBufBytes;
-        for (int q = wave; q < Cfg::kGlds; q += kWaves) glds16(src + q * 1024, dst + q * 1024);
+    // Super-chunk `sc` of B (kSuper consecutive B-form rows, contiguous in HBM; B-form rows are padded to kpad,
+    // a multiple of 256, so a whole super-chunk is always in bounds) -> LDS buffer `buf`.
+    auto issue_super = [&](int sc, int buf) {
+        const unsigned char* src = Bbytes + (size_t)sc * kSupBytes + lane * 16;
+        unsigned char* dst = bbuf + buf * kSupBytes;
+        for (int q = wave; q < kSub * Cfg::kGlds; q += kWaves) glds16(src + q * 1024, dst + q * 1024);
     };
-    // Merge the 4 waves' column partials of chunk `ch` (buffer pb) into colstate (32 lanes of one wave).
-    auto merge_partials = [&](int ch, int pb) {
-        if (wave == (ch & (kWaves - 1)) && lane < kChunk) {
-            const int col = ch * kChunk + lane;
+    // Merge the 4 waves' column partials of super-chunk `sc` (buffer pb) into colstate (one wave, lane = column).
+    auto merge_partials = [&](int sc, int pb) {
+        if (wave == (sc & (kWaves - 1))) {
+            const int col = sc * kSuper + lane;
             if (col < n2) {
                 uint2 s = colstate[col];
                 uint32_t s1 = s.x, s2 = s.y;
 #pragma unroll
                 for (int w = 0; w < kWaves; ++w) {
-                    const uint32_t* pp = partial + ((pb * kWaves + w) * kChunk + lane) * 2;
+                    const uint32_t* pp = partial + ((pb * kWaves + w) * kSuper + lane) * 2;
                     top2_merge(s1, s2, pp[0], pp[1]);
                 }
                 colstate[col] = make_uint2(s1, s2);
@@ -172,57 +187,76 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
         for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
-        const bool rows_partial0 = (r0w + 32 > n1);
-        const bool rows_partial1 = (r0w + 64 > n1);
+        const bool rows_partial1 = (r0w + 64 > n1);  // either row tile of this wave is partial
 
-        issue_chunk(0, 0);
-        __syncthreads();  // vmcnt(0) + barrier: chunk 0 landed, colstate initialised
+        issue_super(0, 0);
+        __syncthreads();  // vmcnt(0) + barrier: super-chunk 0 landed, colstate initialised
 
-        for (int ch = 0; ch < nchunks; ++ch) {
-            const int buf = ch & 1;
-            if (ch + 1 < nchunks) issue_chunk(ch + 1, buf ^ 1);  // lands during this chunk's MFMAs
-
-            // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows
-            const unsigned char* bb = bbuf + buf * Cfg::kBufBytes + lrow * Cfg::kRowBytes + half * 16;
-            f32x16 acc0 = {}, acc1 = {};
+        for (int sc = 0; sc < nsup; ++sc) {
+            const int buf = sc & 1;
+            if (sc + 1 < nsup) issue_super(sc + 1, buf ^ 1);  // lands during this super-chunk's MFMAs
+#pragma unroll 1
+            for (int sub = 0; sub < kSub; ++sub) {
+                const int ch = sc * kSub + sub;
+                // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows
+                const unsigned char* bb =
+                    bbuf + buf * kSupBytes + (sub * kChunk + lrow) * Cfg::kRowBytes + half * 16;
+                f32x16 acc0 = {}, acc1 = {};
 #pragma unroll
-            for (int s = 0; s < NK; ++s) {
-                const half8 bf = *(const half8*)(bb + 32 * s);
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc1, 0, 0, 0);
-            }
+                for (int s = 0; s < NK; ++s) {
+                    const half8 bf = *(const half8*)(bb + 32 * s);
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc1, 0, 0, 0);
+                }
 
-            const uint32_t gcol = (uint32_t)(ch * kChunk + lrow);
-            const bool col_ok = (int)gcol < n2;
-            const bool cols_partial = (ch * kChunk + kChunk > n2);
-            uint32_t cb1 = kNoKey, cb2 = kNoKey;
+                const uint32_t gcol = (uint32_t)(ch * kChunk + lrow);
+                const bool cols_partial = (ch * kChunk + kChunk > n2);
+                uint32_t cb1 = kNoKey, cb2 = kNoKey;
+                // Epilogue: 2 key builds + 2 top-2 inserts per distance. Partial tiles (last row tile / column
+                // chunk) take a separate masked copy so the full-tile path carries no selects.
+                auto epilogue = [&](auto masked) {
+                    constexpr bool kMasked = decltype(masked)::value;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const f32x16& acc = t ? acc1 : acc0;
-                const bool rows_partial = t ? rows_partial1 : rows_partial0;
-                const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 4 * half);
+                    for (int t = 0; t < 2; ++t) {
+                        const f32x16& acc = t ? acc1 : acc0;
+                        const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 4 * half);
 #pragma unroll
-                for (int g = 0; g < 16; ++g) {
-                    const uint32_t d2 = umin((uint32_t)acc[g], dsat);
-                    const uint32_t grow = rowbase + (uint32_t)((g & 3) + 8 * (g >> 2));
-                    uint32_t rk = (d2 << ib) | gcol;
-                    uint32_t ck = (d2 << ib) | grow;
-                    if (cols_partial) rk = col_ok ? rk : kNoKey;
-                    if (rows_partial) ck = ((int)grow < n1) ? ck : kNoKey;
-                    top2_insert(rb1[t][g], rb2[t][g], rk);
-                    top2_insert(cb1, cb2, ck);
+                        for (int g = 0; g < 16; ++g) {
+                            const uint32_t grow = rowbase + (uint32_t)((g & 3) + 8 * (g >> 2));
+                            uint32_t rk, ck;
+                            if constexpr (kFast) {
+                                const uint32_t bits = __float_as_uint(acc[g]);
+                                rk = lshl_or(bits, (uint32_t)ib, gcol);
+                                ck = lshl_or(bits, (uint32_t)ib, grow);
+                            } else {
+                                const uint32_t d2 = umin((uint32_t)acc[g] - (1u << 23), dsat);
+                                rk = (d2 << ib) | gcol;
+                                ck = (d2 << ib) | grow;
+                            }
+                            if constexpr (kMasked) {
+                                if ((int)gcol >= n2) rk = kNoKey;
+                                if ((int)grow >= n1) ck = kNoKey;
+                            }
+                            top2_insert(rb1[t][g], rb2[t][g], rk);
+                            top2_insert(cb1, cb2, ck);
+                        }
+                    }
+                };
+                if (cols_partial || rows_partial1)
+                    epilogue(std::true_type{});
+                else
+                    epilogue(std::false_type{});
+                // combine the two half-waves (same column, rows +0/+4) and publish the wave's column partial
+                {
+                    const uint32_t o1 = __shfl_xor(cb1, 32), o2 = __shfl_xor(cb2, 32);
+                    top2_merge(cb1, cb2, o1, o2);
+                    partial[((buf * kWaves + wave) * kSuper + sub * kChunk + lrow) * 2 + half] = half ? cb2 : cb1;
                 }
             }
-            // combine the two half-waves (same column, rows +0/+4) and publish the wave's column partial
-            {
-                const uint32_t o1 = __shfl_xor(cb1, 32), o2 = __shfl_xor(cb2, 32);
-                top2_merge(cb1, cb2, o1, o2);
-                partial[((buf * kWaves + wave) * kChunk + lrow) * 2 + half] = half ? cb2 : cb1;
-            }
-            if (ch > 0) merge_partials(ch - 1, buf ^ 1);
-            __syncthreads();  // next chunk landed (vmcnt(0)); partials of this chunk visible
+            if (sc > 0) merge_partials(sc - 1, buf ^ 1);
+            __syncthreads();  // next super-chunk landed (vmcnt(0)); partials of this one visible
         }
-        merge_partials(nchunks - 1, (nchunks - 1) & 1);
+        merge_partials(nsup - 1, (nsup - 1) & 1);
 
         // reduce each row's top-2 across the 32 lanes of its half-wave and store it
 #pragma unroll
@@ -463,20 +497,34 @@ inline int next_pow2(int x) {
     return n;
 }
 
-inline int pack_da(int dim) { return (int)gtsfm_align_up((size_t)dim + 4, 16); }
+// K width of the packed forms: dim + 5 folded columns, rounded up to an instantiated MFMA depth (NK in {2, 5, 9})
+inline int pack_da(int dim) {
+    const int nk = (dim + 5 + 15) / 16;
+    return 16 * (nk <= 2 ? 2 : nk <= 5 ? 5 : nk <= 9 ? 9 : nk);
+}
 inline int pack_kpad(int kmax) { return (int)gtsfm_align_up((size_t)kmax, kRowsPerPass); }
+
+template <int NK, bool kFast>
+int launch_mnn_t(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
+                 int kpad, int kmax, int ib, uint2* rowres, uint2* colres, hipStream_t stream) {
+    using Cfg = MnnCfg<NK>;
+    const size_t lds = 2 * kSub * Cfg::kBufBytes + 2 * kWaves * kSuper * 2 * sizeof(uint32_t) +
+                       (size_t)kmax * sizeof(uint2);
+    if (lds > 160 * 1024) return GTSFM_ERR_ARG;
+    if (lds > 65536)
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)mnn_mfma_kernel<NK, kFast>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((mnn_mfma_kernel<NK, kFast>), dim3(n_pairs), dim3(kThreads), lds, stream, a_form, b_form,
+                       counts, pairs, kpad, kmax, ib, rowres, colres);
+    return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
+}
 
 template <int NK>
 int launch_mnn(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
                int kpad, int kmax, int ib, uint2* rowres, uint2* colres, hipStream_t stream) {
-    using Cfg = MnnCfg<NK>;
-    const size_t lds = 2 * Cfg::kBufBytes + 2 * kWaves * kChunk * 2 * sizeof(uint32_t) + (size_t)kmax * sizeof(uint2);
-    if (lds > 65536)
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)mnn_mfma_kernel<NK>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(mnn_mfma_kernel<NK>, dim3(n_pairs), dim3(kThreads), lds, stream, a_form, b_form, counts, pairs,
-                       kpad, kmax, ib, rowres, colres);
-    return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
+    if (ib <= 12)
+        return launch_mnn_t<NK, true>(a_form, b_form, counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream);
+    return launch_mnn_t<NK, false>(a_form, b_form, counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream);
 }
 
 template <bool kPacked>
@@ -521,7 +569,7 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
 
     if (mode == GTSFM_MATCH_INT_F16) {
         const int da = pack_da(dim), kpad = pack_kpad(kmax), nk = da / 16, ib = index_bits(kmax);
-        if (dim > 140 || kmax > kMaxKmaxPacked) return GTSFM_ERR_ARG;
+        if (dim > 139 || kmax > kMaxKmaxPacked) return GTSFM_ERR_ARG;
         const size_t form_bytes = gtsfm_align_up((size_t)n_img * kpad * da * sizeof(_Float16), 256);
         _Float16* a_form = (_Float16*)ws;
         _Float16* b_form = (_Float16*)(ws + form_bytes);

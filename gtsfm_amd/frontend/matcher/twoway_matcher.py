@@ -32,7 +32,7 @@ class MatchingDistanceType(Enum):
 def select_match_mode(d1: np.ndarray, d2: np.ndarray) -> int:
     """INT_F16 (MFMA) when every descriptor is an integer in [0, 1023] with |d|^2 < 2^19, else EXACT_F32."""
     kmax = max(d1.shape[0], d2.shape[0])
-    if d1.shape[1] > 140 or kmax > 8192:
+    if d1.shape[1] > 139 or kmax > 8192:
         return native.GTSFM_MATCH_EXACT_F32
     for d in (d1, d2):
         if d.size == 0:

@@ -55,7 +55,7 @@ const char* gtsfm_hip_target(void);
  * mode GTSFM_MATCH_INT_F16:   integer-valued descriptors in [0, 1023] with squared norm < 2^19
  *      (every SIFT descriptor). One fp16 MFMA distance GEMM per pair with the norms folded into
  *      extra K columns, fused row/column top-2. Exact integer arithmetic: bit-identical to EXACT_F32.
- *      kmax <= 8192, dim <= 140. (EXACT_F32: kmax <= 65535.)
+ *      kmax <= 8192, dim <= 139. (EXACT_F32: kmax <= 65535.)
  * ---------------------------------------------------------------------------------------------- */
 #define GTSFM_MATCH_EXACT_F32 0
 #define GTSFM_MATCH_INT_F16 1
