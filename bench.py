@@ -9,13 +9,12 @@ value = all pairs pushed through match + verify (every rank) / max-over-ranks st
 
 Workload (configs[1] of BASELINE.json): 100 rendered 1920x1080 images, all 4950 pairs, at N=1. For N GPUs the scene
 grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work constant: "scaling": "weak"); pairs are
-dealt round-robin, images round-robin for extraction.
+cut into one contiguous block per rank, images dealt round-robin for extraction.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--images n] [--kpts 2048] [--no-cpu-baseline]
 """
 import argparse
 import json
-import math
 import os
 import sys
 import time
@@ -28,6 +27,7 @@ sys.path.insert(0, REPO)
 
 from gtsfm_amd import device as hip  # noqa: E402
 from gtsfm_amd import native, synthetic  # noqa: E402
+from gtsfm_amd.frontend import sharding  # noqa: E402
 
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0
@@ -52,13 +52,14 @@ class FrontEnd:
                  world: int):
         self.rank, self.world, self.kpts, self.n_img = rank, world, kpts, n_img
         self.dev = scene_images.device
-        self.n_per = int(math.ceil(n_img / world))
+        self.n_per = sharding.images_per_rank(n_img, world)
         self.local_images = scene_images  # (n_local, H, W, 3): images rank, rank + world, ...
-        # global slot of original image i: (i % world) * n_per + i // world  (rank-major after the all-gather)
-        slot = np.array([(i % world) * self.n_per + i // world for i in range(n_img)], dtype=np.int64)
-        pairs = synthetic.all_pairs(n_img)
+        slot = sharding.global_slots(n_img, world)  # rank-major rows after the all-gather
+        pairs = sharding.all_pairs(n_img)
         self.total_pairs = len(pairs)
-        mine = pairs[rank::world]
+        block = sharding.rank_pairs(pairs, world, rank)
+        self.pair_id_base = int(block[0]) if len(block) else 0  # global pair index keys the RANSAC sampler
+        mine = pairs[block]
         self.my_pairs_orig = mine
         self.pairs = torch.from_numpy(slot[mine].astype(np.int32)).to(self.dev)
         intr = np.zeros((world * self.n_per, 3))
@@ -73,28 +74,15 @@ class FrontEnd:
         feats = hip.sift_extract(self.local_images, self.kpts)
         if "t1" in ev:
             ev["t1"].record()
-        n_local = self.local_images.shape[0]
-        if self.world > 1:
-            pad = self.n_per - n_local
-            xy, desc, cnt = feats.xy, feats.desc, feats.count
-            if pad:
-                xy = torch.cat([xy, xy.new_zeros((pad,) + xy.shape[1:])])
-                desc = torch.cat([desc, desc.new_zeros((pad,) + desc.shape[1:])])
-                cnt = torch.cat([cnt, cnt.new_zeros((pad,))])
-            xy_all = torch.empty((self.world * self.n_per,) + xy.shape[1:], dtype=xy.dtype, device=self.dev)
-            desc_all = torch.empty((self.world * self.n_per,) + desc.shape[1:], dtype=desc.dtype, device=self.dev)
-            cnt_all = torch.empty((self.world * self.n_per,), dtype=cnt.dtype, device=self.dev)
-            torch.distributed.all_gather_into_tensor(desc_all, desc.contiguous())
-            torch.distributed.all_gather_into_tensor(xy_all, xy.contiguous())
-            torch.distributed.all_gather_into_tensor(cnt_all, cnt.contiguous())
-        else:
-            xy_all, desc_all, cnt_all = feats.xy, feats.desc, feats.count
+        # the one exchange step (N > 1): padded feature blocks, rank-major
+        xy_all, desc_all, cnt_all = sharding.allgather_features((feats.xy, feats.desc, feats.count), self.n_per)
         if "t2" in ev:
             ev["t2"].record()
         idx, mcnt = hip.match_pairs(desc_all, cnt_all, self.pairs, RATIO, native.GTSFM_MATCH_INT_F16)
         if "t3" in ev:
             ev["t3"].record()
-        res = hip.ransac_essential(xy_all, self.intr, self.pairs, idx, mcnt, THRESH_PX)
+        res = hip.ransac_essential(xy_all, self.intr, self.pairs, idx, mcnt, THRESH_PX,
+                                   pair_id_base=self.pair_id_base)
         if "t4" in ev:
             ev["t4"].record()
         # inlier-support processor (frontend/inlier_support_processor.py:73-87), on device
@@ -204,12 +192,7 @@ def main():
         stage_ms["verify"].append(evs["t3"].elapsed_time(evs["t4"]))
     stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
     counts = feats.count
-    if world > 1:
-        counts_all = torch.empty((world * fe.n_per,), dtype=counts.dtype, device=dev)
-        cnt_local = torch.cat([counts, counts.new_zeros((fe.n_per - counts.shape[0],))])
-        torch.distributed.all_gather_into_tensor(counts_all, cnt_local)
-    else:
-        counts_all = counts
+    (counts_all,) = sharding.allgather_features((counts,), fe.n_per)
     c = counts_all.to(torch.float64)
     pairs = fe.pairs.long()
     match_flops = float((2.0 * c[pairs[:, 0]] * c[pairs[:, 1]] * 128).sum().item())
@@ -235,7 +218,7 @@ def main():
         "config": {"workload": f"C2: {n_img} synthetic {args.width}x{args.height} images, all "
                                f"{fe.total_pairs} pairs, SIFT {args.kpts} kpts/img, ratio {RATIO}, "
                                f"5-pt RANSAC {THRESH_PX}px", "images": n_img, "pairs": fe.total_pairs,
-                   "kpts": args.kpts, "parallelism": f"pairs round-robin x{world}"},
+                   "kpts": args.kpts, "parallelism": f"pair blocks x{world}"},
         "pairs_passing_isp": int(ok.item()),
         "stage_ms": {k: round(v, 3) for k, v in stage.items()},
         "roofline": roof,

@@ -3,7 +3,7 @@
 
 extern "C" {
 
-int gtsfm_hip_abi_version(void) { return 100; }
+int gtsfm_hip_abi_version(void) { return 101; }
 
 const char* gtsfm_hip_target(void) { return "gfx950"; }
 

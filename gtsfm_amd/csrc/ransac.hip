@@ -867,7 +867,8 @@ __global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int 
 __global__ __launch_bounds__(64, 1) void ransac_solve_kernel(const int* __restrict__ match_count, int mcap,
                                                              const double2* __restrict__ x1n_all,
                                                              const double2* __restrict__ x2n_all, uint64_t seed,
-                                                             int pair_id_base, const PairState* __restrict__ st,
+                                                             int pair_id_base, const int* __restrict__ pair_ids,
+                                                             const PairState* __restrict__ st,
                                                              double* __restrict__ cand, int* __restrict__ nsol) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int p = blockIdx.x, lane = threadIdx.x;
@@ -881,7 +882,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve_kernel(const int* __restri
     double* cout = cand + ((size_t)p * kBatch + lane) * (kMaxSol * 9);
     int ns = 0;
     int idx[5];
-    if (sample5(seed, pair_id_base + p, done + lane, M, idx)) {
+    if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + lane, M, idx)) {
         double s1[10], s2[10];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -1103,7 +1104,7 @@ size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap) {
 int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
                            int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
                            double thr_px, double prob, int max_iters, uint64_t seed, int pair_id_base,
-                           void* d_workspace, size_t workspace_bytes, double* d_E, double* d_R, double* d_t,
+                           const int* d_pair_ids, void* d_workspace, size_t workspace_bytes, double* d_E, double* d_R, double* d_t,
                            int* d_n_inliers, int* d_status, int* d_n_hyp, uint8_t* d_inlier_mask, void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
     if (n_pairs == 0) return GTSFM_OK;
@@ -1134,7 +1135,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     const int n_batches = (max_iters + kBatch - 1) / kBatch;
     for (int b = 0; b < n_batches; ++b) {
         hipLaunchKernelGGL(ransac_solve_kernel, dim3(n_pairs), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
-                           x2n, seed, pair_id_base, st, cand, nsol);
+                           x2n, seed, pair_id_base, d_pair_ids, st, cand, nsol);
         hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics,
                            d_match_count, mcap, pts, thr_px, prob, cand, nsol, st);
     }

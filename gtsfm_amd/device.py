@@ -67,13 +67,15 @@ class RansacResult:
 def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
                      match_count: torch.Tensor, thr_px: float, prob: float = 0.999999, max_iters: int = 1000,
                      seed: int = native.RANSAC_DEFAULT_SEED, pair_id_base: int = 0,
-                     stream: Optional[torch.cuda.Stream] = None) -> RansacResult:
+                     pair_ids: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None) -> RansacResult:
     """Batched 5-point RANSAC + LO + recoverPose for every pair (gtsfm_ransac_E_batched).
 
     Args:
         kp_xy: (n_img, kmax, 2) float32 keypoint pixels; intrinsics: (n_img, 3) float64 (f, u0, v0).
         pairs: (P, 2) int32; match_idx: (P, mcap, 2) int32 (uint32 values); match_count: (P,) int32.
+        pair_ids: optional (P,) int32 sampler keys (default pair_id_base + p).
     """
+    assert pair_ids is None or (pair_ids.dtype == torch.int32 and pair_ids.is_cuda and pair_ids.numel() == pairs.shape[0])
     assert kp_xy.is_cuda and kp_xy.dtype == torch.float32 and kp_xy.dim() == 3 and kp_xy.is_contiguous()
     assert intrinsics.dtype == torch.float64 and intrinsics.is_contiguous()
     assert match_idx.dtype == torch.int32 and match_idx.is_contiguous() and match_count.dtype == torch.int32
@@ -95,7 +97,7 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
             ws.record_stream(stream)
         rc = L.gtsfm_ransac_E_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
                                       _ptr(match_count), mcap, float(thr_px), float(prob), int(max_iters), int(seed),
-                                      int(pair_id_base), _ptr(ws), ws.numel(), _ptr(E), _ptr(R), _ptr(t),
+                                      int(pair_id_base), _ptr(pair_ids), _ptr(ws), ws.numel(), _ptr(E), _ptr(R), _ptr(t),
                                       _ptr(n_inl), _ptr(status), _ptr(n_hyp), _ptr(mask),
                                       native.stream_handle(stream))
         native.check(rc, "gtsfm_ransac_E_batched")

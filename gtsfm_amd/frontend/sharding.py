@@ -1,0 +1,93 @@
+"""Multi-GPU layout of the all-pairs front-end: one process per GPU, one exchange step.
+
+The reference fans the front-end out as Dask tasks, one per image and one per pair
+(det_desc_correspondence_generator.py:64-80, two_view_estimator.py:568-584), and pickles ~2 MiB of features into
+every pair task. Here each rank owns a fixed share instead:
+
+- extraction: image i -> rank i mod world (rank-local order i // world);
+- exchange: ONE all-gather of the fixed-size per-rank feature blocks (descriptors, keypoint xy, counts), padded to
+  `n_per = ceil(n / world)` images per rank, so the gathered tensor is rank-major: image i sits in global slot
+  `(i mod world) * n_per + i // world`;
+- matching + verification: the lexicographic (i1, i2) pair list cut into `world` contiguous blocks (rank r owns
+  pairs [r * per, min((r + 1) * per, P)), per = ceil(P / world)). Consecutive pairs of a block share i1, so its
+  descriptors stay in L2, and every pair keeps its global index, which keys the RANSAC sampler: a pair's result
+  does not depend on the world size.
+
+Nothing here is GPU specific: the same functions run on CPU tensors under the gloo backend (tests/test_sharding.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+
+def images_per_rank(n_img: int, world: int) -> int:
+    return int(math.ceil(n_img / max(world, 1)))
+
+
+def local_images(n_img: int, world: int, rank: int) -> np.ndarray:
+    """Original indices of the images rank `rank` extracts, in its local order."""
+    return np.arange(rank, n_img, world, dtype=np.int64)
+
+
+def global_slots(n_img: int, world: int) -> np.ndarray:
+    """slot[i] = row of image i in the gathered (world * n_per, ...) feature tensors."""
+    i = np.arange(n_img, dtype=np.int64)
+    return (i % world) * images_per_rank(n_img, world) + i // world
+
+
+def all_pairs(n_img: int) -> np.ndarray:
+    """Every (i1 < i2) pair in lexicographic order, (P, 2) int64 (the exhaustive pair list of the reference)."""
+    i1, i2 = np.triu_indices(n_img, k=1)
+    return np.stack([i1, i2], axis=1).astype(np.int64)
+
+
+def rank_pairs(pairs: np.ndarray, world: int, rank: int) -> np.ndarray:
+    """Positions (into `pairs`) of the pairs rank `rank` matches and verifies: one contiguous block."""
+    per = int(math.ceil(len(pairs) / max(world, 1)))
+    return np.arange(min(rank * per, len(pairs)), min((rank + 1) * per, len(pairs)), dtype=np.int64)
+
+
+def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
+                       group: Optional[torch.distributed.ProcessGroup] = None) -> Tuple[torch.Tensor, ...]:
+    """Pads each rank's (n_local, ...) feature tensors to n_per rows and all-gathers them rank-major.
+
+    One collective per tensor (descriptors dominate: 2048 x 128 x 4 B per image). With world == 1 the inputs are
+    returned unchanged.
+    """
+    world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
+    if world == 1:
+        return tuple(tensors)
+    out = []
+    for t in tensors:
+        pad = n_per - t.shape[0]
+        if pad < 0:
+            raise ValueError(f"rank holds {t.shape[0]} images, more than n_per={n_per}")
+        if pad:
+            t = torch.cat([t, t.new_zeros((pad,) + tuple(t.shape[1:]))])
+        t = t.contiguous()
+        g = torch.empty((world * n_per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        torch.distributed.all_gather_into_tensor(g, t, group=group)
+        out.append(g)
+    return tuple(out)
+
+
+def gather_pair_results(local: torch.Tensor, n_pairs: int,
+                        group: Optional[torch.distributed.ProcessGroup] = None) -> torch.Tensor:
+    """Reassembles a per-pair result tensor (rank r holds the block rank_pairs(.., r)) into pair order everywhere.
+
+    Used only where a caller wants every rank to hold every pair's compact result (R, t, counts); the bench and the
+    batched drop-ins copy each rank's results to the host instead.
+    """
+    world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
+    if world == 1:
+        return local
+    per = int(math.ceil(n_pairs / world))
+    pad = per - local.shape[0]
+    buf = torch.cat([local, local.new_zeros((pad,) + tuple(local.shape[1:]))]) if pad else local.contiguous()
+    g = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    torch.distributed.all_gather_into_tensor(g, buf, group=group)
+    return g[:n_pairs]

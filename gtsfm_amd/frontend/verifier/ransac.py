@@ -8,7 +8,7 @@ relative pose from the essential matrix and the verified correspondences (utils/
 The estimation runs in libgtsfm_hip.so (gtsfm_ransac_E_batched): 5-point RANSAC with deterministic sampling,
 iterative local optimisation and the recoverPose cheirality vote, one wavefront per pair.
 """
-from typing import Optional, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -70,3 +70,60 @@ class Ransac(VerifierBase):
         R = res.R[0].cpu().numpy()
         t = res.t[0].cpu().numpy()
         return geometry.Rot3(R), geometry.Unit3(t), v_corr_idxs, inlier_ratio
+
+    def verify_batch(
+        self,
+        keypoints_list: Sequence[Keypoints],
+        putative_corr_idxs_dict: Dict[Tuple[int, int], np.ndarray],
+        camera_intrinsics: Sequence,
+        chunk: int = 8192,
+    ) -> Dict[Tuple[int, int], Tuple[Optional[object], Optional[object], np.ndarray, float]]:
+        """verify() of every pair of the dict through ONE gtsfm_ransac_E_batched launch sequence per chunk.
+
+        Same guards and failure tuple as verify(), and the same sampler stream: every pair is keyed by pair id 0,
+        as a one-pair verify() call is, so the batch reproduces verify() pair for pair.
+        """
+        if not self._use_intrinsics_in_verification:
+            raise NotImplementedError(
+                "The fundamental-matrix (8-point, use_intrinsics_in_verification=False) path is not on the MI355X "
+                "verifier yet; use use_intrinsics_in_verification=True")
+        native.require_gpu()
+        dev = torch.device("cuda")
+        n = len(keypoints_list)
+        kmax = max([len(k) for k in keypoints_list] + [1])
+        kp = np.zeros((n, kmax, 2), np.float32)
+        for i, k in enumerate(keypoints_list):
+            kp[i, : len(k)] = k.coordinates
+        kp_d = torch.from_numpy(kp).to(dev)
+        intr = np.stack([geometry.calibration_params(c) if c is not None else np.zeros(3) for c in camera_intrinsics])
+        intr_d = torch.from_numpy(intr).to(dev)
+        keys = list(putative_corr_idxs_dict.keys())
+        out: Dict[Tuple[int, int], Tuple[Optional[object], Optional[object], np.ndarray, float]] = {}
+        for s in range(0, len(keys), chunk):
+            blk = keys[s: s + chunk]
+            run = [p for p in blk if len(putative_corr_idxs_dict[p]) >= max(self._min_matches, 6)]
+            for p in blk:
+                out[p] = self._failure_result
+            if not run:
+                continue
+            mcap = max(len(putative_corr_idxs_dict[p]) for p in run)
+            mi = np.zeros((len(run), mcap, 2), np.int32)
+            cnt = np.zeros(len(run), np.int32)
+            for j, p in enumerate(run):
+                m = np.asarray(putative_corr_idxs_dict[p]).reshape(-1, 2)
+                mi[j, : len(m)] = m.astype(np.int64).astype(np.int32)
+                cnt[j] = len(m)
+            res = device.ransac_essential(
+                kp_d, intr_d, torch.tensor(run, dtype=torch.int32, device=dev), torch.from_numpy(mi).to(dev),
+                torch.from_numpy(cnt).to(dev), self._estimation_threshold_px, RANSAC_SUCCESS_PROB, RANSAC_MAX_ITERS,
+                self._seed, pair_ids=torch.zeros(len(run), dtype=torch.int32, device=dev))
+            status = res.status.cpu().numpy()
+            mask = res.mask.cpu().numpy().astype(bool)
+            R, t = res.R.cpu().numpy(), res.t.cpu().numpy()
+            for j, p in enumerate(run):
+                if status[j] != native.RANSAC_STATUS_OK:
+                    continue
+                m = np.asarray(putative_corr_idxs_dict[p]).reshape(-1, 2)
+                mk = mask[j, : len(m)]
+                out[p] = (geometry.Rot3(R[j]), geometry.Unit3(t[j]), m[np.flatnonzero(mk)], float(np.mean(mk)))
+        return out

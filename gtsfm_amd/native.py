@@ -52,7 +52,7 @@ SIGNATURES = {
     "gtsfm_ransac_E_batched": (
         c_int,
         [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_int,
-         c_uint64, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_uint64, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p],
     ),
     "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),

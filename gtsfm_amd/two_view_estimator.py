@@ -1,0 +1,142 @@
+"""Two-view estimation of every putative pair: verify -> report -> inlier-support filter.
+
+Drop-in for gtsfm/two_view_estimator.py: `TwoViewEstimator.run_2view` (:276-351), `generate_two_view_report`
+(:354-393), `compute_relative_pose_metrics` (:396-420) and `run_two_view_estimator_as_futures` (:531-587), with
+the same TWO_VIEW_OUTPUT 6-tuple (i2Ri1, i2Ui1, v_corr_idxs, pre-BA report, post-BA report, post-ISP report).
+
+`run_two_view_estimator_as_futures` is where the batching happens: instead of one Dask task per pair, every pair
+goes through ONE batched RANSAC launch sequence (Ransac.verify_batch) and only the cheap report / ISP logic runs per
+pair on the host. Two-view bundle adjustment (:311-337) is out of scope for this build: with
+`bundle_adjust_2view=True` the post-BA outputs equal the pre-BA ones, exactly as the reference's own else-branch
+(:338-342) produces them, and a warning says so once.
+"""
+from __future__ import annotations
+
+import dataclasses
+import logging
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+from scipy.spatial.transform import Rotation
+
+from gtsfm_amd.common import geometry
+from gtsfm_amd.common.keypoints import Keypoints
+from gtsfm_amd.common.two_view_estimation_report import TwoViewEstimationReport
+from gtsfm_amd.frontend.inlier_support_processor import InlierSupportProcessor
+from gtsfm_amd.frontend.verifier.verifier_base import VerifierBase
+
+logger = logging.getLogger(__name__)
+
+TWO_VIEW_OUTPUT = Tuple[Optional[Any], Optional[Any], np.ndarray, TwoViewEstimationReport, TwoViewEstimationReport,
+                        TwoViewEstimationReport]
+
+
+def _pose(camera) -> Optional[Tuple[np.ndarray, np.ndarray]]:
+    """(wRi, wti) of a GT camera: a gtsam camera (.pose()), or a 4x4 / 3x4 wTi matrix."""
+    if camera is None:
+        return None
+    if hasattr(camera, "pose"):
+        p = camera.pose()
+        return np.asarray(p.rotation().matrix(), np.float64), np.asarray(p.translation(), np.float64).reshape(3)
+    T = np.asarray(camera, np.float64)
+    return T[:3, :3], T[:3, 3]
+
+
+def compute_relative_pose_metrics(i2Ri1, i2Ui1, gt_camera_i1, gt_camera_i2) -> Tuple[Optional[float], Optional[float]]:
+    """Rotation angle of i2Ri1^-1 * i2Ri1_gt and angle between i2Ui1 and the GT direction, in degrees
+    (two_view_estimator.py:396-420 with geometry_comparisons.py:266-309)."""
+    p1, p2 = _pose(gt_camera_i1), _pose(gt_camera_i2)
+    if p1 is None or p2 is None:
+        return None, None
+    (R1, t1), (R2, t2) = p1, p2
+    R_gt = R2.T @ R1  # i2Ti1 = wTi2^-1 * wTi1
+    t_gt = R2.T @ (t1 - t2)
+    R_err = U_err = None
+    if i2Ri1 is not None:
+        rel = geometry.rotation_matrix(i2Ri1).T @ R_gt
+        R_err = float(np.rad2deg(np.linalg.norm(Rotation.from_matrix(rel).as_rotvec())))
+    if i2Ui1 is not None:
+        u = t_gt / np.linalg.norm(t_gt)
+        U_err = float(np.rad2deg(np.arccos(np.clip(np.dot(geometry.unit_vector(i2Ui1), u), -1, 1))))
+    return R_err, U_err
+
+
+def generate_two_view_report(inlier_ratio_est_model: float, v_corr_idxs: np.ndarray, R_error_deg=None,
+                             U_error_deg=None, v_corr_idxs_inlier_mask_gt=None,
+                             reproj_error_gt_model=None) -> TwoViewEstimationReport:
+    if v_corr_idxs_inlier_mask_gt is not None and reproj_error_gt_model is not None:
+        num_gt = np.count_nonzero(v_corr_idxs_inlier_mask_gt)
+        ratio_gt = num_gt / v_corr_idxs.shape[0] if len(v_corr_idxs) > 0 else 0.0
+        inl_err = np.mean(reproj_error_gt_model[v_corr_idxs_inlier_mask_gt])
+        out_err = np.nanmean(reproj_error_gt_model[np.logical_not(v_corr_idxs_inlier_mask_gt)])
+    else:
+        num_gt, ratio_gt, inl_err, out_err = 0, float("nan"), float("nan"), float("nan")
+    return TwoViewEstimationReport(
+        inlier_ratio_est_model=inlier_ratio_est_model, num_inliers_est_model=v_corr_idxs.shape[0],
+        num_inliers_gt_model=num_gt, inlier_ratio_gt_model=ratio_gt,
+        v_corr_idxs_inlier_mask_gt=v_corr_idxs_inlier_mask_gt, v_corr_idxs=v_corr_idxs, R_error_deg=R_error_deg,
+        U_error_deg=U_error_deg, reproj_error_gt_model=reproj_error_gt_model,
+        inlier_avg_reproj_error_gt_model=inl_err, outlier_avg_reproj_error_gt_model=out_err)
+
+
+class TwoViewEstimator:
+    def __init__(self, verifier: VerifierBase, inlier_support_processor: InlierSupportProcessor,
+                 bundle_adjust_2view: bool, eval_threshold_px: float, triangulation_options: Any = None,
+                 bundle_adjust_2view_maxiters: int = 100, ba_reproj_error_thresholds: List[Optional[float]] = [0.5]
+                 ) -> None:
+        self._verifier = verifier
+        self.processor = inlier_support_processor
+        self._bundle_adjust_2view = bundle_adjust_2view
+        self._corr_metric_dist_threshold = eval_threshold_px
+        self._triangulation_options = triangulation_options
+        self._ba_reproj_error_thresholds = ba_reproj_error_thresholds
+        self._bundle_adjust_2view_maxiters = bundle_adjust_2view_maxiters
+        if bundle_adjust_2view:
+            logger.warning("two-view BA is not part of the MI355X front-end (SURVEY.md §8 f2): post-BA = pre-BA")
+
+    def get_corr_metric_dist_threshold(self) -> float:
+        return self._corr_metric_dist_threshold
+
+    def _finish(self, verified, gt_camera_i1, gt_camera_i2) -> TWO_VIEW_OUTPUT:
+        """Report + (skipped) BA + inlier-support processor for one verifier result (:298-351)."""
+        i2Ri1, i2Ui1, v_corr, ratio = verified
+        R_err, U_err = (None, None)
+        if gt_camera_i1 is not None and gt_camera_i2 is not None:
+            R_err, U_err = compute_relative_pose_metrics(i2Ri1, i2Ui1, gt_camera_i1, gt_camera_i2)
+        pre_ba_report = generate_two_view_report(ratio, v_corr, R_error_deg=R_err, U_error_deg=U_err)
+        post_ba_report = dataclasses.replace(pre_ba_report)
+        post_isp = self.processor.run_inlier_support(i2Ri1, i2Ui1, v_corr, post_ba_report)
+        return post_isp[0], post_isp[1], post_isp[2], pre_ba_report, post_ba_report, post_isp[3]
+
+    def run_2view(self, keypoints_i1: Keypoints, keypoints_i2: Keypoints, putative_corr_idxs: np.ndarray,
+                  camera_intrinsics_i1, camera_intrinsics_i2, i2Ti1_prior=None, gt_camera_i1=None,
+                  gt_camera_i2=None, gt_scene_mesh=None) -> TWO_VIEW_OUTPUT:
+        verified = self._verifier.verify(keypoints_i1, keypoints_i2, putative_corr_idxs, camera_intrinsics_i1,
+                                         camera_intrinsics_i2)
+        return self._finish(verified, gt_camera_i1, gt_camera_i2)
+
+
+def run_two_view_estimator_as_futures(
+    client,
+    two_view_estimator: TwoViewEstimator,
+    keypoints_list: Sequence[Keypoints],
+    putative_corr_idxs_dict: Dict[Tuple[int, int], np.ndarray],
+    camera_intrinsics: Sequence,
+    relative_pose_priors: Dict[Tuple[int, int], Any],
+    gt_cameras: Sequence[Optional[Any]],
+    gt_scene_mesh: Optional[Any],
+) -> Dict[Tuple[int, int], TWO_VIEW_OUTPUT]:
+    """All pairs of `putative_corr_idxs_dict` -> TWO_VIEW_OUTPUT, one batched verifier launch for all of them.
+
+    `client` is accepted for signature compatibility (two_view_estimator.py:531-540) and unused.
+    """
+    verifier = two_view_estimator._verifier
+    gt = list(gt_cameras) if gt_cameras is not None else [None] * len(keypoints_list)
+    if hasattr(verifier, "verify_batch"):
+        verified = verifier.verify_batch(keypoints_list, putative_corr_idxs_dict, camera_intrinsics)
+    else:
+        verified = {(i1, i2): verifier.verify(keypoints_list[i1], keypoints_list[i2], m, camera_intrinsics[i1],
+                                              camera_intrinsics[i2])
+                    for (i1, i2), m in putative_corr_idxs_dict.items()}
+    return {(i1, i2): two_view_estimator._finish(verified[(i1, i2)], gt[i1], gt[i2])
+            for (i1, i2) in putative_corr_idxs_dict}

@@ -73,7 +73,8 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
  * (Cal3Bundler with k1 = k2 = 0). Putatives per pair: d_match_idx[n_pairs][mcap][2] uint32 keypoint indices
  * and d_match_count[n_pairs] (exactly the matcher's output). Threshold thr_px / max(f1, f2) in normalized
  * coordinates on the squared Sampson distance, success probability `prob`, at most `max_iters` hypotheses
- * (checked per batch of 64); `seed` and pair_id_base + p key the deterministic sampling of pair p.
+ * (checked per batch of 64); `seed` and the pair id key the deterministic sampling of pair p: d_pair_ids[p]
+ * when d_pair_ids is non-NULL (e.g. all 0 to reproduce one-pair calls), else pair_id_base + p.
  * Outputs per pair: E, R (i2Ri1) row-major 3x3, unit t (i2ti1), inlier count, status (0 ok, 1 fewer than
  * 6 putatives, 2 no model), number of hypotheses evaluated (d_n_hyp may be NULL) and the inlier mask
  * d_inlier_mask[n_pairs][mcap] over the putatives in matcher order.
@@ -83,8 +84,8 @@ size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap);
 int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax,
                            const int* d_pairs, int n_pairs, const uint32_t* d_match_idx,
                            const int* d_match_count, int mcap, double thr_px, double prob, int max_iters,
-                           uint64_t seed, int pair_id_base, void* d_workspace, size_t workspace_bytes,
-                           double* d_E, double* d_R, double* d_t, int* d_n_inliers, int* d_status,
+                           uint64_t seed, int pair_id_base, const int* d_pair_ids, void* d_workspace,
+                           size_t workspace_bytes, double* d_E, double* d_R, double* d_t, int* d_n_inliers, int* d_status,
                            int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
