@@ -1148,3 +1148,621 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
 }
 
 }  // extern "C"
+
+// ====================================================================================================================
+// Fundamental-matrix verifier (use_intrinsics_in_verification=False): the restatement in oracle/fundamental.c of
+// cv2.findFundamentalMat(FM_RANSAC, px, 0.999999, 1e6) (frontend/verifier/ransac.py:84-111) + E = K2^T F K1
+// (utils/verification.py:97-110) + recoverPose (utils/verification.py:52-94). Everything below is compiled without
+// FMA contraction and performs the oracle's double operations in the oracle's order, so the GPU reproduces the
+// oracle's samples, minimal models, errors, counts and the final F bit for bit.
+// ====================================================================================================================
+#pragma clang fp contract(off)
+namespace {
+
+constexpr int kFBatch = 64;
+constexpr int kFAttempts = 4;
+constexpr int kFDraws = 16;
+constexpr int kFMaxSol = 3;
+constexpr float kFltEps = 1.19209290e-07f;
+constexpr double kDblEps = 2.220446049250313e-16;
+
+__device__ __forceinline__ bool fm_collinear3(float ax, float ay, float bx, float by, float cx, float cy) {
+    const float dx1 = bx - ax, dy1 = by - ay, dx2 = cx - ax, dy2 = cy - ay;
+    return fabsf(dx2 * dy1 - dy2 * dx1) <= kFltEps * (fabsf(dx1) + fabsf(dy1) + fabsf(dx2) + fabsf(dy2));
+}
+
+// 7 distinct indices without a collinear triple in either image (oracle_sample7)
+__device__ bool sample7(uint64_t seed, int pair, int h, int M, const float4* __restrict__ pts, int* idx) {
+    const uint64_t key = sm_mix(seed ^ sm_mix((uint64_t)(uint32_t)pair));
+    for (int a = 0; a < kFAttempts; ++a) {
+        int n = 0;
+        for (int d = 0; d < kFDraws && n < 7; ++d) {
+            const uint64_t r = sm_mix(key + ((uint64_t)h * kFAttempts + (uint64_t)a) * kFDraws + (uint64_t)d);
+            const int v = (int)(((r >> 32) * (uint64_t)(uint32_t)M) >> 32);
+            bool dup = false;
+            for (int k = 0; k < n; ++k) dup |= (idx[k] == v);
+            if (!dup) idx[n++] = v;
+        }
+        if (n < 7) continue;
+        float4 q[7];
+#pragma unroll
+        for (int k = 0; k < 7; ++k) q[k] = pts[idx[k]];
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < 7; ++i)
+#pragma unroll
+            for (int j = i + 1; j < 7; ++j)
+#pragma unroll
+                for (int k = j + 1; k < 7; ++k)
+                    bad |= fm_collinear3(q[i].x, q[i].y, q[j].x, q[j].y, q[k].x, q[k].y) ||
+                           fm_collinear3(q[i].z, q[i].w, q[j].z, q[j].w, q[k].z, q[k].w);
+        if (!bad) return true;
+    }
+    return false;
+}
+
+__device__ __forceinline__ double fm_cubic_eval(const double* a, double x) { return ((x + a[0]) * x + a[1]) * x + a[2]; }
+
+__device__ int fm_bisect(const double* a, double lo, double hi, double* root) {
+    double flo = fm_cubic_eval(a, lo), fhi = fm_cubic_eval(a, hi);
+    if (flo == 0.0) { *root = lo; return 1; }
+    if (fhi == 0.0) { *root = hi; return 1; }
+    if ((flo < 0.0) == (fhi < 0.0)) return 0;
+    for (int it = 0; it < 200; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (!(mid > lo && mid < hi)) break;
+        const double fm = fm_cubic_eval(a, mid);
+        if (fm == 0.0) { lo = hi = mid; break; }
+        if ((fm < 0.0) == (flo < 0.0)) { lo = mid; flo = fm; } else { hi = mid; }
+    }
+    *root = 0.5 * (lo + hi);
+    return 1;
+}
+
+__device__ int fm_solve_cubic(const double* c, double* r) {
+    const double m = fmax(fmax(fabs(c[0]), fabs(c[1])), fmax(fabs(c[2]), fabs(c[3])));
+    if (!(m > 0.0)) return 0;
+    if (fabs(c[0]) <= 1e-12 * m) {
+        if (fabs(c[1]) <= 1e-12 * m) {
+            if (fabs(c[2]) <= 1e-12 * m) return 0;
+            r[0] = -c[3] / c[2];
+            return 1;
+        }
+        const double d = c[2] * c[2] - 4.0 * c[1] * c[3];
+        if (d < 0.0) return 0;
+        const double s = sqrt(d);
+        const double x1 = (-c[2] - s) / (2.0 * c[1]), x2 = (-c[2] + s) / (2.0 * c[1]);
+        r[0] = fmin(x1, x2);
+        r[1] = fmax(x1, x2);
+        return r[1] > r[0] ? 2 : 1;
+    }
+    const double a[3] = {c[1] / c[0], c[2] / c[0], c[3] / c[0]};
+    const double B = 1.0 + fmax(fabs(a[0]), fmax(fabs(a[1]), fabs(a[2])));
+    const double disc = a[0] * a[0] - 3.0 * a[1];
+    int n = 0;
+    if (disc <= 0.0) return fm_bisect(a, -B, B, r);
+    const double sd = sqrt(disc);
+    double k1 = (-a[0] - sd) / 3.0, k2 = (-a[0] + sd) / 3.0;
+    k1 = fmin(fmax(k1, -B), B);
+    k2 = fmin(fmax(k2, -B), B);
+    const double edges[4] = {-B, k1, k2, B};
+    for (int s = 0; s < 3; ++s) {
+        double x;
+        if (!(edges[s + 1] >= edges[s])) continue;
+        if (fm_bisect(a, edges[s], edges[s + 1], &x)) {
+            if (n == 0 || x > r[n - 1]) r[n++] = x;
+        }
+    }
+    return n;
+}
+
+// F = T2^T Fn T1 (Hartley de-normalisation), scaled so F33 = 1 when |F33| > DBL_EPSILON
+__device__ __forceinline__ void fm_denormalize(const double* Fn, double s1, double c1x, double c1y, double s2,
+                                               double c2x, double c2y, double* F) {
+    const double T1[9] = {s1, 0.0, -s1 * c1x, 0.0, s1, -s1 * c1y, 0.0, 0.0, 1.0};
+    const double T2[9] = {s2, 0.0, -s2 * c2x, 0.0, s2, -s2 * c2y, 0.0, 0.0, 1.0};
+    double G[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc)
+            G[3 * r + cc] = Fn[3 * r + 0] * T1[0 * 3 + cc] + Fn[3 * r + 1] * T1[1 * 3 + cc] + Fn[3 * r + 2] * T1[2 * 3 + cc];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc)
+            F[3 * r + cc] = T2[0 * 3 + r] * G[0 * 3 + cc] + T2[1 * 3 + r] * G[1 * 3 + cc] + T2[2 * 3 + r] * G[2 * 3 + cc];
+    if (fabs(F[8]) > kDblEps) {
+        const double inv = 1.0 / F[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) F[i] = F[i] * inv;
+        F[8] = 1.0;
+    }
+}
+
+// 7-point solver (oracle_seven_point); the 7x9 system stays in registers (row swaps by selects)
+__device__ int seven_point(const float4* __restrict__ pts, const int* idx, double* Fs) {
+    float4 q[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) q[k] = pts[idx[k]];
+    double c1x = 0.0, c1y = 0.0, c2x = 0.0, c2y = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        c1x += q[k].x; c1y += q[k].y; c2x += q[k].z; c2y += q[k].w;
+    }
+    c1x /= 7.0; c1y /= 7.0; c2x /= 7.0; c2y /= 7.0;
+    double d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double ax = q[k].x - c1x, ay = q[k].y - c1y, bx = q[k].z - c2x, by = q[k].w - c2y;
+        d1 += sqrt(ax * ax + ay * ay);
+        d2 += sqrt(bx * bx + by * by);
+    }
+    if (!(d1 > 1e-12) || !(d2 > 1e-12)) return 0;
+    const double s1 = 1.4142135623730951 * 7.0 / d1, s2 = 1.4142135623730951 * 7.0 / d2;
+    double A[7][9];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        const double u1 = (q[k].x - c1x) * s1, v1 = (q[k].y - c1y) * s1;
+        const double u2 = (q[k].z - c2x) * s2, v2 = (q[k].w - c2y) * s2;
+        A[k][0] = u2 * u1; A[k][1] = u2 * v1; A[k][2] = u2;
+        A[k][3] = v2 * u1; A[k][4] = v2 * v1; A[k][5] = v2;
+        A[k][6] = u1; A[k][7] = v1; A[k][8] = 1.0;
+    }
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        int pr = c;
+        double best = fabs(A[c][c]);
+#pragma unroll
+        for (int r = c + 1; r < 7; ++r)
+            if (fabs(A[r][c]) > best) { best = fabs(A[r][c]); pr = r; }
+        if (!(best > 1e-10)) return 0;
+#pragma unroll
+        for (int r = c + 1; r < 7; ++r) {
+            const bool sw = (r == pr);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) {
+                const double a = A[c][j], b = A[r][j];
+                A[c][j] = sw ? b : a;
+                A[r][j] = sw ? a : b;
+            }
+        }
+        const double inv = 1.0 / A[c][c];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) A[c][j] = A[c][j] * inv;
+#pragma unroll
+        for (int r = 0; r < 7; ++r) {
+            if (r == c) continue;
+            const double f = A[r][c];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) A[r][j] = A[r][j] - f * A[c][j];
+        }
+    }
+    double f1[9], f2[9];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) { f1[r] = -A[r][7]; f2[r] = -A[r][8]; }
+    f1[7] = 1.0; f1[8] = 0.0;
+    f2[7] = 0.0; f2[8] = 1.0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f1[i] = f1[i] - f2[i];
+    double c[4];
+    double t0 = f2[4] * f2[8] - f2[5] * f2[7];
+    double t1 = f2[3] * f2[8] - f2[5] * f2[6];
+    double t2 = f2[3] * f2[7] - f2[4] * f2[6];
+    c[3] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2;
+    c[2] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2 - f1[3] * (f2[1] * f2[8] - f2[2] * f2[7]) +
+           f1[4] * (f2[0] * f2[8] - f2[2] * f2[6]) - f1[5] * (f2[0] * f2[7] - f2[1] * f2[6]) +
+           f1[6] * (f2[1] * f2[5] - f2[2] * f2[4]) - f1[7] * (f2[0] * f2[5] - f2[2] * f2[3]) +
+           f1[8] * (f2[0] * f2[4] - f2[1] * f2[3]);
+    t0 = f1[4] * f1[8] - f1[5] * f1[7];
+    t1 = f1[3] * f1[8] - f1[5] * f1[6];
+    t2 = f1[3] * f1[7] - f1[4] * f1[6];
+    c[1] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2 - f2[3] * (f1[1] * f1[8] - f1[2] * f1[7]) +
+           f2[4] * (f1[0] * f1[8] - f1[2] * f1[6]) - f2[5] * (f1[0] * f1[7] - f1[1] * f1[6]) +
+           f2[6] * (f1[1] * f1[5] - f1[2] * f1[4]) - f2[7] * (f1[0] * f1[5] - f1[2] * f1[3]) +
+           f2[8] * (f1[0] * f1[4] - f1[1] * f1[3]);
+    c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
+    double roots[3];
+    const int nr = fm_solve_cubic(c, roots);
+    for (int k = 0; k < nr; ++k) {
+        double Fn[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) Fn[i] = roots[k] * f1[i] + f2[i];
+        fm_denormalize(Fn, s1, c1x, c1y, s2, c2x, c2y, Fs + 9 * k);
+    }
+    return nr;
+}
+
+// FMEstimatorCallback::computeError (oracle_f_error)
+__device__ __forceinline__ float fm_error(const double* F, float4 p) {
+    const double x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+    double a = F[0] * x1 + F[1] * y1 + F[2];
+    double b = F[3] * x1 + F[4] * y1 + F[5];
+    double c = F[6] * x1 + F[7] * y1 + F[8];
+    const double s2 = 1.0 / (a * a + b * b);
+    const double d2 = x2 * a + y2 * b + c;
+    a = F[0] * x2 + F[3] * y2 + F[6];
+    b = F[1] * x2 + F[4] * y2 + F[7];
+    c = F[2] * x2 + F[5] * y2 + F[8];
+    const double s1 = 1.0 / (a * a + b * b);
+    const double d1 = x1 * a + y1 * b + c;
+    return (float)fmax(d1 * d1 * s1, d2 * d2 * s2);
+}
+
+// inlier count of F at thr2, -1 once it provably cannot exceed floor_count
+__device__ int fm_wave_count(const double* F, const float4* __restrict__ pts, int M, float thr2, int floor_count,
+                             int lane) {
+    int c = 0;
+    for (int base = 0; base < M; base += 64) {
+        const int i = base + lane;
+        bool in = false;
+        if (i < M) in = fm_error(F, pts[i]) <= thr2;
+        c += __popcll(__ballot(in));
+        const int remaining = M - (base + 64);
+        if (remaining > 0 && c + remaining <= floor_count) return -1;
+    }
+    return c;
+}
+
+// serial cyclic Jacobi (oracle fm_jacobi), one lane
+template <int N>
+__device__ void fm_jacobi(double* a, double* w, double* V) {
+    for (int i = 0; i < N * N; ++i) V[i] = 0.0;
+    for (int i = 0; i < N; ++i) V[i * N + i] = 1.0;
+    for (int sweep = 0; sweep < 30; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) off += a[p * N + q] * a[p * N + q];
+        if (!(off > 1e-300)) break;
+        for (int p = 0; p < N; ++p)
+            for (int q = p + 1; q < N; ++q) {
+                const double apq = a[p * N + q];
+                if (fabs(apq) < 1e-300) continue;
+                const double theta = (a[q * N + q] - a[p * N + p]) / (2.0 * apq);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
+                for (int k = 0; k < N; ++k) {
+                    const double akp = a[k * N + p], akq = a[k * N + q];
+                    a[k * N + p] = c * akp - sn * akq;
+                    a[k * N + q] = sn * akp + c * akq;
+                }
+                for (int k = 0; k < N; ++k) {
+                    const double apk = a[p * N + k], aqk = a[q * N + k];
+                    a[p * N + k] = c * apk - sn * aqk;
+                    a[q * N + k] = sn * apk + c * aqk;
+                }
+                for (int k = 0; k < N; ++k) {
+                    const double vkp = V[k * N + p], vkq = V[k * N + q];
+                    V[k * N + p] = c * vkp - sn * vkq;
+                    V[k * N + q] = sn * vkp + c * vkq;
+                }
+            }
+    }
+    for (int i = 0; i < N; ++i) w[i] = a[i * N + i];
+}
+
+// normalised 8-point on the masked correspondences (oracle_eight_point), one lane, arrays in LDS scratch
+__device__ bool eight_point_serial(const float4* __restrict__ pts, const uint8_t* __restrict__ mask, int M,
+                                   double* AtA /*81*/, double* V /*81*/, double* F) {
+    int n = 0;
+    double c1x = 0.0, c1y = 0.0, c2x = 0.0, c2y = 0.0;
+    for (int i = 0; i < M; ++i) {
+        if (!mask[i]) continue;
+        const float4 p = pts[i];
+        c1x += p.x; c1y += p.y; c2x += p.z; c2y += p.w;
+        ++n;
+    }
+    if (n < 8) return false;
+    c1x /= n; c1y /= n; c2x /= n; c2y /= n;
+    double d1 = 0.0, d2 = 0.0;
+    for (int i = 0; i < M; ++i) {
+        if (!mask[i]) continue;
+        const float4 p = pts[i];
+        const double ax = p.x - c1x, ay = p.y - c1y, bx = p.z - c2x, by = p.w - c2y;
+        d1 += sqrt(ax * ax + ay * ay);
+        d2 += sqrt(bx * bx + by * by);
+    }
+    if (!(d1 > 1e-12) || !(d2 > 1e-12)) return false;
+    const double s1 = 1.4142135623730951 * n / d1, s2 = 1.4142135623730951 * n / d2;
+    for (int k = 0; k < 81; ++k) AtA[k] = 0.0;
+    for (int i = 0; i < M; ++i) {
+        if (!mask[i]) continue;
+        const float4 p = pts[i];
+        const double u1 = (p.x - c1x) * s1, v1 = (p.y - c1y) * s1;
+        const double u2 = (p.z - c2x) * s2, v2 = (p.w - c2y) * s2;
+        const double r[9] = {u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, 1.0};
+#pragma unroll
+        for (int a = 0; a < 9; ++a)
+#pragma unroll
+            for (int b = a; b < 9; ++b) AtA[a * 9 + b] = AtA[a * 9 + b] + r[a] * r[b];
+    }
+    for (int a = 0; a < 9; ++a)
+        for (int b = 0; b < a; ++b) AtA[a * 9 + b] = AtA[b * 9 + a];
+    double w[9];
+    fm_jacobi<9>(AtA, w, V);
+    int kmin = 0;
+    for (int k = 1; k < 9; ++k)
+        if (w[k] < w[kmin]) kmin = k;
+    double Fn[9];
+    for (int e = 0; e < 9; ++e) Fn[e] = V[e * 9 + kmin];
+    double FtF[9], w3[3], V3[9];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b)
+            FtF[a * 3 + b] = Fn[0 * 3 + a] * Fn[0 * 3 + b] + Fn[1 * 3 + a] * Fn[1 * 3 + b] + Fn[2 * 3 + a] * Fn[2 * 3 + b];
+    fm_jacobi<3>(FtF, w3, V3);
+    int k3 = 0;
+    for (int k = 1; k < 3; ++k)
+        if (w3[k] < w3[k3]) k3 = k;
+    const double v[3] = {V3[0 * 3 + k3], V3[1 * 3 + k3], V3[2 * 3 + k3]};
+    for (int r = 0; r < 3; ++r) {
+        const double fv = Fn[3 * r] * v[0] + Fn[3 * r + 1] * v[1] + Fn[3 * r + 2] * v[2];
+        for (int c = 0; c < 3; ++c) Fn[3 * r + c] = Fn[3 * r + c] - fv * v[c];
+    }
+    fm_denormalize(Fn, s1, c1x, c1y, s2, c2x, c2y, F);
+    return true;
+}
+
+// Gather the putatives of every pair: pixel float4 (x1, y1, x2, y2) for estimation and K-normalised double2 for
+// recoverPose (utils/verification.py:78-79).
+__global__ void fmat_gather_kernel(const float* __restrict__ kp_xy, const double* __restrict__ intr, int kmax,
+                                   const int* __restrict__ pairs, const uint32_t* __restrict__ match_idx,
+                                   const int* __restrict__ match_count, int mcap, float4* __restrict__ pts,
+                                   double2* __restrict__ x1n, double2* __restrict__ x2n) {
+    const int p = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int M = match_count[p];
+    if (i >= M) return;
+    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+    const uint32_t a = match_idx[((size_t)p * mcap + i) * 2], b = match_idx[((size_t)p * mcap + i) * 2 + 1];
+    const float* k1 = kp_xy + ((size_t)i1 * kmax + a) * 2;
+    const float* k2 = kp_xy + ((size_t)i2 * kmax + b) * 2;
+    const size_t o = (size_t)p * mcap + i;
+    pts[o] = make_float4(k1[0], k1[1], k2[0], k2[1]);
+    x1n[o] = make_double2(((double)k1[0] - intr[3 * i1 + 1]) / intr[3 * i1], ((double)k1[1] - intr[3 * i1 + 2]) / intr[3 * i1]);
+    x2n[o] = make_double2(((double)k2[0] - intr[3 * i2 + 1]) / intr[3 * i2], ((double)k2[1] - intr[3 * i2 + 2]) / intr[3 * i2]);
+}
+
+struct FOutputs {
+    double* F;
+    double* E;
+    double* R;
+    double* t;
+    int* n_inliers;
+    int* status;
+    int* n_hyp;
+    uint8_t* mask;
+};
+
+// One wave per pair: 7-point RANSAC (M >= 15) or LMedS (8 <= M < 15) in batches of 64 hypotheses (lane = hypothesis),
+// candidates scored in (hypothesis, root) order, then the 8-point refit, E = K2^T F K1 and recoverPose. Every lane
+// runs the same number of batches (niters is wave-uniform), so the loop always drains.
+__global__ __launch_bounds__(64) void fmat_ransac_kernel(const int* __restrict__ pairs, const double* __restrict__ intr,
+                                                         const int* __restrict__ match_count, int mcap,
+                                                         const float4* __restrict__ pts_all,
+                                                         const double2* __restrict__ x1n_all,
+                                                         const double2* __restrict__ x2n_all, double thr_px,
+                                                         double prob, int max_iters, uint64_t seed, int pair_id_base,
+                                                         const int* __restrict__ pair_ids, FOutputs out) {
+    __shared__ double candF[kFBatch * kFMaxSol * 9];
+    __shared__ int cand_n[kFBatch];
+    __shared__ double scratch[81 * 2 + 9];
+    __shared__ int refit_ok;
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int M = match_count[p];
+    uint8_t* mask = out.mask + (size_t)p * mcap;
+    if (M < 8) {  // verifier_base.py:39-44 (NUM_MATCHES_REQ_F_MATRIX)
+        for (int i = lane; i < M; i += 64) mask[i] = 0;
+        if (lane == 0) {
+            out.n_inliers[p] = 0;
+            out.status[p] = 1;
+            if (out.n_hyp) out.n_hyp[p] = 0;
+        }
+        return;
+    }
+    const float4* pts = pts_all + (size_t)p * mcap;
+    const int pid = pair_ids ? pair_ids[p] : pair_id_base + p;
+    const bool lmeds = M < 15;
+    int niters = lmeds ? update_num_iters(prob, 0.45, 7, max_iters) : max_iters;
+    if (niters < 1) niters = 1;
+    const float thr2 = (float)(thr_px * thr_px);
+    int done = 0, best = -1;
+    bool have = false;
+    float min_median = 3.402823466e+38f;
+    double bestF[9];
+    for (int e = 0; e < 9; ++e) bestF[e] = 0.0;
+    while (done < niters) {
+        int idx[7];
+        int ns = 0;
+        if (sample7(seed, pid, done + lane, M, pts, idx)) ns = seven_point(pts, idx, candF + lane * kFMaxSol * 9);
+        cand_n[lane] = ns;
+        __syncthreads();
+        for (int hl = 0; hl < kFBatch; ++hl) {
+            const int nsh = cand_n[hl];
+            for (int s = 0; s < nsh; ++s) {
+                const double* F = candF + (hl * kFMaxSol + s) * 9;
+                double Fr[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) Fr[e] = F[e];
+                if (lmeds) {
+                    const float err = lane < M ? fm_error(Fr, pts[lane]) : 0.0f;
+                    int rank = 0;
+                    for (int j = 0; j < M; ++j) {
+                        const float ej = __shfl(err, j);
+                        rank += (ej < err || (ej == err && j < lane)) ? 1 : 0;
+                    }
+                    const uint64_t who = __ballot(lane < M && rank == M / 2);
+                    const float med = __shfl(err, (int)__ffsll((unsigned long long)who) - 1);
+                    if (med < min_median) {
+                        min_median = med;
+#pragma unroll
+                        for (int e = 0; e < 9; ++e) bestF[e] = Fr[e];
+                        have = true;
+                    }
+                } else {
+                    const int floor_c = best > 6 ? best : 6;
+                    const int c = fm_wave_count(Fr, pts, M, thr2, floor_c, lane);
+                    if (c > floor_c) {
+                        best = c;
+#pragma unroll
+                        for (int e = 0; e < 9; ++e) bestF[e] = Fr[e];
+                        have = true;
+                    }
+                }
+            }
+        }
+        __syncthreads();  // candF / cand_n are rewritten by the next batch
+        done += kFBatch;
+        if (!lmeds && best > 0) {
+            const int upd = update_num_iters(prob, (double)(M - best) / M, 7, niters);
+            if (upd < niters) niters = upd;
+        }
+    }
+    int cnt = -1;
+    if (have) {
+        double th = thr_px;
+        if (lmeds) {
+            th = 2.5 * 1.4826 * (1.0 + 5.0 / (M - 7)) * sqrt((double)min_median);
+            if (th < 0.001) th = 0.001;
+        }
+        const float th2 = (float)(th * th);
+        auto write_mask = [&](const double* F) {
+            int c = 0;
+            for (int i = lane; i < M; i += 64) {
+                const bool in = fm_error(F, pts[i]) <= th2;
+                mask[i] = in ? 1 : 0;
+                c += in ? 1 : 0;
+            }
+            for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
+            return c;
+        };
+        cnt = write_mask(bestF);
+        if (cnt >= 8) {
+            __syncthreads();  // mask visible to lane 0
+            if (lane == 0) refit_ok = eight_point_serial(pts, mask, M, scratch, scratch + 81, scratch + 162) ? 1 : 0;
+            __syncthreads();
+            if (refit_ok) {
+                double Fr[9];
+#pragma unroll
+                for (int e = 0; e < 9; ++e) Fr[e] = scratch[162 + e];
+                const int cr = fm_wave_count(Fr, pts, M, th2, -1, lane);
+                if (cr >= cnt) {
+#pragma unroll
+                    for (int e = 0; e < 9; ++e) bestF[e] = Fr[e];
+                    cnt = write_mask(bestF);
+                }
+            }
+        }
+        if (lmeds && cnt < 7) cnt = -1;
+    }
+    if (cnt < 0) {
+        for (int i = lane; i < M; i += 64) mask[i] = 0;
+        if (lane == 0) {
+            out.n_inliers[p] = 0;
+            out.status[p] = 2;
+            if (out.n_hyp) out.n_hyp[p] = done;
+        }
+        return;
+    }
+    __syncthreads();  // final mask visible to every lane
+    // E = K2^T F K1 (utils/verification.py:97-110)
+    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
+    const double K1[9] = {intr[3 * i1], 0.0, intr[3 * i1 + 1], 0.0, intr[3 * i1], intr[3 * i1 + 2], 0.0, 0.0, 1.0};
+    const double K2[9] = {intr[3 * i2], 0.0, intr[3 * i2 + 1], 0.0, intr[3 * i2], intr[3 * i2 + 2], 0.0, 0.0, 1.0};
+    double FK[9], E[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            FK[3 * r + c] = bestF[3 * r + 0] * K1[0 * 3 + c] + bestF[3 * r + 1] * K1[1 * 3 + c] + bestF[3 * r + 2] * K1[2 * 3 + c];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            E[3 * r + c] = K2[0 * 3 + r] * FK[0 * 3 + c] + K2[1 * 3 + r] * FK[1 * 3 + c] + K2[2 * 3 + r] * FK[2 * 3 + c];
+    // recoverPose on the K-normalised inliers (same decomposition + cheirality vote as the E path)
+    const double2* x1 = x1n_all + (size_t)p * mcap;
+    const double2* x2 = x2n_all + (size_t)p * mcap;
+    double U[9], sv[3], V[9];
+    svd3(E, U, sv, V);
+    if (det3(U) < 0)
+        for (int k = 0; k < 9; ++k) U[k] = -U[k];
+    if (det3(V) < 0)
+        for (int k = 0; k < 9; ++k) V[k] = -V[k];
+    double R1[9], R2[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            const double uw0 = -U[r * 3 + 1], uw1 = U[r * 3 + 0], uw2 = U[r * 3 + 2];
+            const double uwt0 = U[r * 3 + 1], uwt1 = -U[r * 3 + 0], uwt2 = U[r * 3 + 2];
+            R1[r * 3 + c] = uw0 * V[c * 3 + 0] + uw1 * V[c * 3 + 1] + uw2 * V[c * 3 + 2];
+            R2[r * 3 + c] = uwt0 * V[c * 3 + 0] + uwt1 * V[c * 3 + 1] + uwt2 * V[c * 3 + 2];
+        }
+    const double tp[3] = {U[2], U[5], U[8]};
+    const double tn[3] = {-U[2], -U[5], -U[8]};
+    const int g1 = wave_cheirality(R1, tp, x1, x2, mask, M, lane);
+    const int g2 = wave_cheirality(R2, tp, x1, x2, mask, M, lane);
+    const int g3 = wave_cheirality(R1, tn, x1, x2, mask, M, lane);
+    const int g4 = wave_cheirality(R2, tn, x1, x2, mask, M, lane);
+    const double* Rs;
+    const double* ts;
+    if (g1 >= g2 && g1 >= g3 && g1 >= g4) { Rs = R1; ts = tp; }
+    else if (g2 >= g1 && g2 >= g3 && g2 >= g4) { Rs = R2; ts = tp; }
+    else if (g3 >= g1 && g3 >= g2 && g3 >= g4) { Rs = R1; ts = tn; }
+    else { Rs = R2; ts = tn; }
+    if (lane == 0) {
+        for (int k = 0; k < 9; ++k) {
+            out.F[9 * p + k] = bestF[k];
+            out.E[9 * p + k] = E[k];
+            out.R[9 * p + k] = Rs[k];
+        }
+        for (int k = 0; k < 3; ++k) out.t[3 * p + k] = ts[k];
+        out.n_inliers[p] = cnt;
+        out.status[p] = 0;
+        if (out.n_hyp) out.n_hyp[p] = done;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+static size_t fmat_layout(int n_pairs, int mcap, size_t* off_x1n, size_t* off_x2n) {
+    const size_t n = (size_t)n_pairs * mcap;
+    size_t o = gtsfm_align_up(n * sizeof(float4), 256);
+    *off_x1n = o;
+    o += gtsfm_align_up(n * sizeof(double2), 256);
+    *off_x2n = o;
+    o += gtsfm_align_up(n * sizeof(double2), 256);
+    return o;
+}
+
+size_t gtsfm_ransac_F_workspace_bytes(int n_pairs, int mcap) {
+    if (n_pairs <= 0 || mcap <= 0) return 0;
+    size_t a, b;
+    return fmat_layout(n_pairs, mcap, &a, &b);
+}
+
+int gtsfm_ransac_F_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
+                           int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
+                           double thr_px, double prob, int max_iters, uint64_t seed, int pair_id_base,
+                           const int* d_pair_ids, void* d_workspace, size_t workspace_bytes, double* d_F, double* d_E,
+                           double* d_R, double* d_t, int* d_n_inliers, int* d_status, int* d_n_hyp,
+                           uint8_t* d_inlier_mask, void* stream_v) {
+    hipStream_t stream = (hipStream_t)stream_v;
+    if (n_pairs == 0) return GTSFM_OK;
+    if (!d_kp_xy || !d_intrinsics || !d_pairs || !d_match_idx || !d_match_count || !d_F || !d_E || !d_R || !d_t ||
+        !d_n_inliers || !d_status || !d_inlier_mask || n_img <= 0 || kmax <= 0 || n_pairs < 0 || mcap <= 0 ||
+        max_iters <= 0 || !(thr_px > 0.0))
+        return GTSFM_ERR_ARG;
+    size_t o_x1n, o_x2n;
+    const size_t need = fmat_layout(n_pairs, mcap, &o_x1n, &o_x2n);
+    if (workspace_bytes < need) return GTSFM_ERR_CAPACITY;
+    unsigned char* ws = (unsigned char*)d_workspace;
+    float4* pts = (float4*)ws;
+    double2* x1n = (double2*)(ws + o_x1n);
+    double2* x2n = (double2*)(ws + o_x2n);
+    hipLaunchKernelGGL(fmat_gather_kernel, dim3((mcap + 255) / 256, n_pairs), dim3(256), 0, stream, d_kp_xy,
+                       d_intrinsics, kmax, d_pairs, d_match_idx, d_match_count, mcap, pts, x1n, x2n);
+    const FOutputs o{d_F, d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask};
+    hipLaunchKernelGGL(fmat_ransac_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics, d_match_count,
+                       mcap, pts, x1n, x2n, thr_px, prob, max_iters, seed, pair_id_base, d_pair_ids, o);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    return GTSFM_OK;
+}
+
+}  // extern "C"

@@ -104,6 +104,51 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
     return RansacResult(E[:P], R[:P], t[:P], n_inl[:P], status[:P], n_hyp[:P], mask[:P])
 
 
+class FundamentalResult(RansacResult):
+    """Per-pair F-path outputs: F plus everything RansacResult holds (E = K2^T F K1)."""
+
+    def __init__(self, F, E, R, t, n_inliers, status, n_hyp, mask):
+        super().__init__(E, R, t, n_inliers, status, n_hyp, mask)
+        self.F = F
+
+
+def ransac_fundamental(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
+                       match_count: torch.Tensor, thr_px: float, prob: float = 0.999999, max_iters: int = 1000000,
+                       seed: int = native.RANSAC_DEFAULT_SEED, pair_id_base: int = 0,
+                       pair_ids: Optional[torch.Tensor] = None,
+                       stream: Optional[torch.cuda.Stream] = None) -> FundamentalResult:
+    """Batched 7-point RANSAC / LMedS F estimation + 8-point refit + E + recoverPose (gtsfm_ransac_F_batched).
+
+    Same tensor conventions as ransac_essential; thr_px is in pixels (no focal-length scaling).
+    """
+    assert kp_xy.is_cuda and kp_xy.dtype == torch.float32 and kp_xy.dim() == 3 and kp_xy.is_contiguous()
+    assert intrinsics.dtype == torch.float64 and intrinsics.is_contiguous()
+    assert match_idx.dtype == torch.int32 and match_idx.is_contiguous() and match_count.dtype == torch.int32
+    assert pair_ids is None or (pair_ids.dtype == torch.int32 and pair_ids.is_cuda and pair_ids.numel() == pairs.shape[0])
+    n_img, kmax, _ = kp_xy.shape
+    P = pairs.shape[0]
+    mcap = match_idx.shape[1]
+    dev = kp_xy.device
+    L = native.lib()
+    F = torch.zeros((max(P, 1), 3, 3), dtype=torch.float64, device=dev)
+    E, R = torch.zeros_like(F), torch.zeros_like(F)
+    t = torch.zeros((max(P, 1), 3), dtype=torch.float64, device=dev)
+    n_inl = torch.zeros((max(P, 1),), dtype=torch.int32, device=dev)
+    status, n_hyp = torch.zeros_like(n_inl), torch.zeros_like(n_inl)
+    mask = torch.zeros((max(P, 1), max(mcap, 1)), dtype=torch.uint8, device=dev)
+    if P > 0:
+        ws = _workspace(L.gtsfm_ransac_F_workspace_bytes(P, mcap), dev)
+        if stream is not None:
+            ws.record_stream(stream)
+        rc = L.gtsfm_ransac_F_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
+                                      _ptr(match_count), mcap, float(thr_px), float(prob), int(max_iters), int(seed),
+                                      int(pair_id_base), _ptr(pair_ids), _ptr(ws), ws.numel(), _ptr(F), _ptr(E),
+                                      _ptr(R), _ptr(t), _ptr(n_inl), _ptr(status), _ptr(n_hyp), _ptr(mask),
+                                      native.stream_handle(stream))
+        native.check(rc, "gtsfm_ransac_F_batched")
+    return FundamentalResult(F[:P], E[:P], R[:P], t[:P], n_inl[:P], status[:P], n_hyp[:P], mask[:P])
+
+
 class SiftResult:
     """Per-image SIFT outputs (device tensors): xy (n,k,2), attr (n,k,3) size/angle/response, desc (n,k,128),
     count (n,), n_detected (n,)."""

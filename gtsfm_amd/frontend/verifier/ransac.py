@@ -5,8 +5,10 @@ gtsfm/frontend/verifier/opencv_verifier_base.py:45-109: fewer than 5 (E) / 6 put
 normalised with K; threshold estimation_threshold_px / max(fx1, fx2); inlier mask; inlier ratio = mean(mask);
 relative pose from the essential matrix and the verified correspondences (utils/verification.py:52-94).
 
-The estimation runs in libgtsfm_hip.so (gtsfm_ransac_E_batched): 5-point RANSAC with deterministic sampling,
-iterative local optimisation and the recoverPose cheirality vote, one wavefront per pair.
+The estimation runs in libgtsfm_hip.so: gtsfm_ransac_E_batched (5-point RANSAC with deterministic sampling,
+iterative local optimisation and the recoverPose cheirality vote, one wavefront per pair) when
+use_intrinsics_in_verification=True, gtsfm_ransac_F_batched (7-point RANSAC / LMedS on pixel coordinates, 8-point
+refit, E = K2^T F K1, recoverPose; ransac.py:84-111, utils/verification.py:97-110) otherwise.
 """
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -20,10 +22,11 @@ from gtsfm_amd.frontend.verifier.verifier_base import VerifierBase
 
 RANSAC_SUCCESS_PROB = 0.999999
 RANSAC_MAX_ITERS = 1000  # cv2.findEssentialMat default maxIters
+RANSAC_MAX_ITERS_F = 1000000  # ransac.py:23, passed to cv2.findFundamentalMat
 
 
 class Ransac(VerifierBase):
-    """5-point RANSAC verifier (E path) computed by HIP kernels."""
+    """RANSAC verifier computed by HIP kernels: 5-point E path with intrinsics, 7-point F path without."""
 
     def __init__(self, use_intrinsics_in_verification: bool, estimation_threshold_px: float,
                  seed: int = native.RANSAC_DEFAULT_SEED) -> None:
@@ -38,14 +41,13 @@ class Ransac(VerifierBase):
         camera_intrinsics_i1,
         camera_intrinsics_i2,
     ) -> Tuple[Optional[object], Optional[object], np.ndarray, float]:
-        if not self._use_intrinsics_in_verification:
-            raise NotImplementedError(
-                "The fundamental-matrix (8-point, use_intrinsics_in_verification=False) path is not on the MI355X "
-                "verifier yet; use use_intrinsics_in_verification=True")
         if match_indices.shape[0] < self._min_matches or match_indices.shape[0] < 6:
             return self._failure_result
         native.require_gpu()
         M = match_indices.shape[0]
+        if not self._use_intrinsics_in_verification:
+            return self.verify_batch([keypoints_i1, keypoints_i2], {(0, 1): match_indices},
+                                     [camera_intrinsics_i1, camera_intrinsics_i2])[(0, 1)]
         dev = torch.device("cuda")
         c1 = keypoints_i1.coordinates.astype(np.float32)
         c2 = keypoints_i2.coordinates.astype(np.float32)
@@ -83,10 +85,6 @@ class Ransac(VerifierBase):
         Same guards and failure tuple as verify(), and the same sampler stream: every pair is keyed by pair id 0,
         as a one-pair verify() call is, so the batch reproduces verify() pair for pair.
         """
-        if not self._use_intrinsics_in_verification:
-            raise NotImplementedError(
-                "The fundamental-matrix (8-point, use_intrinsics_in_verification=False) path is not on the MI355X "
-                "verifier yet; use use_intrinsics_in_verification=True")
         native.require_gpu()
         dev = torch.device("cuda")
         n = len(keypoints_list)
@@ -113,10 +111,13 @@ class Ransac(VerifierBase):
                 m = np.asarray(putative_corr_idxs_dict[p]).reshape(-1, 2)
                 mi[j, : len(m)] = m.astype(np.int64).astype(np.int32)
                 cnt[j] = len(m)
-            res = device.ransac_essential(
-                kp_d, intr_d, torch.tensor(run, dtype=torch.int32, device=dev), torch.from_numpy(mi).to(dev),
-                torch.from_numpy(cnt).to(dev), self._estimation_threshold_px, RANSAC_SUCCESS_PROB, RANSAC_MAX_ITERS,
-                self._seed, pair_ids=torch.zeros(len(run), dtype=torch.int32, device=dev))
+            args = (kp_d, intr_d, torch.tensor(run, dtype=torch.int32, device=dev), torch.from_numpy(mi).to(dev),
+                    torch.from_numpy(cnt).to(dev), self._estimation_threshold_px, RANSAC_SUCCESS_PROB)
+            ids = torch.zeros(len(run), dtype=torch.int32, device=dev)
+            if self._use_intrinsics_in_verification:
+                res = device.ransac_essential(*args, RANSAC_MAX_ITERS, self._seed, pair_ids=ids)
+            else:
+                res = device.ransac_fundamental(*args, RANSAC_MAX_ITERS_F, self._seed, pair_ids=ids)
             status = res.status.cpu().numpy()
             mask = res.mask.cpu().numpy().astype(bool)
             R, t = res.R.cpu().numpy(), res.t.cpu().numpy()

@@ -55,6 +55,13 @@ SIGNATURES = {
          c_uint64, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p],
     ),
+    "gtsfm_ransac_F_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "gtsfm_ransac_F_batched": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_int,
+         c_uint64, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p],
+    ),
     "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gtsfm_sift_batched": (
         c_int,

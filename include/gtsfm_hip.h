@@ -89,6 +89,24 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
+ * Verifier, fundamental-matrix path (use_intrinsics_in_verification=False). Replaces Ransac.estimate_F
+ * (gtsfm/frontend/verifier/ransac.py:84-111: cv2.findFundamentalMat(FM_RANSAC, thr_px, 0.999999, 1e6)) and the
+ * F branch of OpencvVerifierBase.verify (opencv_verifier_base.py:90-109: E = K2^T F K1, recoverPose on the
+ * K-normalised inliers). Same inputs as gtsfm_ransac_E_batched; pixel coordinates are used for estimation.
+ * 7-point RANSAC for M >= 15, LMedS for 8 <= M < 15, normalised 8-point refit on the inliers.
+ * Outputs per pair: F (F33 = 1), E, R (i2Ri1), unit t (i2ti1), inlier count, status (0 ok, 1 fewer than 8
+ * putatives, 2 no model), hypotheses drawn (d_n_hyp may be NULL), inlier mask d_inlier_mask[n_pairs][mcap].
+ * ---------------------------------------------------------------------------------------------- */
+size_t gtsfm_ransac_F_workspace_bytes(int n_pairs, int mcap);
+
+int gtsfm_ransac_F_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax,
+                           const int* d_pairs, int n_pairs, const uint32_t* d_match_idx,
+                           const int* d_match_count, int mcap, double thr_px, double prob, int max_iters,
+                           uint64_t seed, int pair_id_base, const int* d_pair_ids, void* d_workspace,
+                           size_t workspace_bytes, double* d_F, double* d_E, double* d_R, double* d_t,
+                           int* d_n_inliers, int* d_status, int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
+
+/* ----------------------------------------------------------------------------------------------
  * Detector-descriptor: SIFT (OpenCV defaults) + top-k by response over a batch of same-sized images.
  *
  * d_images[n_img][H][W][channels] uint8, channels 1 (gray) or 3 (RGB, converted like cv.COLOR_RGB2GRAY).

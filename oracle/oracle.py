@@ -60,6 +60,16 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_sample5.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p]
         l.oracle_recover_pose.restype = ctypes.c_int
         l.oracle_recover_pose.argtypes = [_f64p, _f64p, _f64p, ctypes.c_void_p, ctypes.c_int, _f64p, _f64p]
+    if hasattr(l, "oracle_ransac_F"):
+        l.oracle_ransac_F.restype = ctypes.c_int
+        l.oracle_ransac_F.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                      ctypes.c_uint64, ctypes.c_int, _f64p, _u8p, ctypes.POINTER(ctypes.c_int)]
+        l.oracle_seven_point.restype = ctypes.c_int
+        l.oracle_seven_point.argtypes = [_f32p, _i32p, _f64p]
+        l.oracle_sample7.restype = ctypes.c_int
+        l.oracle_sample7.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _i32p]
+        l.oracle_f_error.restype = ctypes.c_float
+        l.oracle_f_error.argtypes = [_f64p, _f32p]
     if hasattr(l, "oracle_sift_detect_describe"):
         l.oracle_sift_detect_describe.restype = ctypes.c_int
         l.oracle_sift_detect_describe.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
@@ -129,6 +139,52 @@ def ransac_E(x1n: np.ndarray, x2n: np.ndarray, thr: float, prob: float = 0.99999
     if n < 0:
         return None
     return E.reshape(3, 3), mask[:M].copy(), R.reshape(3, 3), t, n, nh.value
+
+
+def seven_point(x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
+    """All fundamental matrices (k,3,3), k <= 3, through 7 pixel correspondences (x1, x2: (7,2))."""
+    pts = np.ascontiguousarray(np.hstack([x1, x2]), np.float32)
+    Fs = np.zeros(27, np.float64)
+    n = lib().oracle_seven_point(pts.ravel(), np.arange(7, dtype=np.int32), Fs)
+    return Fs[: 9 * n].reshape(n, 3, 3)
+
+
+def f_errors(F: np.ndarray, x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
+    """Per-correspondence max squared point-to-epipolar-line distance (float32), as the F verifier scores it."""
+    pts = np.ascontiguousarray(np.hstack([x1, x2]), np.float32)
+    Fd = np.ascontiguousarray(F, np.float64).ravel()
+    return np.array([lib().oracle_f_error(Fd, pts[i].copy()) for i in range(len(pts))], np.float32)
+
+
+def ransac_F(x1: np.ndarray, x2: np.ndarray, thr_px: float, prob: float = 0.999999, max_iters: int = 1000000,
+             seed: int = RANSAC_SEED, pair_id: int = 0):
+    """F path on pixel coordinates: (F (3,3), mask (M,) uint8, n_inliers, n_hypotheses) or None."""
+    x1 = np.ascontiguousarray(x1, np.float32)
+    x2 = np.ascontiguousarray(x2, np.float32)
+    M = x1.shape[0]
+    F = np.zeros(9)
+    mask = np.zeros(max(M, 1), np.uint8)
+    nh = ctypes.c_int(0)
+    n = lib().oracle_ransac_F(x1.ravel(), x2.ravel(), M, thr_px, prob, max_iters, seed, pair_id, F, mask,
+                              ctypes.byref(nh))
+    if n < 0:
+        return None
+    return F.reshape(3, 3), mask[:M].copy(), n, nh.value
+
+
+def verify_F(x1: np.ndarray, x2: np.ndarray, K1: np.ndarray, K2: np.ndarray, thr_px: float, **kw):
+    """opencv_verifier_base.verify with use_intrinsics_in_verification=False: F, E = K2^T F K1, recoverPose on
+    the K-normalised inliers. Returns (R, t, mask, n_inliers) or None."""
+    r = ransac_F(x1, x2, thr_px, **kw)
+    if r is None:
+        return None
+    F, mask, n, _ = r
+    E = K2.T @ F @ K1
+    sel = mask.astype(bool)
+    n1 = (np.asarray(x1, np.float64)[sel] - K1[:2, 2]) / K1[0, 0]
+    n2 = (np.asarray(x2, np.float64)[sel] - K2[:2, 2]) / K2[0, 0]
+    R, t, _ = recover_pose(E, n1, n2)
+    return R, t, mask, n
 
 
 def recover_pose(E: np.ndarray, x1n: np.ndarray, x2n: np.ndarray):

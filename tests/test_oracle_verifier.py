@@ -79,3 +79,51 @@ def test_synthetic_scenes_pose_accuracy(oracle_mod):
 
 def test_too_few_correspondences(oracle_mod):
     assert oracle_mod.ransac_E(np.zeros((5, 2)), np.zeros((5, 2)), 0.01) is None
+
+
+# ---------------------------------------------------------------- fundamental-matrix path (oracle/fundamental.c)
+def test_F_two_plane_scene(oracle_mod):
+    """tests/frontend/verifier/test_ransac.py:22-30 (TestRansacForFundamentalMatrix) on the same two-plane scene:
+    8 putatives -> the LMedS branch; all verified, R and t within 2 deg."""
+    uv1, uv2, R, t = scenes.two_planes_scene(4, 4)
+    Re, te, mask, n = oracle_mod.verify_F(uv1, uv2, np.eye(3), np.eye(3), 0.5)
+    assert n == 8 and mask.all()
+    assert scenes.rotation_angle_deg(R, Re) < 2 and scenes.direction_angle_deg(t, te) < 2
+
+
+def test_F_seven_point_solutions(oracle_mod):
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        kp1, kp2, K, R, t, inl = scenes.random_two_view(rng, 7, 0, noise_px=0.0)
+        Fs = oracle_mod.seven_point(kp1, kp2)
+        assert 1 <= len(Fs) <= 3
+        Kinv = np.linalg.inv(K)
+        Fgt = Kinv.T @ scenes.skew(t) @ R @ Kinv
+        Fgt /= Fgt[2, 2]
+        h1, h2 = np.c_[kp1, np.ones(7)], np.c_[kp2, np.ones(7)]
+        for F in Fs:
+            assert F[2, 2] == 1.0
+            assert np.abs(oracle_mod.f_errors(F, kp1, kp2)).max() < 1e-6
+            assert abs(np.linalg.det(F / np.linalg.norm(F))) < 1e-9
+        # the true F is one of the roots
+        assert min(np.linalg.norm(F - Fgt) / np.linalg.norm(Fgt) for F in Fs) < 1e-5
+
+
+def test_F_synthetic_scenes_pose_accuracy(oracle_mod):
+    rng = np.random.default_rng(5)
+    for _ in range(6):
+        kp1, kp2, K, R, t, inl = scenes.random_two_view(rng, 300, 200)
+        r = oracle_mod.verify_F(kp1, kp2, K, K, 4.0, max_iters=100000)
+        assert r is not None
+        Re, te, mask, n = r
+        assert (mask.astype(bool) & inl).sum() >= 0.9 * inl.sum()
+        assert scenes.rotation_angle_deg(R, Re) < 3.0
+        assert scenes.direction_angle_deg(t, te) < 10.0
+
+
+def test_F_lmeds_branch_and_guards(oracle_mod):
+    rng = np.random.default_rng(9)
+    kp1, kp2, K, R, t, inl = scenes.random_two_view(rng, 12, 0, noise_px=0.0)
+    F, mask, n, nh = oracle_mod.ransac_F(kp1, kp2, 1.0)
+    assert n == 12 and mask.all() and nh >= 64  # M < 15: LMedS with its fixed iteration count
+    assert oracle_mod.ransac_F(kp1[:7], kp2[:7], 1.0) is None  # M < 8
