@@ -180,3 +180,43 @@ def sift_extract(images: torch.Tensor, max_kpts: int, stream: Optional[torch.cud
                               _ptr(out.desc), _ptr(out.count), _ptr(out.n_detected), native.stream_handle(stream))
     native.check(rc, "gtsfm_sift_batched")
     return out
+
+
+class SuperPointResult:
+    """Per-image SuperPoint outputs (device tensors): xy (n,k,2) float32 (x, y), scores (n,k), desc (n,k,256),
+    count (n,), n_detected (n,)."""
+
+    def __init__(self, xy, scores, desc, count, n_detected):
+        self.xy, self.scores, self.desc, self.count, self.n_detected = xy, scores, desc, count, n_detected
+
+
+def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: int, keypoint_threshold: float = 0.005,
+                       nms_radius: int = 4, remove_borders: int = 4,
+                       stream: Optional[torch.cuda.Stream] = None) -> SuperPointResult:
+    """SuperPoint on a batch of same-sized uint8 images (n, H, W) gray or (n, H, W, 3) RGB (gtsfm_superpoint_batched).
+
+    weights: the packed fp32 blob (gtsfm_amd.frontend.detector_descriptor.superpoint.pack_superpoint_weights).
+    """
+    assert images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous()
+    assert weights.is_cuda and weights.dtype == torch.float32 and weights.is_contiguous()
+    L = native.lib()
+    assert weights.numel() == L.gtsfm_superpoint_weights_floats()
+    n, H, W = images.shape[0], images.shape[1], images.shape[2]
+    C = 1 if images.dim() == 3 else images.shape[3]
+    dev = images.device
+    out = SuperPointResult(torch.zeros((n, max_kpts, 2), dtype=torch.float32, device=dev),
+                           torch.zeros((n, max_kpts), dtype=torch.float32, device=dev),
+                           torch.empty((n, max_kpts, 256), dtype=torch.float32, device=dev),
+                           torch.zeros((n,), dtype=torch.int32, device=dev),
+                           torch.zeros((n,), dtype=torch.int32, device=dev))
+    if n == 0:
+        return out
+    ws = _workspace(L.gtsfm_superpoint_workspace_bytes(n, H, W, max_kpts), dev)
+    if stream is not None:
+        ws.record_stream(stream)
+    rc = L.gtsfm_superpoint_batched(_ptr(images), n, H, W, C, _ptr(weights), max_kpts, float(keypoint_threshold),
+                                    int(nms_radius), int(remove_borders), _ptr(ws), ws.numel(), _ptr(out.xy),
+                                    _ptr(out.scores), _ptr(out.desc), _ptr(out.count), _ptr(out.n_detected),
+                                    native.stream_handle(stream))
+    native.check(rc, "gtsfm_superpoint_batched")
+    return out

@@ -62,6 +62,13 @@ SIGNATURES = {
          c_uint64, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p, c_void_p],
     ),
+    "gtsfm_superpoint_weights_floats": (c_size_t, []),
+    "gtsfm_superpoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "gtsfm_superpoint_batched": (
+        c_int,
+        [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_size_t, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gtsfm_sift_batched": (
         c_int,

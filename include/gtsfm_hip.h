@@ -123,6 +123,30 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
                        void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_attr, float* d_desc,
                        int* d_counts, int* d_n_detected, void* stream);
 
+/* ----------------------------------------------------------------------------------------------
+ * SuperPoint detector-descriptor. Replaces SuperPointDetectorDescriptor.detect_and_describe
+ * (gtsfm/frontend/detector_descriptor/superpoint.py:48-74) and the network it wraps
+ * (thirdparty/SuperGluePretrainedNetwork/models/superpoint.py:145-202), batched over n same-sized images
+ * d_images[n][H][W][C] (C = 1 gray or 3 RGB -> cv COLOR_RGB2GRAY fixed point), scaled by 1/255.
+ * d_weights: packed fp32 blob of gtsfm_superpoint_weights_floats() floats, layers in the order
+ *   conv1a, conv1b, conv2a, conv2b, conv3a, conv3b, conv4a, conv4b, [convPa | convDa], convPb, convDb
+ * each as W[k*k][cin][cout_pad] (W[ky*k+kx][ci][co] = torch weight[co][ci][ky][kx]) followed by bias[cout_pad];
+ * (k, cin, cout_pad) = (3,1,64) (3,64,64) (3,64,64) (3,64,64) (3,64,128) (3,128,128) (3,128,128) (3,128,128)
+ * (3,128,512: Pa in 0..255, Da in 256..511) (1,256,128: 65 used) (1,256,256); padded outputs are zero.
+ * Detection: softmax over 65, 8x8 depth-to-space, simple_nms(nms_radius), score > keypoint_threshold, border
+ * remove_borders; the max_kpts highest scores are kept (ties by raster order) and emitted in raster order
+ * (the reference's own order when max_kpts >= detections). Outputs: d_xy[n][max_kpts][2] (x, y) float,
+ * d_scores[n][max_kpts], d_desc[n][max_kpts][256] unit-norm, d_count[n], d_n_detected[n] (may be NULL).
+ * ---------------------------------------------------------------------------------------------- */
+size_t gtsfm_superpoint_weights_floats(void);
+
+size_t gtsfm_superpoint_workspace_bytes(int n, int H, int W, int max_kpts);
+
+int gtsfm_superpoint_batched(const uint8_t* d_images, int n, int H, int W, int C, const float* d_weights,
+                             int max_kpts, float keypoint_threshold, int nms_radius, int remove_borders,
+                             void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_scores, float* d_desc,
+                             int* d_count, int* d_n_detected, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

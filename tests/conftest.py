@@ -6,8 +6,11 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(REPO, "tests", "golden")
+TESTS = os.path.join(REPO, "tests")
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
+if TESTS not in sys.path:
+    sys.path.append(TESTS)  # test helper modules (superpoint_weights, scenes)
 
 
 def pytest_configure(config):

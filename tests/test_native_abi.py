@@ -2,6 +2,8 @@
 import os
 import re
 
+import numpy as np
+
 from tests.conftest import REPO
 
 
@@ -34,3 +36,18 @@ def test_workspace_queries_without_gpu():
     ws = lib.gtsfm_match_workspace_bytes(100, 2048, 128, 4950, native.GTSFM_MATCH_INT_F16)
     assert ws > 2 * 4950 * 2048 * 8
     assert lib.gtsfm_match_workspace_bytes(0, 2048, 128, 10, 1) == 0
+
+
+def test_superpoint_weight_blob_layout():
+    """The packed blob the Python side builds has exactly the size the library expects (include/gtsfm_hip.h)."""
+    from gtsfm_amd import native
+    from gtsfm_amd.frontend.detector_descriptor.superpoint import pack_superpoint_weights
+    from superpoint_weights import superpoint_state_dict
+
+    sd = superpoint_state_dict(0)
+    blob = pack_superpoint_weights(sd)
+    assert blob.dtype == np.float32 and blob.size == native.lib().gtsfm_superpoint_weights_floats()
+    # conv1a occupies the first 9*64 weights + 64 biases: W[ky*3+kx][0][co] = weight[co][0][ky][kx]
+    w = sd["conv1a.weight"]
+    np.testing.assert_array_equal(blob[: 9 * 64].reshape(9, 64), w[:, 0].reshape(64, 9).T)
+    np.testing.assert_array_equal(blob[9 * 64: 9 * 64 + 64], sd["conv1a.bias"])
