@@ -1,0 +1,683 @@
+// SuperGlue matcher on gfx950: thirdparty/SuperGluePretrainedNetwork/models/superglue.py:228-283 as driven by
+// gtsfm/frontend/matcher/superglue_matcher.py:43-111 (20 Sinkhorn iterations, match threshold 0.2), batched over
+// image pairs.
+//
+//   keypoint normalisation + MLP encoder (with eval BatchNorm) -> 18 x {self, cross} attentional propagation
+//   (4-head attention d = 256, MLP 512 -> 512 -> 256, residual) -> final projection -> scores / 16
+//   -> log-space optimal transport with a dustbin -> mutual argmax + threshold.
+//
+// Layout: every (pair, side) owns a kmax x C row-major (point-major) feature block, so each 1x1 Conv1d is a
+// batched GEMM  Y[n][co] = sum_ci X[n][ci] W^T[ci][co]  on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, exact
+// fp32 products and sums: the network matches the fp32 torch reference up to summation order). Heads are stored
+// head-major (channel h * 64 + d; the reference's view(b, 64, 4, n) interleaves them as 4 d + h — the host packs
+// the q/k/v/merge weights accordingly). Attention is one fused kernel (online softmax, v_mfma_f32_16x16x4_f32):
+// the K1 x K2 probability matrix never reaches HBM. The Sinkhorn matrix (K1 + 1) x (K2 + 1) does, once per pair.
+#include <float.h>
+
+#include "common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kD = 256;     // descriptor_dim
+constexpr int kHeads = 4;
+constexpr int kHd = 64;     // per-head dim
+
+// ------------------------------------------------------------------ packed weights (include/gtsfm_hip.h)
+// GEMM weights are W^T[cin][cout] row-major. Encoder layers: W^T (cin_pad x cout), bias, bn_scale, bn_shift
+// (the last encoder layer has no BN). GNN layer: Wqkv^T (256 x 768, columns [q | k | v], head-major), bqkv,
+// Wm^T (256 x 256, rows head-major), bm, W1^T (512 x 512: rows 0..255 act on x, 256..511 on the message), b1,
+// bn1 scale, bn1 shift, W2^T (512 x 256), b2. Then final_proj W^T (256 x 256), bias, and bin_score (1 float).
+constexpr int kEncIn[5] = {16, 32, 64, 128, 256};  // cin (the 3 encoder inputs zero-padded to 16)
+constexpr int kEncOut[5] = {32, 64, 128, 256, 256};
+
+__host__ __device__ constexpr size_t enc_floats(int i) {
+    return (size_t)kEncIn[i] * kEncOut[i] + kEncOut[i] + (i < 4 ? 2 * kEncOut[i] : 0);
+}
+__host__ __device__ constexpr size_t enc_total() {
+    size_t o = 0;
+    for (int i = 0; i < 5; ++i) o += enc_floats(i);
+    return o;
+}
+constexpr size_t kLayerFloats = (size_t)256 * 768 + 768 + 256 * 256 + 256 + 512 * 512 + 512 * 3 + 512 * 256 + 256;
+__host__ __device__ constexpr size_t sg_weights_floats(int n_layers) {
+    return enc_total() + (size_t)n_layers * kLayerFloats + 256 * 256 + 256 + 1;
+}
+
+// ------------------------------------------------------------------ batched GEMM on fp32 MFMA
+constexpr int kGemmThreads = 256;
+constexpr int kKc = 16;  // K chunk staged in LDS
+
+struct GemmArgs {
+    const float* A;   // A[z][m][k] (k < Ksplit), row stride lda, batch stride a_batch
+    long lda, a_batch;
+    const float* A2;  // A2[z][m][k - Ksplit] (k >= Ksplit)
+    long lda2, a2_batch;
+    int Ksplit;
+    const float* B;   // b_trans = 0: B[z][k][n] (ldb); 1: B[z][n][k]
+    long ldb, b_batch;
+    int b_trans;
+    const float* bias, *bn_scale, *bn_shift;  // per output column, may be null
+    int relu;
+    float alpha;      // applied last (before the residual add)
+    float* C;         // C[z][m][n], row stride ldc
+    long ldc, c_batch;
+    int residual;     // C += result
+    int M, N, K;
+    const int* m_lim; // per-batch valid rows / columns (may be null)
+    const int* n_lim;
+    int lim_stride;   // index of batch z into m_lim / n_lim: z * lim_stride (+1 for n_lim)
+};
+
+// 64 x 64 output tile per workgroup; wave w computes rows 32 (w & 1) .., columns 32 (w >> 1) ..
+__global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
+    __shared__ float As[64 * (kKc + 1)];
+    __shared__ float Bs[kKc * 64];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int z = blockIdx.z;
+    const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+    int Mv = g.M, Nv = g.N;
+    if (g.m_lim) Mv = min(Mv, g.m_lim[z * g.lim_stride]);
+    if (g.n_lim) Nv = min(Nv, g.n_lim[z * g.lim_stride + 1]);
+    if (m0 >= Mv || n0 >= Nv) return;
+    const float* A = g.A + z * g.a_batch;
+    const float* A2 = g.A2 ? g.A2 + z * g.a2_batch : nullptr;
+    const float* B = g.B + z * g.b_batch;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r = lane & 31, kh = lane >> 5;
+    f32x16 acc = {};
+    for (int k0 = 0; k0 < g.K; k0 += kKc) {
+        // A tile: 64 rows x 16 k (float4 per thread)
+        {
+            const int row = tid >> 2, q = tid & 3;
+            const int gm = m0 + row, gk = k0 + 4 * q;
+            f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (gm < g.M) {
+                if (gk < g.Ksplit) v = *(const f32x4_t*)(A + (long)gm * g.lda + gk);
+                else v = *(const f32x4_t*)(A2 + (long)gm * g.lda2 + (gk - g.Ksplit));
+            }
+            float* d = As + row * (kKc + 1) + 4 * q;
+            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+        }
+        // B tile: 16 k x 64 n
+        if (!g.b_trans) {
+            const int kk = tid >> 4, q = tid & 15;
+            const int gn = n0 + 4 * q;
+            f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (gn < g.N) v = *(const f32x4_t*)(B + (long)(k0 + kk) * g.ldb + gn);
+            *(f32x4_t*)(Bs + kk * 64 + 4 * q) = v;
+        } else {
+            const int nn = tid >> 2, q = tid & 3;
+            const int gn = n0 + nn;
+            f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (gn < g.N) v = *(const f32x4_t*)(B + (long)gn * g.ldb + k0 + 4 * q);
+            Bs[(4 * q + 0) * 64 + nn] = v[0];
+            Bs[(4 * q + 1) * 64 + nn] = v[1];
+            Bs[(4 * q + 2) * 64 + nn] = v[2];
+            Bs[(4 * q + 3) * 64 + nn] = v[3];
+        }
+        __syncthreads();
+        const float* pa = As + (32 * wm + r) * (kKc + 1) + 8 * kh;
+        const float* pb = Bs + (8 * kh) * 64 + 32 * wn + r;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], pb[s * 64], acc, 0, 0, 0);
+        __syncthreads();
+    }
+    const int n = n0 + 32 * wn + r;
+    if (n >= Nv) return;
+    const float b = g.bias ? g.bias[n] : 0.0f;
+    const float sc = g.bn_scale ? g.bn_scale[n] : 1.0f;
+    const float sh = g.bn_shift ? g.bn_shift[n] : 0.0f;
+    float* C = g.C + z * g.c_batch + n;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int m = m0 + 32 * wm + 4 * kh + (e & 3) + 8 * (e >> 2);
+        if (m >= Mv) continue;
+        float v = acc[e] + b;
+        if (g.bn_scale) v = v * sc + sh;
+        if (g.relu) v = v > 0.0f ? v : 0.0f;
+        if (g.alpha != 1.0f) v = v * g.alpha;
+        float* c = C + (long)m * g.ldc;
+        *c = g.residual ? *c + v : v;
+    }
+}
+
+// ------------------------------------------------------------------ fused multi-head attention
+// superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 64 queries of one
+// (pair, side, head); wave w owns queries 16 w .. +16 and streams the source side's keys in chunks of 64 (online
+// softmax). v_mfma_f32_16x16x4_f32 layouts: A lane l = A[l % 16][l / 16], B lane l = B[l / 16][l % 16],
+// C lane l, j = C[4 (l / 16) + j][l % 16].
+constexpr int kAttnKeys = 64;
+constexpr int kKvStride = kHd + 1;
+
+__global__ __launch_bounds__(256) void sg_attention_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
+                                                           const int* __restrict__ side_counts /*(2P)*/, int kmax,
+                                                           int cross, float* __restrict__ out /*(2P, kmax, 256)*/) {
+    __shared__ float Kc[kAttnKeys * kKvStride];
+    __shared__ float Vc[kAttnKeys * kKvStride];
+    __shared__ float Pw[4][16 * (kAttnKeys + 1)];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int zs = blockIdx.z;              // (pair, side) of the queries
+    const int zsrc = cross ? (zs ^ 1) : zs; // keys / values side
+    const int h = blockIdx.y;
+    const int q0 = blockIdx.x * 64 + 16 * wave;
+    const int nkeys = side_counts[zsrc];
+    const int nq = side_counts[zs];
+    if (blockIdx.x * 64 >= nq) return;
+    const int lr = lane & 15, lq = lane >> 4;
+    // Q fragments: qa[s] = Q[q0 + lr][4 s + lq]
+    float qa[16];
+    {
+        const float* qrow = qkv + ((long)zs * kmax + min(q0 + lr, kmax - 1)) * 768 + h * kHd;
+#pragma unroll
+        for (int s = 0; s < 16; ++s) qa[s] = qrow[4 * s + lq];
+    }
+    float m_run[4], l_run[4];
+    f32x4_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        m_run[j] = -INFINITY;
+        l_run[j] = 0.0f;
+        o[j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    const float* kbase = qkv + (long)zsrc * kmax * 768 + 256 + h * kHd;
+    const float* vbase = qkv + (long)zsrc * kmax * 768 + 512 + h * kHd;
+    for (int c0 = 0; c0 < nkeys; c0 += kAttnKeys) {
+        __syncthreads();  // previous chunk consumed
+        for (int e = tid; e < kAttnKeys * 16; e += 256) {
+            const int key = e >> 4, q4 = e & 15;
+            f32x4_t kv = {0.0f, 0.0f, 0.0f, 0.0f}, vv = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (c0 + key < nkeys) {
+                kv = *(const f32x4_t*)(kbase + (long)(c0 + key) * 768 + 4 * q4);
+                vv = *(const f32x4_t*)(vbase + (long)(c0 + key) * 768 + 4 * q4);
+            }
+            float* kd = Kc + key * kKvStride + 4 * q4;
+            float* vd = Vc + key * kKvStride + 4 * q4;
+            kd[0] = kv[0]; kd[1] = kv[1]; kd[2] = kv[2]; kd[3] = kv[3];
+            vd[0] = vv[0]; vd[1] = vv[1]; vd[2] = vv[2]; vd[3] = vv[3];
+        }
+        __syncthreads();
+        // S = Q K^T / 8 for 16 queries x 64 keys (4 tiles of 16 keys)
+        f32x4_t s4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], Kc[(16 * t + lr) * kKvStride + 4 * s + lq], acc, 0,
+                                                           0, 0);
+            s4[t] = acc;
+        }
+        // lane holds S[4 lq + j][16 t + lr]
+        float cmax[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                float v = s4[t][j] / 8.0f;
+                if (c0 + 16 * t + lr >= nkeys) v = -INFINITY;
+                s4[t][j] = v;
+                mx = fmaxf(mx, v);
+            }
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+            cmax[j] = mx;
+        }
+        float* pw = Pw[wave];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float mnew = fmaxf(m_run[j], cmax[j]);
+            const float corr = expf(m_run[j] - mnew);
+            float rs = 0.0f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float p = expf(s4[t][j] - mnew);
+                rs = rs + p;
+                pw[(4 * lq + j) * (kAttnKeys + 1) + 16 * t + lr] = p;
+            }
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) rs = rs + __shfl_xor(rs, m);
+            l_run[j] = l_run[j] * corr + rs;
+            m_run[j] = mnew;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u][j] = o[u][j] * corr;
+        }
+        __syncthreads();  // P (written in C layout) is read back in A layout
+        // O += P V: A = P (16 queries x 64 keys), B = V (64 keys x 64 dims, 4 tiles of 16)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f32x4_t acc = o[u];
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pw[lr * (kAttnKeys + 1) + 4 * s + lq],
+                                                           Vc[(4 * s + lq) * kKvStride + 16 * u + lr], acc, 0, 0, 0);
+            o[u] = acc;
+        }
+    }
+    float* ob = out + (long)zs * kmax * 256 + h * kHd;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int q = q0 + 4 * lq + j;
+        if (q >= nq) continue;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ob[(long)q * 256 + 16 * u + lr] = l_run[j] > 0.0f ? o[u][j] / l_run[j] : 0.0f;
+    }
+}
+
+// ------------------------------------------------------------------ encoder input and descriptor init
+// superglue.py:64-71 normalize_keypoints: (kpts - size / 2) / (max(W, H) * 0.7), size = (W, H); the encoder input is
+// (x_n, y_n, score) (:79-81), zero-padded to 16 channels. X <- descriptors (rows >= count zeroed).
+__global__ void sg_prepare_kernel(const float* __restrict__ kp, const float* __restrict__ scores,
+                                  const float* __restrict__ desc, const int* __restrict__ counts,
+                                  const int* __restrict__ hw, const int* __restrict__ pairs, int kmax,
+                                  float* __restrict__ enc_in /*(2P, kmax, 16)*/, float* __restrict__ X,
+                                  int* __restrict__ side_counts) {
+    const int zs = blockIdx.y;
+    const int img = pairs[zs];
+    const int n = counts[img];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0 && threadIdx.x == 0) side_counts[zs] = n;
+    if (i >= kmax) return;
+    float* e = enc_in + ((long)zs * kmax + i) * 16;
+    float* x = X + ((long)zs * kmax + i) * kD;
+    const float* d = desc + ((long)img * kmax + i) * kD;
+    if (i < n) {
+        const float W = (float)hw[2 * img + 1], H = (float)hw[2 * img];
+        const float scaling = fmaxf(W, H) * 0.7f;
+        e[0] = (kp[((long)img * kmax + i) * 2] - W / 2.0f) / scaling;
+        e[1] = (kp[((long)img * kmax + i) * 2 + 1] - H / 2.0f) / scaling;
+        e[2] = scores[(long)img * kmax + i];
+        for (int c = 0; c < kD; ++c) x[c] = d[c];
+    } else {
+        e[0] = e[1] = e[2] = 0.0f;
+        for (int c = 0; c < kD; ++c) x[c] = 0.0f;
+    }
+    for (int c = 3; c < 16; ++c) e[c] = 0.0f;
+}
+
+// ------------------------------------------------------------------ log-space optimal transport
+// superglue.py:114-145 with iters = 20: couplings [[S, alpha], [alpha, alpha]], norm = -log(m + n),
+// log_mu = [norm] * m + [log(n) + norm], log_nu = [norm] * n + [log(m) + norm],
+// u = log_mu - logsumexp(Z + v, 2), v = log_nu - logsumexp(Z + u, 1); result Z + u + v - norm.
+__global__ void sk_init_kernel(float* __restrict__ Z, const int* __restrict__ side_counts, int kmax,
+                               const float* __restrict__ bin_score, float* __restrict__ u, float* __restrict__ v) {
+    const int p = blockIdx.y;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const long ld = kmax + 1;
+    float* Zp = Z + (long)p * ld * ld;
+    const float alpha = bin_score[0];
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m) Zp[(long)t * ld + n] = alpha;
+    if (t < n) Zp[(long)m * ld + t] = alpha;
+    if (t == 0) Zp[(long)m * ld + n] = alpha;
+    if (t <= m) u[(long)p * ld + t] = 0.0f;
+    if (t <= n) v[(long)p * ld + t] = 0.0f;
+}
+
+__device__ __forceinline__ void lse_push(float x, float& mx, float& s) {
+    if (x > mx) {
+        s = s * expf(mx - x) + 1.0f;
+        mx = x;
+    } else {
+        s = s + expf(x - mx);
+    }
+}
+
+__device__ __forceinline__ void lse_merge(float& mx, float& s, float mo, float so) {
+    if (mo > mx) {
+        s = s * expf(mx - mo) + so;
+        mx = mo;
+    } else if (so > 0.0f) {
+        s = s + so * expf(mo - mx);
+    }
+}
+
+__device__ __forceinline__ float sk_norm(int m, int n) { return -logf((float)m + (float)n); }
+
+// u[i] for rows 0..m: one wave per row
+__global__ __launch_bounds__(256) void sk_rows_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                      int kmax, float* __restrict__ u, const float* __restrict__ v) {
+    const int p = blockIdx.y;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i > m) return;
+    const long ld = kmax + 1;
+    const float* row = Z + (long)p * ld * ld + (long)i * ld;
+    const float* vp = v + (long)p * ld;
+    float mx = -INFINITY, s = 0.0f;
+    for (int j = lane; j <= n; j += 64) lse_push(row[j] + vp[j], mx, s);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float mo = __shfl_xor(mx, o), so = __shfl_xor(s, o);
+        lse_merge(mx, s, mo, so);
+    }
+    if (lane == 0) {
+        const float norm = sk_norm(m, n);
+        const float log_mu = i < m ? norm : logf((float)n) + norm;
+        u[(long)p * ld + i] = log_mu - (logf(s) + mx);
+    }
+}
+
+// v[j] for columns 0..n: 64 columns x 4 row groups per workgroup
+__global__ __launch_bounds__(256) void sk_cols_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                      int kmax, const float* __restrict__ u, float* __restrict__ v) {
+    __shared__ float pm[4][64], ps[4][64];
+    const int p = blockIdx.y;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    if (blockIdx.x * 64 > n) return;
+    const long ld = kmax + 1;
+    const float* Zp = Z + (long)p * ld * ld;
+    const float* up = u + (long)p * ld;
+    float mx = -INFINITY, s = 0.0f;
+    if (j <= n)
+        for (int i = g; i <= m; i += 4) lse_push(Zp[(long)i * ld + j] + up[i], mx, s);
+    pm[g][c] = mx;
+    ps[g][c] = s;
+    __syncthreads();
+    if (g == 0 && j <= n) {
+        for (int o = 1; o < 4; ++o) lse_merge(mx, s, pm[o][c], ps[o][c]);
+        const float norm = sk_norm(m, n);
+        const float log_nu = j < n ? norm : logf((float)m) + norm;
+        v[(long)p * ld + j] = log_nu - (logf(s) + mx);
+    }
+}
+
+// row-wise max / argmax of the final scores ((Z + u) + v) - norm over the first n columns (first index on ties)
+__global__ __launch_bounds__(256) void sk_rowmax_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                        int kmax, const float* __restrict__ u,
+                                                        const float* __restrict__ v, float* __restrict__ max0,
+                                                        int* __restrict__ idx0) {
+    const int p = blockIdx.y;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i >= m) return;
+    const long ld = kmax + 1;
+    const float* row = Z + (long)p * ld * ld + (long)i * ld;
+    const float ui = u[(long)p * ld + i];
+    const float* vp = v + (long)p * ld;
+    const float norm = sk_norm(m, n);
+    float best = -INFINITY;
+    int bj = 0x7fffffff;
+    for (int j = lane; j < n; j += 64) {
+        const float z = ((row[j] + ui) + vp[j]) - norm;
+        if (z > best) { best = z; bj = j; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const int oj = __shfl_xor(bj, o);
+        if (ob > best || (ob == best && oj < bj)) { best = ob; bj = oj; }
+    }
+    if (lane == 0) {
+        max0[(long)p * kmax + i] = best;
+        idx0[(long)p * kmax + i] = bj;
+    }
+}
+
+__global__ __launch_bounds__(256) void sk_colmax_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                        int kmax, const float* __restrict__ u,
+                                                        const float* __restrict__ v, int* __restrict__ idx1) {
+    __shared__ float pb[4][64];
+    __shared__ int pi[4][64];
+    const int p = blockIdx.y;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    if (blockIdx.x * 64 >= n) return;
+    const long ld = kmax + 1;
+    const float* Zp = Z + (long)p * ld * ld;
+    const float* up = u + (long)p * ld;
+    const float norm = sk_norm(m, n);
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    if (j < n) {
+        const float vj = v[(long)p * ld + j];
+        for (int i = g; i < m; i += 4) {
+            const float z = ((Zp[(long)i * ld + j] + up[i]) + vj) - norm;
+            if (z > best) { best = z; bi = i; }
+        }
+    }
+    pb[g][c] = best;
+    pi[g][c] = bi;
+    __syncthreads();
+    if (g == 0 && j < n) {
+        for (int o = 1; o < 4; ++o)
+            if (pb[o][c] > best || (pb[o][c] == best && pi[o][c] < bi)) { best = pb[o][c]; bi = pi[o][c]; }
+        idx1[(long)p * kmax + j] = bi;
+    }
+}
+
+// mutual check + threshold (superglue.py:268-276), matches in ascending i (superglue_matcher.py:104-109)
+__global__ __launch_bounds__(256) void sg_emit_kernel(const int* __restrict__ side_counts, int kmax,
+                                                      const float* __restrict__ max0, const int* __restrict__ idx0,
+                                                      const int* __restrict__ idx1, float threshold,
+                                                      uint32_t* __restrict__ out_idx, int* __restrict__ out_count,
+                                                      float* __restrict__ out_mscore) {
+    __shared__ int sh[4];
+    const int p = blockIdx.x;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int base = 0;
+    for (int i0 = 0; i0 < kmax; i0 += 256) {
+        const int i = i0 + threadIdx.x;
+        int valid = 0;
+        float ms = 0.0f;
+        int j = -1;
+        if (i < m && n > 0) {
+            j = idx0[(long)p * kmax + i];
+            const bool mutual = idx1[(long)p * kmax + j] == i;
+            ms = mutual ? expf(max0[(long)p * kmax + i]) : 0.0f;
+            valid = (mutual && ms > threshold) ? 1 : 0;
+        }
+        if (out_mscore && i < kmax) out_mscore[(long)p * kmax + i] = i < m ? ms : 0.0f;
+        int x = valid;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) sh[wave] = x;
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wave; ++w) off += sh[w];
+        const int total = sh[0] + sh[1] + sh[2] + sh[3];
+        if (valid) {
+            const int o = off + x - 1;
+            out_idx[((long)p * kmax + o) * 2] = (uint32_t)i;
+            out_idx[((long)p * kmax + o) * 2 + 1] = (uint32_t)j;
+        }
+        base += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out_count[p] = base;
+}
+
+// ------------------------------------------------------------------ host-side orchestration
+struct SgLayout {
+    size_t enc_in, X, T1, T2, qkv, att, msg, hid, Z, u, v, max0, idx0, idx1, cnt, total;
+};
+
+__host__ SgLayout sg_layout(int P, int kmax) {
+    SgLayout L{};
+    const size_t S = (size_t)2 * P * kmax;
+    const size_t ld = (size_t)kmax + 1;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t r = o; o += gtsfm_align_up(bytes, 256); return r; };
+    L.enc_in = take(S * 16 * 4);
+    L.X = take(S * kD * 4);
+    L.T1 = take(S * kD * 4);
+    L.T2 = take(S * kD * 4);
+    L.qkv = take(S * 768 * 4);
+    L.att = take(S * kD * 4);
+    L.msg = take(S * kD * 4);
+    L.hid = take(S * 512 * 4);
+    L.Z = take((size_t)P * ld * ld * 4);
+    L.u = take((size_t)P * ld * 4);
+    L.v = take((size_t)P * ld * 4);
+    L.max0 = take((size_t)P * kmax * 4);
+    L.idx0 = take((size_t)P * kmax * 4);
+    L.idx1 = take((size_t)P * kmax * 4);
+    L.cnt = take((size_t)2 * P * 4);
+    L.total = o;
+    return L;
+}
+
+hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
+    const dim3 grid((unsigned)((g.N + 63) / 64), (unsigned)((g.M + 63) / 64), (unsigned)batches);
+    hipLaunchKernelGGL(sg_gemm_kernel, grid, dim3(kGemmThreads), 0, stream, g);
+    return hipGetLastError();
+}
+
+GemmArgs side_gemm(const float* A, int lda, const float* W, int K, int N, const float* bias, float* C, int ldc,
+                   int kmax) {
+    GemmArgs g{};
+    g.A = A; g.lda = lda; g.a_batch = (long)kmax * lda;
+    g.A2 = nullptr; g.Ksplit = K;
+    g.B = W; g.ldb = N; g.b_batch = 0; g.b_trans = 0;
+    g.bias = bias; g.alpha = 1.0f;
+    g.C = C; g.ldc = ldc; g.c_batch = (long)kmax * ldc;
+    g.M = kmax; g.N = N; g.K = K;
+    return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gtsfm_superglue_weights_floats(int n_layers) { return n_layers > 0 ? sg_weights_floats(n_layers) : 0; }
+
+size_t gtsfm_superglue_workspace_bytes(int n_pairs, int kmax) {
+    if (n_pairs <= 0 || kmax <= 0) return 0;
+    return sg_layout(n_pairs, (kmax + 63) / 64 * 64).total;
+}
+
+int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const float* d_desc, const int* d_counts,
+                            const int* d_image_hw, int n_img, int kmax, const int* d_pairs, int n_pairs,
+                            const float* d_weights, int n_layers, int sinkhorn_iters, float match_threshold,
+                            void* d_workspace, size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count,
+                            float* d_out_mscores, void* stream_v) {
+    hipStream_t stream = (hipStream_t)stream_v;
+    if (n_pairs == 0) return GTSFM_OK;
+    if (!d_kp || !d_scores || !d_desc || !d_counts || !d_image_hw || !d_pairs || !d_weights || !d_workspace ||
+        !d_out_idx || !d_out_count || n_img <= 0 || kmax <= 0 || n_pairs < 0 || n_layers <= 0 || sinkhorn_iters < 0 ||
+        kmax % 64 != 0)
+        return GTSFM_ERR_ARG;
+    const SgLayout L = sg_layout(n_pairs, kmax);
+    if (workspace_bytes < L.total) return GTSFM_ERR_CAPACITY;
+    unsigned char* ws = (unsigned char*)d_workspace;
+    float* enc_in = (float*)(ws + L.enc_in);
+    float* X = (float*)(ws + L.X);
+    float* T1 = (float*)(ws + L.T1);
+    float* T2 = (float*)(ws + L.T2);
+    float* qkv = (float*)(ws + L.qkv);
+    float* att = (float*)(ws + L.att);
+    float* msg = (float*)(ws + L.msg);
+    float* hid = (float*)(ws + L.hid);
+    float* Z = (float*)(ws + L.Z);
+    float* u = (float*)(ws + L.u);
+    float* v = (float*)(ws + L.v);
+    float* max0 = (float*)(ws + L.max0);
+    int* idx0 = (int*)(ws + L.idx0);
+    int* idx1 = (int*)(ws + L.idx1);
+    int* side_counts = (int*)(ws + L.cnt);
+    const int S = 2 * n_pairs;
+    hipLaunchKernelGGL(sg_prepare_kernel, dim3((kmax + 255) / 256, S), dim3(256), 0, stream, d_kp, d_scores, d_desc,
+                       d_counts, d_image_hw, d_pairs, kmax, enc_in, X, side_counts);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    // keypoint encoder (superglue.py:74-81): MLP [3, 32, 64, 128, 256, 256], BN + ReLU between layers; desc += enc
+    const float* w = d_weights;
+    {
+        const float* in = enc_in;
+        int cin = 16;
+        float* bufs[2] = {T1, T2};
+        for (int i = 0; i < 5; ++i) {
+            const float* W = w;
+            const float* bias = W + (size_t)kEncIn[i] * kEncOut[i];
+            const int co = kEncOut[i];
+            GemmArgs g = side_gemm(in, cin, W, kEncIn[i], co, bias, i < 4 ? bufs[i & 1] : X, i < 4 ? co : kD, kmax);
+            if (i < 4) {
+                g.bn_scale = bias + co;
+                g.bn_shift = bias + 2 * co;
+                g.relu = 1;
+            } else {
+                g.residual = 1;  // desc0 + kenc(...)
+            }
+            GTSFM_CHECK_HIP(run_gemm(g, S, stream));
+            in = bufs[i & 1];
+            cin = co;
+            w += enc_floats(i);
+        }
+    }
+    // attentional GNN (superglue.py:104-121): layer l is 'self' for even l, 'cross' for odd l
+    for (int l = 0; l < n_layers; ++l) {
+        const float* Wqkv = w;
+        const float* bqkv = Wqkv + 256 * 768;
+        const float* Wm = bqkv + 768;
+        const float* bm = Wm + 256 * 256;
+        const float* W1 = bm + 256;
+        const float* b1 = W1 + 512 * 512;
+        const float* s1 = b1 + 512;
+        const float* h1 = s1 + 512;
+        const float* W2 = h1 + 512;
+        const float* b2 = W2 + 512 * 256;
+        w += kLayerFloats;
+        GTSFM_CHECK_HIP(run_gemm(side_gemm(X, kD, Wqkv, kD, 768, bqkv, qkv, 768, kmax), S, stream));
+        hipLaunchKernelGGL(sg_attention_kernel, dim3(kmax / 64, kHeads, S), dim3(256), 0, stream, qkv, side_counts,
+                           kmax, l & 1, att);
+        GTSFM_CHECK_HIP(hipGetLastError());
+        GTSFM_CHECK_HIP(run_gemm(side_gemm(att, kD, Wm, kD, kD, bm, msg, kD, kmax), S, stream));
+        GemmArgs g1 = side_gemm(X, kD, W1, 512, 512, b1, hid, 512, kmax);
+        g1.Ksplit = kD;  // cat([x, message])
+        g1.A2 = msg;
+        g1.lda2 = kD;
+        g1.a2_batch = (long)kmax * kD;
+        g1.bn_scale = s1;
+        g1.bn_shift = h1;
+        g1.relu = 1;
+        GTSFM_CHECK_HIP(run_gemm(g1, S, stream));
+        GemmArgs g2 = side_gemm(hid, 512, W2, 512, kD, b2, X, kD, kmax);
+        g2.residual = 1;  // desc + delta
+        GTSFM_CHECK_HIP(run_gemm(g2, S, stream));
+    }
+    // final projection, scores = mdesc0^T mdesc1 / 16 into the coupling matrix interior
+    const float* Wf = w;
+    const float* bf = Wf + 256 * 256;
+    const float* bin = bf + 256;
+    GTSFM_CHECK_HIP(run_gemm(side_gemm(X, kD, Wf, kD, kD, bf, T1, kD, kmax), S, stream));
+    const long ld = kmax + 1;
+    {
+        GemmArgs g{};
+        g.A = T1; g.lda = kD; g.a_batch = (long)2 * kmax * kD;
+        g.Ksplit = kD;
+        g.B = T1 + (long)kmax * kD; g.ldb = kD; g.b_batch = (long)2 * kmax * kD; g.b_trans = 1;
+        g.alpha = 1.0f / 16.0f;
+        g.C = Z; g.ldc = ld; g.c_batch = ld * ld;
+        g.M = kmax; g.N = kmax; g.K = kD;
+        g.m_lim = side_counts; g.n_lim = side_counts; g.lim_stride = 2;
+        GTSFM_CHECK_HIP(run_gemm(g, n_pairs, stream));
+    }
+    hipLaunchKernelGGL(sk_init_kernel, dim3((kmax + 256) / 256, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
+                       bin, u, v);
+    for (int it = 0; it < sinkhorn_iters; ++it) {
+        hipLaunchKernelGGL(sk_rows_kernel, dim3((kmax + 4) / 4, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
+                           u, (const float*)v);
+        hipLaunchKernelGGL(sk_cols_kernel, dim3((kmax + 64) / 64, n_pairs), dim3(256), 0, stream, Z, side_counts,
+                           kmax, (const float*)u, v);
+    }
+    hipLaunchKernelGGL(sk_rowmax_kernel, dim3(kmax / 4, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax, u, v,
+                       max0, idx0);
+    hipLaunchKernelGGL(sk_colmax_kernel, dim3(kmax / 64, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax, u, v,
+                       idx1);
+    hipLaunchKernelGGL(sg_emit_kernel, dim3(n_pairs), dim3(256), 0, stream, side_counts, kmax, max0, idx0, idx1,
+                       match_threshold, d_out_idx, d_out_count, d_out_mscores);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    return GTSFM_OK;
+}
+
+}  // extern "C"

@@ -220,3 +220,37 @@ def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: in
                                     native.stream_handle(stream))
     native.check(rc, "gtsfm_superpoint_batched")
     return out
+
+
+def superglue_match(kp: torch.Tensor, scores: torch.Tensor, desc: torch.Tensor, counts: torch.Tensor,
+                    image_hw: torch.Tensor, pairs: torch.Tensor, weights: torch.Tensor, n_layers: int = 18,
+                    sinkhorn_iters: int = 20, match_threshold: float = 0.2,
+                    stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """SuperGlue over every pair (gtsfm_superglue_batched).
+
+    Args: kp (n_img, kmax, 2) f32, scores (n_img, kmax) f32, desc (n_img, kmax, 256) f32, counts (n_img,) int32,
+    image_hw (n_img, 2) int32 (H, W), pairs (P, 2) int32, weights: the packed blob. kmax must be a multiple of 64.
+    Returns idx (P, kmax, 2) int32 (uint32 values, i ascending), count (P,) int32, mscores0 (P, kmax) f32.
+    """
+    for t in (kp, scores, desc, weights):
+        assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+    assert counts.dtype == torch.int32 and image_hw.dtype == torch.int32 and pairs.dtype == torch.int32
+    n_img, kmax = kp.shape[0], kp.shape[1]
+    assert kmax % 64 == 0 and desc.shape == (n_img, kmax, 256) and scores.shape == (n_img, kmax)
+    L = native.lib()
+    assert weights.numel() == L.gtsfm_superglue_weights_floats(n_layers)
+    P = pairs.shape[0]
+    dev = kp.device
+    idx = torch.zeros((max(P, 1), kmax, 2), dtype=torch.int32, device=dev)
+    cnt = torch.zeros((max(P, 1),), dtype=torch.int32, device=dev)
+    ms = torch.zeros((max(P, 1), kmax), dtype=torch.float32, device=dev)
+    if P > 0:
+        ws = _workspace(L.gtsfm_superglue_workspace_bytes(P, kmax), dev)
+        if stream is not None:
+            ws.record_stream(stream)
+        rc = L.gtsfm_superglue_batched(_ptr(kp), _ptr(scores), _ptr(desc), _ptr(counts), _ptr(image_hw), n_img, kmax,
+                                       _ptr(pairs), P, _ptr(weights), int(n_layers), int(sinkhorn_iters),
+                                       float(match_threshold), _ptr(ws), ws.numel(), _ptr(idx), _ptr(cnt), _ptr(ms),
+                                       native.stream_handle(stream))
+        native.check(rc, "gtsfm_superglue_batched")
+    return idx[:P], cnt[:P], ms[:P]

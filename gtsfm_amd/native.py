@@ -69,6 +69,13 @@ SIGNATURES = {
         [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_size_t, c_void_p,
          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "gtsfm_superglue_weights_floats": (c_size_t, [c_int]),
+    "gtsfm_superglue_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "gtsfm_superglue_batched": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
+         c_float, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
     "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gtsfm_sift_batched": (
         c_int,

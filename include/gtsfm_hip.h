@@ -147,6 +147,27 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, int n, int H, int W, int C
                              void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_scores, float* d_desc,
                              int* d_count, int* d_n_detected, void* stream);
 
+/* ----------------------------------------------------------------------------------------------
+ * SuperGlue matcher. Replaces SuperGlueMatcher.match (gtsfm/frontend/matcher/superglue_matcher.py:43-111) and
+ * the network it wraps (thirdparty/SuperGluePretrainedNetwork/models/superglue.py:228-283), batched over pairs.
+ * Features of all images: d_kp[n_img][kmax][2] (x, y) float, d_scores[n_img][kmax], d_desc[n_img][kmax][256],
+ * d_counts[n_img], d_image_hw[n_img][2] = (H, W); kmax a multiple of 64. Pairs d_pairs[n_pairs][2] (both sides
+ * must hold >= 1 keypoint: the reference returns no matches for an empty side before running the network).
+ * d_weights: gtsfm_superglue_weights_floats(n_layers) floats (layout in superglue.hip: W^T[cin][cout] per 1x1 conv,
+ * eval BatchNorm folded to scale/shift, q/k/v/merge weights permuted head-major). GNN layer l is 'self' for even l,
+ * 'cross' for odd l. Outputs: matches (i, j) with i ascending in d_out_idx[n_pairs][kmax][2] uint32, counts
+ * d_out_count[n_pairs], and the matching scores of image-0 keypoints d_out_mscores[n_pairs][kmax] (may be NULL).
+ * ---------------------------------------------------------------------------------------------- */
+size_t gtsfm_superglue_weights_floats(int n_layers);
+
+size_t gtsfm_superglue_workspace_bytes(int n_pairs, int kmax);
+
+int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const float* d_desc, const int* d_counts,
+                            const int* d_image_hw, int n_img, int kmax, const int* d_pairs, int n_pairs,
+                            const float* d_weights, int n_layers, int sinkhorn_iters, float match_threshold,
+                            void* d_workspace, size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count,
+                            float* d_out_mscores, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

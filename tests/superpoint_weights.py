@@ -23,3 +23,44 @@ def superpoint_state_dict(seed: int = 0) -> dict:
         sd[f"{name}.weight"] = (rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / fan_in)).astype(np.float32)
         sd[f"{name}.bias"] = rng.uniform(-0.05, 0.05, size=cout).astype(np.float32)
     return sd
+
+
+def superglue_state_dict(seed: int = 0, n_layers: int = 18) -> dict:
+    """Seeded random weights with the reference SuperGlue module's parameter names (superglue.py:165-211):
+    kenc.encoder.{0,3,6,9,12} conv1d (+ BatchNorm1d at 1,4,7,10), gnn.layers.i.attn.{proj.0-2,merge},
+    gnn.layers.i.mlp.{0 (conv 512->512), 1 (BN), 3 (conv 512->256)}, final_proj, bin_score.
+    Conv weights: std 1/sqrt(fan_in), 0.1x on the residual branches' last conv (keypoint encoder, MLP), so the 18
+    residual updates perturb the descriptors by ~10 % each instead of replacing them; final_proj = 12 I + noise, so
+    planted correspondences (cosine ~0.95) get peaked assignments and the golden pairs have matches to compare.
+    BN: gamma U(0.8, 1.2), beta U(-0.1, 0.1), running mean U(-0.1, 0.1), running var U(0.5, 1.5)."""
+    rng = np.random.default_rng(seed)
+    sd = {}
+
+    def conv(name, cin, cout, scale=1.0):
+        sd[f"{name}.weight"] = (rng.standard_normal((cout, cin, 1)) * scale / np.sqrt(cin)).astype(np.float32)
+        sd[f"{name}.bias"] = rng.uniform(-0.05, 0.05, size=cout).astype(np.float32)
+
+    def bn(name, c):
+        sd[f"{name}.weight"] = rng.uniform(0.8, 1.2, size=c).astype(np.float32)
+        sd[f"{name}.bias"] = rng.uniform(-0.1, 0.1, size=c).astype(np.float32)
+        sd[f"{name}.running_mean"] = rng.uniform(-0.1, 0.1, size=c).astype(np.float32)
+        sd[f"{name}.running_var"] = rng.uniform(0.5, 1.5, size=c).astype(np.float32)
+        sd[f"{name}.num_batches_tracked"] = np.array(0, dtype=np.int64)
+
+    chans = [3, 32, 64, 128, 256, 256]
+    for i in range(5):
+        conv(f"kenc.encoder.{3 * i}", chans[i], chans[i + 1], 0.1 if i == 4 else 1.0)
+        if i < 4:
+            bn(f"kenc.encoder.{3 * i + 1}", chans[i + 1])
+    for l in range(n_layers):
+        p = f"gnn.layers.{l}"
+        for j in range(3):
+            conv(f"{p}.attn.proj.{j}", 256, 256)
+        conv(f"{p}.attn.merge", 256, 256)
+        conv(f"{p}.mlp.0", 512, 512)
+        bn(f"{p}.mlp.1", 512)
+        conv(f"{p}.mlp.3", 512, 256, 0.1)
+    conv("final_proj", 256, 256, 0.05)
+    sd["final_proj.weight"][:, :, 0] += 12.0 * np.eye(256, dtype=np.float32)
+    sd["bin_score"] = np.array(1.0, dtype=np.float32)
+    return sd

@@ -51,3 +51,18 @@ def test_superpoint_weight_blob_layout():
     w = sd["conv1a.weight"]
     np.testing.assert_array_equal(blob[: 9 * 64].reshape(9, 64), w[:, 0].reshape(64, 9).T)
     np.testing.assert_array_equal(blob[9 * 64: 9 * 64 + 64], sd["conv1a.bias"])
+
+
+def test_superglue_weight_blob_layout():
+    from gtsfm_amd import native
+    from gtsfm_amd.frontend.matcher.superglue_matcher import _head_major, pack_superglue_weights
+    from superpoint_weights import superglue_state_dict
+
+    sd = superglue_state_dict(0)
+    blob = pack_superglue_weights(sd)
+    assert blob.dtype == np.float32 and blob.size == native.lib().gtsfm_superglue_weights_floats(18)
+    assert blob[-1] == sd["bin_score"]
+    # head-major permutation: new channel h * 64 + d <- reference channel 4 d + h
+    c = np.arange(256)
+    perm = _head_major(c)
+    assert perm[1] == 4 and perm[64] == 1 and sorted(perm.tolist()) == c.tolist()

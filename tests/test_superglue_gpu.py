@@ -1,0 +1,91 @@
+"""HIP SuperGlue (gtsfm_superglue_batched) against the reference module's own outputs.
+
+Golden: tests/golden/superglue_random_w0.npz from tests/golden/make_superglue_golden.py (the reference's
+thirdparty/.../superglue.py run in torch fp32 with seeded random weights, 20 Sinkhorn iterations). The HIP network
+is exact-fp32 MFMA arithmetic in a different summation order (and an online softmax), so the log-assignment
+matrix agrees within 2e-3 absolute after 18 layers + 20 Sinkhorn iterations, and the matches agree except where
+two candidates are within that margin (>= 98 % of the reference's matches, no extra matches beyond 2 %).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from superpoint_weights import superglue_state_dict
+
+pytestmark = pytest.mark.gpu
+CASES = ["small_150x170", "mid_700x650"]
+
+
+@pytest.fixture(scope="module")
+def golden(golden_dir):
+    return np.load(os.path.join(golden_dir, "superglue_random_w0.npz"))
+
+
+@pytest.fixture(scope="module")
+def matcher():
+    from gtsfm_amd import native
+    from gtsfm_amd.frontend.matcher.superglue_matcher import SuperGlueMatcher
+
+    native.require_gpu()
+    return SuperGlueMatcher(state_dict=superglue_state_dict(0))
+
+
+def _case(golden, name):
+    from gtsfm_amd.common.keypoints import Keypoints
+
+    g = lambda k: golden[f"{name}__{k}"]  # noqa: E731
+    H, W = (int(x) for x in g("hw"))
+    kp0 = Keypoints(g("kp0"), responses=g("s0"))
+    kp1 = Keypoints(g("kp1"), responses=g("s1"))
+    return kp0, kp1, g("d0"), g("d1"), (H, W, 1), g("matches0")
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_matches_reference_module(matcher, golden, name):
+    kp0, kp1, d0, d1, shape, m0 = _case(golden, name)
+    got = matcher.match(kp0, kp1, d0, d1, shape, shape)
+    ref = np.stack([np.flatnonzero(m0 >= 0), m0[m0 >= 0]], 1).astype(np.uint32)
+    assert got.dtype == np.uint32 and got.ndim == 2 and got.shape[1] == 2
+    assert np.all(np.diff(got[:, 0].astype(np.int64)) > 0)  # ascending i, one match per i
+    a, b = set(map(tuple, got.tolist())), set(map(tuple, ref.tolist()))
+    assert len(a & b) >= 0.98 * len(b) and len(a - b) <= 0.02 * max(len(b), 1), (len(a), len(b), len(a & b))
+
+
+def test_batch_and_empty(matcher, golden):
+    from gtsfm_amd.common.keypoints import Keypoints
+
+    kp0, kp1, d0, d1, shape, _ = _case(golden, "small_150x170")
+    kq0, kq1, e0, e1, shape2, _ = _case(golden, "mid_700x650")
+    empty = Keypoints(np.zeros((0, 2), np.float32), responses=np.zeros(0, np.float32))
+    out = matcher.match_batch([kp0, kp1, kq0, kq1, empty], [d0, d1, e0, e1, np.zeros((0, 256), np.float32)],
+                              [shape, shape, shape2, shape2, shape], [(0, 1), (2, 3), (0, 4)])
+    assert np.array_equal(out[(0, 1)], matcher.match(kp0, kp1, d0, d1, shape, shape))
+    assert np.array_equal(out[(2, 3)], matcher.match(kq0, kq1, e0, e1, shape2, shape2))
+    assert out[(0, 4)].shape == (0, 2) and out[(0, 4)].dtype == np.uint32
+    with pytest.raises(ValueError):
+        matcher.match(Keypoints(kp0.coordinates), kp1, d0, d1, shape, shape)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_matching_scores_close(matcher, golden, name):
+    """matching_scores0 (exp of the mutual row maxima of the final log-assignment) within 2e-3 absolute."""
+    from gtsfm_amd import device
+
+    kp0, kp1, d0, d1, shape, m0 = _case(golden, name)
+    n0, n1 = len(kp0), len(kp1)
+    kmax = (max(n0, n1) + 63) // 64 * 64
+    kp = np.zeros((2, kmax, 2), np.float32)
+    sc = np.zeros((2, kmax), np.float32)
+    de = np.zeros((2, kmax, 256), np.float32)
+    kp[0, :n0], kp[1, :n1] = kp0.coordinates, kp1.coordinates
+    sc[0, :n0], sc[1, :n1] = kp0.responses, kp1.responses
+    de[0, :n0], de[1, :n1] = d0, d1
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    _, _, ms = device.superglue_match(t(kp), t(sc), t(de), t(np.array([n0, n1], np.int32)),
+                                      t(np.array([shape[:2], shape[:2]], np.int32)), t(np.array([[0, 1]], np.int32)),
+                                      matcher.weights())
+    ref = golden[f"{name}__mscores0"]
+    np.testing.assert_allclose(ms[0, :n0].cpu().numpy(), ref, atol=2e-3)
