@@ -26,6 +26,20 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;  // one v_min3_u32
+    asm volatile("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Insert two keys a, b into a running (b1 <= b2) top-2: 3 ops instead of 4. The second smallest of
+// {b1, b2, a, b} is min(b2, med3(b1, a, b)) because b2 >= b1.
+__device__ __forceinline__ void top2_insert2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
+    const uint32_t m = umed3(b1, a, b);
+    b1 = umin3(b1, a, b);
+    b2 = umin(b2, m);
+}
+
 // (a << s) | b in one v_lshl_or_b32 (keeps the backend from splitting shared shifts into shift + or pairs)
 __device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t s, uint32_t b) {
     uint32_t r;

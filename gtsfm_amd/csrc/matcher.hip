@@ -12,9 +12,11 @@
 // (the last column adds 2^23, see the epilogue)
 // Every factor is an integer exactly representable in fp16 and every partial sum is an integer < 2^24,
 // so the fp32 accumulation is exact in any order: d2 = |a|^2 + |b|^2 - 2 a.b exactly.
-// The epilogue packs key = d2 << ib | index (d2 < 2^20, ib = max(11, ceil log2 kmax)) and keeps a running top-2 per row in
-// registers (v_med3_u32 + v_min_u32 per element) and per column through LDS; the K1 x K2 matrix is
-// never written to HBM. Lexicographic (d2, index) order == OpenCV's strict-'<' scan order, and for
+// The epilogue keeps a running top-2 per row in registers and per column through LDS; the K1 x K2 matrix is never
+// written to HBM. Columns track packed keys d2 << ib | row (ib = max(11, ceil log2 kmax)), inserted two at a time
+// (v_min3 + v_med3 + v_min per pair). Rows track distance VALUES only (v_med3 + v_min on the raw accumulator bits, no
+// key build): a column's best row i is row i's argmin iff row i's best distance equals the column's and row i has no
+// tie at its minimum; tied rows are recomputed exactly in finalize (rare). 4.5 VALU per distance instead of 6. Lexicographic (d2, index) order == OpenCV's strict-'<' scan order, and for
 // d2 < 2^22 ordering by d2 equals ordering by sqrtf(d2), so results are bit-identical to the oracle.
 //
 // Exact path (GTSFM_MATCH_EXACT_F32): float descriptors, per-row sequential fp32 sums (no FMA
@@ -118,12 +120,19 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
 constexpr int kSub = 2;
 constexpr int kSuper = kSub * kChunk;
 
+// Orientation: the GEMM's rows (A operand, held in registers) are image i2's keypoints and its columns (B operand,
+// streamed through LDS) are image i1's. Pairs arrive in lexicographic (i1, i2) order, so consecutive pairs share the
+// streamed image; the XCD-aware block remap below hands every XCD a contiguous run of pairs, so the workgroups
+// resident on one XCD stream the same B image out of that XCD's L2 instead of re-reading it from HBM.
+//   rowres[p][j2] = top-2 of image i2's keypoint j2 (distance values in kFast, packed keys otherwise)
+//   colres[p][j1] = top-2 packed keys of image i1's keypoint j1 (index = keypoint of i2)
 template <int NK, bool kFast>
 __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* __restrict__ a_form,
                                                                const _Float16* __restrict__ b_form,
                                                                const int* __restrict__ counts,
-                                                               const int* __restrict__ pairs, int kpad, int kmax,
-                                                               int ib, uint2* __restrict__ rowres,
+                                                               const int* __restrict__ pairs, int n_pairs,
+                                                               int kpad, int kmax, int ib,
+                                                               uint2* __restrict__ rowres,
                                                                uint2* __restrict__ colres) {
     using Cfg = MnnCfg<NK>;
     constexpr int kSupBytes = kSub * Cfg::kBufBytes;
@@ -133,15 +142,17 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
     uint32_t* partial = (uint32_t*)(smem + 2 * kSupBytes);           // [2][kWaves][kSuper][2]
     uint2* colstate = (uint2*)(partial + 2 * kWaves * kSuper * 2);   // [kmax]
 
-    const int p = blockIdx.x;
-    const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
-    const int n1 = counts[i1], n2 = counts[i2];
+    // bijective XCD remap (blocks b, b + 8, ... share an XCD and take consecutive pairs)
+    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_pairs >> 3, r8 = n_pairs & 7;
+    const int p = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
+    const int img_a = pairs[2 * p + 1], img_b = pairs[2 * p];
+    const int n1 = counts[img_a], n2 = counts[img_b];  // n1 rows (A), n2 columns (B)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int lrow = lane & 31, half = lane >> 5;
     if (n1 <= 0 || n2 <= 0) return;  // nothing to match; finalize reads zero rows
 
-    const _Float16* A = a_form + (size_t)i1 * kpad * Cfg::kDa;
-    const unsigned char* Bbytes = (const unsigned char*)(b_form + (size_t)i2 * kpad * Cfg::kDa);
+    const _Float16* A = a_form + (size_t)img_a * kpad * Cfg::kDa;
+    const unsigned char* Bbytes = (const unsigned char*)(b_form + (size_t)img_b * kpad * Cfg::kDa);
     uint2* rres = rowres + (size_t)p * kmax;
     uint2* cres = colres + (size_t)p * kmax;
 
@@ -195,63 +206,80 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
         for (int sc = 0; sc < nsup; ++sc) {
             const int buf = sc & 1;
             if (sc + 1 < nsup) issue_super(sc + 1, buf ^ 1);  // lands during this super-chunk's MFMAs
-#pragma unroll 1
-            for (int sub = 0; sub < kSub; ++sub) {
-                const int ch = sc * kSub + sub;
-                // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows
-                const unsigned char* bb =
-                    bbuf + buf * kSupBytes + (sub * kChunk + lrow) * Cfg::kRowBytes + half * 16;
-                f32x16 acc0 = {}, acc1 = {};
+            // Both 32-column chunks of the super-chunk against both row tiles (acc[sub][t]), so every row sees two
+            // new distances per epilogue and takes them with one paired top-2 insert (3 VALU per 2 distances).
+            // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows.
+            const unsigned char* bb = bbuf + buf * kSupBytes + lrow * Cfg::kRowBytes + half * 16;
+            f32x16 acc[kSub][2];
 #pragma unroll
-                for (int s = 0; s < NK; ++s) {
-                    const half8 bf = *(const half8*)(bb + 32 * s);
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc1, 0, 0, 0);
+            for (int sub = 0; sub < kSub; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
+#pragma unroll
+            for (int s = 0; s < NK; ++s) {
+#pragma unroll
+                for (int sub = 0; sub < kSub; ++sub) {
+                    const half8 bf = *(const half8*)(bb + sub * Cfg::kBufBytes + 32 * s);
+                    acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc[sub][0], 0, 0, 0);
+                    acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc[sub][1], 0, 0, 0);
                 }
+            }
 
-                const uint32_t gcol = (uint32_t)(ch * kChunk + lrow);
-                const bool cols_partial = (ch * kChunk + kChunk > n2);
-                uint32_t cb1 = kNoKey, cb2 = kNoKey;
-                // Epilogue: 2 key builds + 2 top-2 inserts per distance. Partial tiles (last row tile / column
-                // chunk) take a separate masked copy so the full-tile path carries no selects.
-                auto epilogue = [&](auto masked) {
-                    constexpr bool kMasked = decltype(masked)::value;
+            const int c0 = sc * kSuper;
+            const bool cols_partial = (c0 + kSuper > n2);
+            uint32_t cb1[kSub], cb2[kSub];
+            // Epilogue. kFast: rows keep value-only top-2s of the raw accumulator bits (0x4B000000 | d2, monotone in
+            // d2), columns keep packed keys with the row index (one v_lshl_or), both inserted two at a time. Partial
+            // tiles (last row tile / column chunk) take a separate masked copy so the full-tile path has no selects.
+            auto epilogue = [&](auto masked) {
+                constexpr bool kMasked = decltype(masked)::value;
 #pragma unroll
-                    for (int t = 0; t < 2; ++t) {
-                        const f32x16& acc = t ? acc1 : acc0;
-                        const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 4 * half);
+                for (int sub = 0; sub < kSub; ++sub) cb1[sub] = cb2[sub] = kNoKey;
 #pragma unroll
-                        for (int g = 0; g < 16; ++g) {
+                for (int t = 0; t < 2; ++t) {
+                    const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 4 * half);
+#pragma unroll
+                    for (int g0 = 0; g0 < 16; g0 += 2) {  // two rows at a time: column keys go in as a pair
+                        uint32_t ck[kSub][2];
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int g = g0 + h;
                             const uint32_t grow = rowbase + (uint32_t)((g & 3) + 8 * (g >> 2));
-                            uint32_t rk, ck;
-                            if constexpr (kFast) {
-                                const uint32_t bits = __float_as_uint(acc[g]);
-                                rk = lshl_or(bits, (uint32_t)ib, gcol);
-                                ck = lshl_or(bits, (uint32_t)ib, grow);
-                            } else {
-                                const uint32_t d2 = umin((uint32_t)acc[g] - (1u << 23), dsat);
-                                rk = (d2 << ib) | gcol;
-                                ck = (d2 << ib) | grow;
+                            uint32_t rv[kSub];
+#pragma unroll
+                            for (int sub = 0; sub < kSub; ++sub) {
+                                const uint32_t gcol = (uint32_t)(c0 + sub * kChunk + lrow);
+                                const uint32_t bits = __float_as_uint(acc[sub][t][g]);
+                                if constexpr (kFast) {
+                                    rv[sub] = bits;
+                                    ck[sub][h] = lshl_or(bits, (uint32_t)ib, grow);
+                                } else {
+                                    const uint32_t d2 = umin((uint32_t)acc[sub][t][g] - (1u << 23), dsat);
+                                    rv[sub] = (d2 << ib) | gcol;
+                                    ck[sub][h] = (d2 << ib) | grow;
+                                }
+                                if constexpr (kMasked) {
+                                    if ((int)gcol >= n2) rv[sub] = kNoKey;
+                                    if ((int)grow >= n1) ck[sub][h] = kNoKey;
+                                }
                             }
-                            if constexpr (kMasked) {
-                                if ((int)gcol >= n2) rk = kNoKey;
-                                if ((int)grow >= n1) ck = kNoKey;
-                            }
-                            top2_insert(rb1[t][g], rb2[t][g], rk);
-                            top2_insert(cb1, cb2, ck);
+                            top2_insert2(rb1[t][g], rb2[t][g], rv[0], rv[1]);
                         }
+#pragma unroll
+                        for (int sub = 0; sub < kSub; ++sub) top2_insert2(cb1[sub], cb2[sub], ck[sub][0], ck[sub][1]);
                     }
-                };
-                if (cols_partial || rows_partial1)
-                    epilogue(std::true_type{});
-                else
-                    epilogue(std::false_type{});
-                // combine the two half-waves (same column, rows +0/+4) and publish the wave's column partial
-                {
-                    const uint32_t o1 = __shfl_xor(cb1, 32), o2 = __shfl_xor(cb2, 32);
-                    top2_merge(cb1, cb2, o1, o2);
-                    partial[((buf * kWaves + wave) * kSuper + sub * kChunk + lrow) * 2 + half] = half ? cb2 : cb1;
                 }
+            };
+            static_assert(kSub == 2, "paired row insert takes exactly two chunks");
+            if (cols_partial || rows_partial1)
+                epilogue(std::true_type{});
+            else
+                epilogue(std::false_type{});
+            // combine the two half-waves (same column, rows +0/+4) and publish the wave's column partials
+#pragma unroll
+            for (int sub = 0; sub < kSub; ++sub) {
+                uint32_t a1 = cb1[sub], a2 = cb2[sub];
+                const uint32_t o1 = __shfl_xor(a1, 32), o2 = __shfl_xor(a2, 32);
+                top2_merge(a1, a2, o1, o2);
+                partial[((buf * kWaves + wave) * kSuper + sub * kChunk + lrow) * 2 + half] = half ? a2 : a1;
             }
             if (sc > 0) merge_partials(sc - 1, buf ^ 1);
             __syncthreads();  // next super-chunk landed (vmcnt(0)); partials of this one visible
@@ -383,7 +411,13 @@ __device__ void block_exact_top2(const float* __restrict__ q, const float* __res
     __syncthreads();
 }
 
-template <bool kPacked>
+// Per-keypoint top-2 encodings consumed by finalize. side1 = image i1's keypoints (best in i2), side2 = image i2's.
+//   kResExact:  ExactTop2 on both sides (exact fp32 path)
+//   kResKeys:   packed (d2 << ib | index) keys on both sides (ib = 13)
+//   kResValues: side1 packed keys, side2 raw accumulator bits 0x4B000000 | d2 without an index (ib <= 12)
+constexpr int kResExact = 0, kResKeys = 1, kResValues = 2;
+
+template <int kRes>
 __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void* __restrict__ rowres_v,
                                                                      const void* __restrict__ colres_v,
                                                                      const float* __restrict__ desc,
@@ -411,7 +445,48 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
         keys[slot] = ((unsigned long long)__float_as_uint(d1r) << 32) | ((unsigned long long)i << 16) | (uint32_t)j;
     };
 
-    for (int i = tid; i < n1 && n2 > 0; i += kFinThreads) {
+    constexpr bool kPacked = kRes == kResKeys;
+    const float* D1 = desc + (size_t)i1 * kmax * dim;
+    const float* D2 = desc + (size_t)i2 * kmax * dim;
+    if constexpr (kRes == kResValues) {
+        // side2 carries distances only. Keypoint i's nearest j (from its key) is mutual iff j's best distance equals
+        // d(i, j) and j has no tie at its minimum (then i, reaching that minimum, is j's unique nearest). A tied j
+        // whose own ratio test can pass is recomputed exactly below; one that cannot is in no match.
+        constexpr uint32_t kMant = 0x7FFFFFu;
+        const uint2* s1 = (const uint2*)rowres_v + (size_t)p * kmax;
+        const uint2* s2 = (const uint2*)colres_v + (size_t)p * kmax;
+        for (int j = tid; j < n2 && n1 > 0; j += kFinThreads) {
+            const uint2 v = s2[j];
+            if (v.x == kNoKey || v.x != v.y) continue;
+            const float d = __fsqrt_rn((float)(v.x & kMant));
+            if (ratio_ok(d, d, ratio)) redo[atomicAdd(&hdr[1], 1)] = j;
+        }
+        for (int i = tid; i < n1 && n2 > 0; i += kFinThreads) {
+            const uint2 k = s1[i];
+            if (k.x == kNoKey) continue;
+            const int j = (int)(k.x & imask);
+            const uint32_t d = k.x >> ib;
+            const uint2 v = s2[j];
+            if (v.x == v.y || (v.x & kMant) != d) continue;  // j tied (redo) or j's nearest is not i
+            const float d1r = __fsqrt_rn((float)d);
+            const float d2r = (k.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(k.y >> ib));
+            const float d2c = (v.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(v.y & kMant));
+            if (ratio_ok(d1r, d2r, ratio) && ratio_ok(d1r, d2c, ratio)) push(i, j, d1r);
+        }
+        __syncthreads();
+        const int nredo = hdr[1];
+        for (int r = 0; r < nredo; ++r) {
+            const int j = redo[r];
+            float d1r, d2r, d1c, d2c;
+            int i, jj;
+            block_exact_top2(D2 + (size_t)j * dim, D1, n1, dim, red_d, red_j, d1c, d2c, i);
+            if (i < 0) continue;
+            block_exact_top2(D1 + (size_t)i * dim, D2, n2, dim, red_d, red_j, d1r, d2r, jj);
+            if (tid == 0 && jj == j && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
+            __syncthreads();
+        }
+    }
+    for (int i = tid; i < n1 && n2 > 0 && kRes != kResValues; i += kFinThreads) {
         float d1r, d2r, d1c, d2c;
         int j, ic;
         if (kPacked) {
@@ -446,8 +521,6 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
     __syncthreads();
     if (kPacked) {  // rare: saturated keys -> exact block-wide recomputation of that row and its column
         const int nredo = hdr[1];
-        const float* D1 = desc + (size_t)i1 * kmax * dim;
-        const float* D2 = desc + (size_t)i2 * kmax * dim;
         for (int r = 0; r < nredo; ++r) {
             const int i = redo[r];
             float d1r, d2r, d1c, d2c;
@@ -515,7 +588,7 @@ int launch_mnn_t(const _Float16* a_form, const _Float16* b_form, const int* coun
         GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)mnn_mfma_kernel<NK, kFast>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     hipLaunchKernelGGL((mnn_mfma_kernel<NK, kFast>), dim3(n_pairs), dim3(kThreads), lds, stream, a_form, b_form,
-                       counts, pairs, kpad, kmax, ib, rowres, colres);
+                       counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
 
@@ -527,17 +600,18 @@ int launch_mnn(const _Float16* a_form, const _Float16* b_form, const int* counts
     return launch_mnn_t<NK, false>(a_form, b_form, counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream);
 }
 
-template <bool kPacked>
-int launch_finalize(const void* rowres, const void* colres, const float* desc, const int* counts, const int* pairs,
+// side1 / side2: per-keypoint top-2 of image i1 / image i2 of each pair (encoding kRes)
+template <int kRes>
+int launch_finalize(const void* side1, const void* side2, const float* desc, const int* counts, const int* pairs,
                     int n_pairs, int kmax, int dim, int ib, double ratio, uint32_t* out_idx, int* out_count,
                     hipStream_t stream) {
     const size_t lds = 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * 4, 16) +
                        (size_t)next_pow2(kmax) * sizeof(unsigned long long);
     if (lds > 160 * 1024) return GTSFM_ERR_ARG;
     if (lds > 65536)
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)match_finalize_kernel<kPacked>,
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)match_finalize_kernel<kRes>,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(match_finalize_kernel<kPacked>, dim3(n_pairs), dim3(kFinThreads), lds, stream, rowres, colres,
+    hipLaunchKernelGGL(match_finalize_kernel<kRes>, dim3(n_pairs), dim3(kFinThreads), lds, stream, side1, side2,
                        desc, counts, pairs, kmax, dim, ib, ratio, out_idx, out_count);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
@@ -587,8 +661,12 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
             default: return GTSFM_ERR_ARG;
         }
         if (rc != GTSFM_OK) return rc;
-        return launch_finalize<true>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
-                                     d_out_idx, d_out_count, stream);
+        // the GEMM's columns are image i1's keypoints (side1), its rows image i2's (side2)
+        if (ib <= 12)
+            return launch_finalize<kResValues>(colres, rowres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib,
+                                               ratio, d_out_idx, d_out_count, stream);
+        return launch_finalize<kResKeys>(colres, rowres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
+                                         d_out_idx, d_out_count, stream);
     }
     if (mode != GTSFM_MATCH_EXACT_F32) return GTSFM_ERR_ARG;
     const size_t res_bytes = gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
@@ -599,8 +677,8 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
     GTSFM_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(exact_top2_kernel, grid, dim3(128), 0, stream, d_desc, d_counts, kmax, dim, d_pairs, 1, colres);
     GTSFM_CHECK_HIP(hipGetLastError());
-    return launch_finalize<false>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, 0, ratio, d_out_idx,
-                                  d_out_count, stream);
+    return launch_finalize<kResExact>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, 0, ratio,
+                                      d_out_idx, d_out_count, stream);
 }
 
 }  // extern "C"

@@ -97,6 +97,20 @@ def test_ties_take_lowest_index(dev, oracle_mod):
         np.testing.assert_array_equal(match_descriptor_pair(a, b, ratio), oracle_mod.twoway_match(a, b, ratio))
 
 
+def test_ties_on_both_sides(dev, oracle_mod):
+    """Duplicates in both images (zero distances, tied minima on the query and the train side): the kernel keeps
+    value-only top-2s for image i2, so tied i2 keypoints go through the exact recomputation in finalize."""
+    from gtsfm_amd.frontend.matcher.twoway_matcher import match_descriptor_pair
+
+    rng = np.random.default_rng(13)
+    base = _sift_like(rng, 150)
+    a = np.concatenate([base[:60], base[:60], _sift_like(rng, 200), base[60:90]])
+    b = np.concatenate([base[:90], base[30:60], _sift_like(rng, 90), base[:20]])
+    for ratio in (None, 0.8, 1.0):
+        np.testing.assert_array_equal(match_descriptor_pair(a, b, ratio), oracle_mod.twoway_match(a, b, ratio))
+        np.testing.assert_array_equal(match_descriptor_pair(b, a, ratio), oracle_mod.twoway_match(b, a, ratio))
+
+
 def test_nan_rows_and_empty(dev, oracle_mod):
     from gtsfm_amd.frontend.matcher.twoway_matcher import TwoWayMatcher
 

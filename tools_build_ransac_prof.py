@@ -17,8 +17,8 @@ anchors = [  # (text that starts a line, mark id) -- mark k times the code since
 for text, k in anchors:
     assert s.count(text) == 1, text
     s = s.replace(text, f"    prof_mark({k});\n" + text)
-s = s.replace("    if (sample5(seed, pair_id_base + p, done + lane, M, idx)) {",
-              "    prof_mark(-1);\n    if (sample5(seed, pair_id_base + p, done + lane, M, idx)) {")
+s = s.replace("    if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + lane, M, idx)) {",
+              "    prof_mark(-1);\n    if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + lane, M, idx)) {")
 hdr = """
 __device__ unsigned long long g_prof[16];
 __device__ __forceinline__ void prof_mark(int k) {
@@ -42,5 +42,6 @@ subprocess.check_call([hipcc, *flags, "-c", "/tmp/prof/ransac_prof.hip", "-o", "
 obj = f"{REPO}/gtsfm_amd/_lib/obj"
 os.makedirs(f"{REPO}/gtsfm_amd/_lib/prof", exist_ok=True)
 subprocess.check_call([hipcc, "-shared", "-fPIC", "--offload-arch=gfx950", "-o", f"{REPO}/gtsfm_amd/_lib/prof/libgtsfm_hip.so",
-                       f"{obj}/capi.o", f"{obj}/matcher.o", f"{obj}/sift.o", "/tmp/prof/ransac_prof.o"])
+                       *[os.path.join(obj, f) for f in sorted(os.listdir(obj)) if f.endswith(".o") and f != "ransac.o"],
+                       "/tmp/prof/ransac_prof.o"])
 print("built")
