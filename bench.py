@@ -93,6 +93,20 @@ class FrontEnd:
         return n_ok, (feats, idx, mcnt, res)
 
 
+def pmc_traffic():
+    """HBM bytes per mnn_mfma_kernel launch from the committed rocprofv3 --pmc summary of this bench's command
+    (profiles/*_mnn_pmc.json, written by tools_pmc_summary.py --json): FETCH_SIZE doubled per MI355X_MICROARCH.md
+    (gfx950 tallies 128-B reads at 64 B) + WRITE_SIZE, in bytes. None when no summary is committed."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_mnn_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return float(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+
+
 def cpu_baseline(scene, kpts: int) -> dict:
     """Oracle restatement timed on host cores (1 thread) on a bounded sample, scaled to the full workload."""
     from oracle import oracle
@@ -179,28 +193,44 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = fe.total_pairs / (elapsed / args.steps)
 
-    # stage split + roofline of the dominant kernels (HIP events on the stream the kernels run on)
+    # stage split + roofline of the dominant kernel. HIP events on the stream the kernels run on (torch's current
+    # stream): stage events from Python, the distance-GEMM kernel's own pair through gtsfm_match_set_kernel_events.
     names = ["t0", "t1", "t2", "t3", "t4"]
     stage_ms = {"extract": [], "allgather": [], "match": [], "verify": []}
-    for _ in range(2):
+    kernel_ms = []
+    lib = native.lib()
+    for _ in range(3):
         evs = {k: torch.cuda.Event(enable_timing=True) for k in names}
+        kev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for e in kev:
+            e.record()  # creates the hipEvent_t handle
+        native.check(lib.gtsfm_match_set_kernel_events(kev[0].cuda_event, kev[1].cuda_event), "set_kernel_events")
         _, (feats, idx, mcnt, res) = fe.step(evs)
         torch.cuda.synchronize()
+        native.check(lib.gtsfm_match_set_kernel_events(None, None), "set_kernel_events")
+        kernel_ms.append(kev[0].elapsed_time(kev[1]))
         stage_ms["extract"].append(evs["t0"].elapsed_time(evs["t1"]))
         stage_ms["allgather"].append(evs["t1"].elapsed_time(evs["t2"]))
         stage_ms["match"].append(evs["t2"].elapsed_time(evs["t3"]))
         stage_ms["verify"].append(evs["t3"].elapsed_time(evs["t4"]))
     stage = {k: float(np.mean(v)) for k, v in stage_ms.items()}
+    mnn_ms = float(np.mean(kernel_ms))
     counts = feats.count
     (counts_all,) = sharding.allgather_features((counts,), fe.n_per)
     c = counts_all.to(torch.float64)
     pairs = fe.pairs.long()
     match_flops = float((2.0 * c[pairs[:, 0]] * c[pairs[:, 1]] * 128).sum().item())
-    match_tflops = match_flops / (stage["match"] * 1e-3) / 1e12
+    match_tflops = match_flops / (mnn_ms * 1e-3) / 1e12
+    # algorithmic bytes of the launch: both fp16 operand forms of every image once + the per-keypoint top-2 records
+    kpad = -(-args.kpts // 256) * 256
+    n_rows = world * fe.n_per
+    algo_bytes = 2 * n_rows * kpad * 144 * 2 + 2 * len(pairs) * args.kpts * 8
+    traffic = pmc_traffic()
     roof = {"bound": "mfma", "achieved": round(match_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(match_tflops / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": "mnn_mfma_kernel (+pack, finalize) per batched match launch",
-            "work": "2*K1*K2*128 flop per pair, summed over the launch's pairs"}
+            "frac": round(match_tflops / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
+            "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
+            "kernel": "mnn_mfma_kernel (one launch per step)", "kernel_ms": round(mnn_ms, 3),
+            "work": "2*K1*K2*128 flop per pair, summed over the launch's pairs (GFLOP: %.1f)" % (match_flops / 1e9)}
 
     out = {
         "metric": "verified image-pairs/sec (all-pairs front-end), N images @ 2048 kpts/img",

@@ -13,11 +13,12 @@
 // Every factor is an integer exactly representable in fp16 and every partial sum is an integer < 2^24,
 // so the fp32 accumulation is exact in any order: d2 = |a|^2 + |b|^2 - 2 a.b exactly.
 // The epilogue keeps a running top-2 per row in registers and per column through LDS; the K1 x K2 matrix is never
-// written to HBM. Columns track packed keys d2 << ib | row (ib = max(11, ceil log2 kmax)), inserted two at a time
-// (v_min3 + v_med3 + v_min per pair). Rows track distance VALUES only (v_med3 + v_min on the raw accumulator bits, no
-// key build): a column's best row i is row i's argmin iff row i's best distance equals the column's and row i has no
-// tie at its minimum; tied rows are recomputed exactly in finalize (rare). 4.5 VALU per distance instead of 6. Lexicographic (d2, index) order == OpenCV's strict-'<' scan order, and for
-// d2 < 2^22 ordering by d2 equals ordering by sqrtf(d2), so results are bit-identical to the oracle.
+// written to HBM. Columns (image i1) track packed keys d2 << ib | row (ib = max(11, ceil log2 kmax)); rows (image i2)
+// track distance VALUES only, with no key build. Both insert two values at a time (v_min3 + v_med3 + v_min per pair):
+// 3.8 VALU per distance. In finalize, i1's keypoint i with nearest j is mutual iff j's best distance equals d(i, j) and
+// j has no tie at its minimum; tied j are recomputed exactly (rare). Lexicographic (d2, index) order == OpenCV's
+// strict-'<' scan order, and for d2 < 2^22 ordering by d2 equals ordering by sqrtf(d2), so results are bit-identical
+// to the oracle.
 //
 // Exact path (GTSFM_MATCH_EXACT_F32): float descriptors, per-row sequential fp32 sums (no FMA
 // contraction), top-2 on sqrtf distances — the oracle's arithmetic, for tests and non-SIFT data.
@@ -616,9 +617,17 @@ int launch_finalize(const void* side1, const void* side2, const float* desc, con
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
 
+hipEvent_t g_mnn_events[2] = {nullptr, nullptr};  // gtsfm_match_set_kernel_events
+
 }  // namespace
 
 extern "C" {
+
+int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop) {
+    g_mnn_events[0] = (hipEvent_t)hip_event_start;
+    g_mnn_events[1] = (hipEvent_t)hip_event_stop;
+    return GTSFM_OK;
+}
 
 size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, int mode) {
     if (n_img <= 0 || kmax <= 0 || dim <= 0 || n_pairs < 0) return 0;
@@ -654,6 +663,7 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
                            dim, kpad, da, a_form, b_form);
         GTSFM_CHECK_HIP(hipGetLastError());
         int rc;
+        if (g_mnn_events[0]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[0], stream));
         switch (nk) {
             case 2: rc = launch_mnn<2>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
             case 5: rc = launch_mnn<5>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
@@ -661,6 +671,7 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
             default: return GTSFM_ERR_ARG;
         }
         if (rc != GTSFM_OK) return rc;
+        if (g_mnn_events[1]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[1], stream));
         // the GEMM's columns are image i1's keypoints (side1), its rows image i2's (side2)
         if (ib <= 12)
             return launch_finalize<kResValues>(colres, rowres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib,

@@ -66,6 +66,11 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
                         const int* d_pairs, int n_pairs, double ratio, int mode, void* d_workspace,
                         size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count, void* stream);
 
+/* Measurement hook (no reference counterpart): hipEvent_t handles recorded on the call's stream immediately before
+ * and after the distance-GEMM kernel of every later GTSFM_MATCH_INT_F16 gtsfm_match_batched call, so a benchmark can
+ * time that one kernel. NULL, NULL switches it off. Process-wide; not thread-safe. */
+int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop);
+
 /* ----------------------------------------------------------------------------------------------
  * Verifier: essential-matrix RANSAC over a batch of image pairs (use_intrinsics_in_verification=True path).
  *

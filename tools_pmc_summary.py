@@ -1,7 +1,11 @@
 """Summarise rocprofv3 --pmc counter_collection CSVs: per kernel, dispatches and mean counter value per dispatch.
 
     python tools_pmc_summary.py <dir-with-run_counter_collection.csv> [...] > summary.txt
+    python tools_pmc_summary.py --json OUT.json --kernel mnn_mfma_kernel <dirs...>
+        -> {"hbm_bytes_per_launch": 2*FETCH_SIZE*1024 + WRITE_SIZE*1024, ...} for bench.py's roofline "traffic"
+           (FETCH_SIZE doubled: gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md "HBM"; both in KiB)
 """
+import json
 import collections
 import csv
 import glob
@@ -10,8 +14,16 @@ import sys
 
 
 def main():
+    args = sys.argv[1:]
+    out_json = kernel_sub = None
+    if args[:1] == ["--json"]:
+        out_json, args = args[1], args[2:]
+    if args[:1] == ["--kernel"]:
+        kernel_sub, args = args[1], args[2:]
+    sys.argv = [sys.argv[0]] + args
     rows = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
+    cdisp = collections.defaultdict(set)  # per (kernel, counter): dispatches, for counters from separate passes
     for d in sys.argv[1:]:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
@@ -20,6 +32,22 @@ def main():
                     continue
                 rows[k][r["Counter_Name"]] += float(r["Counter_Value"])
                 disp[k].add(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+                cdisp[(k, r["Counter_Name"])].add((f, r.get("Dispatch_Id") or r.get("Correlation_Id")))
+    if out_json:
+        ks = [k for k in rows if kernel_sub in k]
+        assert ks, f"no kernel matching {kernel_sub}"
+        tot = collections.defaultdict(float)
+        cnt = collections.defaultdict(int)
+        for k in ks:
+            for c, v in rows[k].items():
+                tot[c] += v
+                cnt[c] += len(cdisp[(k, c)])
+        per = {c: v / max(cnt[c], 1) for c, v in tot.items()}
+        res = {"kernel": kernel_sub, "dispatches": dict(cnt), "counters_per_launch": per,
+               "hbm_bytes_per_launch": 2 * per.get("FETCH_SIZE", 0.0) * 1024 + per.get("WRITE_SIZE", 0.0) * 1024}
+        json.dump(res, open(out_json, "w"), indent=1)
+        print(json.dumps(res))
+        return
     for k in sorted(rows, key=lambda k: -sum(rows[k].values())):
         n = max(len(disp[k]), 1)
         vals = " ".join(f"{c}={v / n:.4g}" for c, v in sorted(rows[k].items()))
