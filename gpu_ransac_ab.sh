@@ -1,0 +1,11 @@
+#!/bin/bash
+# Verifier parity tests (E and F paths, batched drop-ins) + a short bench line.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_verifier_gpu.py tests/test_fundamental_gpu.py tests/test_frontend_batched_gpu.py -x -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/pytest_rab.log 2>&1
+rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_rab.log | tail -15; [ $rc -eq 0 ] || { grep -B5 -A25 "Error\|assert" gpurun_out/pytest_rab.log | tail -50; exit $rc; }
+timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rab.json 2> gpurun_out/bench_rab.err
+rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_rab.err; exit $rc; }
+python -c "import json; d=json.load(open('gpurun_out/bench_rab.json')); print('value', d['value'], 'ms', d['ms_per_step'], 'isp', d['pairs_passing_isp'], 'stage', d['stage_ms'])"

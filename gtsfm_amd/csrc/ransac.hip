@@ -75,14 +75,22 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 }
 
 // ------------------------------------------------------------------ lane-private arrays in LDS
-// The solver's dynamically indexed arrays (the 5x9 and 10x20 eliminations, the Sturm chain, the isolation stack)
-// live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit consecutive 8-byte words, so every
-// access is bank-conflict free, and nothing spills to scratch. One 64-lane workgroup owns 102 KB + 16 KB.
+// The solver's dynamically indexed arrays live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit
+// consecutive words, so every access is bank-conflict free, and nothing spills to scratch. The solver runs in two
+// kernels so each one's workgroup holds only its own phase's arrays:
+//   stage 1 (sample, 5x9 nullspace, 10x20 Gauss-Jordan): Q (45) | A (200) doubles + column permutation (9 ints)
+//       = 101 KB per 64-lane workgroup (one per CU);
+//   stage 2 (det B(z), Sturm chain, isolation, bisection, E): triangular Sturm rows (66) + prem scratch (11) |
+//       isolation stack (2 x 24) + intervals (2 x 10) doubles, stack counts and chain degrees as bytes
+//       = 42.5 KB per workgroup (three per CU).
 constexpr int kLanes = 64;
-constexpr int kUnion = 200;   // doubles per lane: Q (45) | A (200) | Sturm (121) + t (11) + stack (2 x 24)
-constexpr int kInts = 112;    // ints per lane: col perm (9) | stack va/vb (2 x 48) + chain degrees (11)
-constexpr int kStack = 48;  // == oracle/ransac.c isolation stack
+constexpr int kUnion = 200;   // stage-1 doubles per lane: Q (45) | A (200)
+constexpr int kInts = 9;      // stage-1 ints per lane: column permutation
+constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
+constexpr int kRootDbl = 77;  // stage-2 doubles per lane: Sturm rows (66) + t (11) | stack (48) + intervals (20)
+constexpr int kRootB = 64;    // stage-2 bytes per lane: stack va/vb (2 x 24) + chain degrees (11), padded
 constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double) + (size_t)kInts * kLanes * sizeof(int);
+constexpr size_t kRootLds = (size_t)kRootDbl * kLanes * sizeof(double) + (size_t)kRootB * kLanes;
 
 template <typename T>
 struct LaneArr {
@@ -122,6 +130,17 @@ __device__ __forceinline__ SolverMem solver_mem(unsigned char* smem, int lane) {
     double* d = (double*)smem;
     int* iv = (int*)(smem + (size_t)kUnion * kLanes * sizeof(double));
     return SolverMem{LaneArr<double>{d + lane}, LaneArr<int>{iv + lane}};
+}
+
+struct RootMem {
+    LaneArr<double> u;     // kRootDbl doubles
+    LaneArr<uint8_t> b;    // kRootB bytes
+};
+
+__device__ __forceinline__ RootMem root_mem(unsigned char* smem, int lane) {
+    double* d = (double*)smem;
+    uint8_t* b = smem + (size_t)kRootDbl * kLanes * sizeof(double);
+    return RootMem{LaneArr<double>{d + lane}, LaneArr<uint8_t>{b + lane}};
 }
 
 // Register-resident Sturm chain: row k (degree <= 10 - k) at kRowOff[k], zero-padded to length 11 - k. Horner over
@@ -171,22 +190,22 @@ __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
 // bisected together (10 independent chains), so a wave never serialises one lane's bisection behind another's
 // isolation step.
 template <typename RootFn>
-__device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_root) {
-    LaneArr<double> S = m.u;  // chain rows at 11*k during construction
-    LaneArr<double> t = m.u.at(121);
-    LaneArr<int> sdeg = m.iv.at(2 * kStack);
+__device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_root) {
+    LaneArr<double> S = m.u;  // chain row k at row_off(k) (degree <= 10 - k) during construction
+    LaneArr<double> t = m.u.at(kChain);
+    LaneArr<uint8_t> sdeg = m.b.at(2 * kStack);
     while (deg > 0 && fabs(pin[deg]) <= 1e-300) --deg;
     if (deg <= 0) return 0;
     for (int i = 0; i <= deg; ++i) S[i] = pin[i] / pin[deg];
-    sdeg[0] = deg;
-    for (int i = 1; i <= deg; ++i) S[11 + i - 1] = (double)i * S[i];
-    sdeg[1] = deg - 1;
+    sdeg[0] = (uint8_t)deg;
+    for (int i = 1; i <= deg; ++i) S[row_off(1) + i - 1] = (double)i * S[i];
+    sdeg[1] = (uint8_t)(deg - 1);
     int n = 2;
     while (n < 11 && sdeg[n - 1] > 0) {
-        const int dr = prem(S.at(11 * (n - 2)), sdeg[n - 2], S.at(11 * (n - 1)), sdeg[n - 1], S.at(11 * n), t);
+        const int dr = prem(S.at(row_off(n - 2)), sdeg[n - 2], S.at(row_off(n - 1)), sdeg[n - 1], S.at(row_off(n)), t);
         if (dr < 0) break;
-        for (int i = 0; i <= dr; ++i) S[11 * n + i] = -S[11 * n + i];
-        sdeg[n] = dr;
+        for (int i = 0; i <= dr; ++i) S[row_off(n) + i] = -S[row_off(n) + i];
+        sdeg[n] = (uint8_t)dr;
         n++;
     }
     double R[kChain];
@@ -194,7 +213,7 @@ __device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_r
     for (int k = 0; k < 11; ++k) {
         const int dk = k < n ? sdeg[k] : -1;
 #pragma unroll
-        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dk ? S[11 * k + i] : 0.0;
+        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dk ? S[row_off(k) + i] : 0.0;
     }
     // root bound (== oracle root_bound_pow2): exact exponent arithmetic, a power of two
     double bound;
@@ -214,12 +233,12 @@ __device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_r
     }
     // isolation (stack and the interval list reuse the chain's LDS)
     LaneArr<double> st_a = m.u, st_b = m.u.at(kStack), iv_a = m.u.at(2 * kStack), iv_b = m.u.at(2 * kStack + kMaxSol);
-    LaneArr<int> st_va = m.iv, st_vb = m.iv.at(kStack);
+    LaneArr<uint8_t> st_va = m.b, st_vb = m.b.at(kStack);
     int ns = 1, nr = 0, guard = 0;
     st_a[0] = -bound;
     st_b[0] = bound;
-    st_va[0] = sign_changes_reg(R, -bound);
-    st_vb[0] = sign_changes_reg(R, bound);
+    st_va[0] = (uint8_t)sign_changes_reg(R, -bound);
+    st_vb[0] = (uint8_t)sign_changes_reg(R, bound);
     while (ns > 0 && nr < kMaxSol && guard < 2000) {
         ++guard;
         --ns;
@@ -236,8 +255,8 @@ __device__ int real_roots(const double* pin, int deg, SolverMem m, RootFn&& on_r
         const double mid = 0.5 * (a + b);
         const int vm = sign_changes_reg(R, mid);
         if (ns + 2 <= kStack) {
-            st_a[ns] = mid; st_b[ns] = b; st_va[ns] = vm; st_vb[ns] = vb; ++ns;
-            st_a[ns] = a; st_b[ns] = mid; st_va[ns] = va; st_vb[ns] = vm; ++ns;
+            st_a[ns] = mid; st_b[ns] = b; st_va[ns] = (uint8_t)vm; st_vb[ns] = (uint8_t)vb; ++ns;
+            st_a[ns] = a; st_b[ns] = mid; st_va[ns] = (uint8_t)va; st_vb[ns] = (uint8_t)vm; ++ns;
         }
     }
     double lo[kMaxSol], hi[kMaxSol], flo[kMaxSol];
@@ -351,11 +370,13 @@ __device__ __forceinline__ void addmul_ql_lds(const double* q, const double* l, 
         for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += s * (q[i] * l[j]);
 }
 
-// 5 correspondences -> up to 10 unit-norm E; on_sol(s, E) is called for each solution in root order.
-template <typename SolFn>
-__device__ int five_point(const double* x1, const double* x2, SolverMem m, SolFn&& on_sol) {
-    double N[4][9];
-    if (!nullspace_5x9(x1, x2, m, N)) return 0;
+// Nister 5-point, stage 1: 5 correspondences -> nullspace basis N (4 x 9) and rows 4..9, columns 10..19 of the
+// Gauss-Jordan-reduced 10 x 20 constraint matrix (all that stage 2 reads). False for a degenerate sample.
+constexpr int kStageVals = 6 * 10 + 4 * 9;  // doubles handed from stage 1 to stage 2 per hypothesis
+
+__device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem m, double N[4][9],
+                                  double Rt[6][10]) {
+    if (!nullspace_5x9(x1, x2, m, N)) return false;
     double E[9][4];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
@@ -420,7 +441,7 @@ __device__ int five_point(const double* x1, const double* x2, SolverMem m, SolFn
             const double v = fabs(A[20 * r + c]);
             if (v > best) { best = v; pr = r; }
         }
-        if (best < 1e-14) return 0;
+        if (best < 1e-14) return false;
         double prow[20];
 #pragma unroll
         for (int j = 0; j < 20; ++j) prow[j] = A[20 * pr + j];
@@ -448,16 +469,28 @@ __device__ int five_point(const double* x1, const double* x2, SolverMem m, SolFn
             for (int j = 0; j < 20; ++j) A[20 * r + j] = row[j];
         }
     }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int j = 0; j < 10; ++j) Rt[r][j] = A[20 * (4 + r) + 10 + j];
+    return true;
+}
+
+// Stage 2: the 3 x 3 polynomial matrix B(z) from the reduced rows, its degree-10 determinant, real roots, and up to
+// 10 unit-norm E; on_sol(s, E) is called for each solution in root order.
+template <typename SolFn>
+__device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], RootMem m, SolFn&& on_sol) {
     double B[3][3][5];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const int e = 20 * (4 + 2 * r), f = 20 * (5 + 2 * r);
-        B[r][0][0] = A[e + 12]; B[r][0][1] = A[e + 11] - A[f + 12]; B[r][0][2] = A[e + 10] - A[f + 11];
-        B[r][0][3] = -A[f + 10]; B[r][0][4] = 0.0;
-        B[r][1][0] = A[e + 15]; B[r][1][1] = A[e + 14] - A[f + 15]; B[r][1][2] = A[e + 13] - A[f + 14];
-        B[r][1][3] = -A[f + 13]; B[r][1][4] = 0.0;
-        B[r][2][0] = A[e + 19]; B[r][2][1] = A[e + 18] - A[f + 19]; B[r][2][2] = A[e + 17] - A[f + 18];
-        B[r][2][3] = A[e + 16] - A[f + 17]; B[r][2][4] = -A[f + 16];
+        const double* e = Rt[2 * r];  // e[k] == A[20 * (4 + 2r) + 10 + k]
+        const double* f = Rt[2 * r + 1];
+        B[r][0][0] = e[2]; B[r][0][1] = e[1] - f[2]; B[r][0][2] = e[0] - f[1];
+        B[r][0][3] = -f[0]; B[r][0][4] = 0.0;
+        B[r][1][0] = e[5]; B[r][1][1] = e[4] - f[5]; B[r][1][2] = e[3] - f[4];
+        B[r][1][3] = -f[3]; B[r][1][4] = 0.0;
+        B[r][2][0] = e[9]; B[r][2][1] = e[8] - f[9]; B[r][2][2] = e[7] - f[8];
+        B[r][2][3] = e[6] - f[7]; B[r][2][4] = -f[6];
     }
     double n[11];
 #pragma unroll
@@ -863,13 +896,15 @@ __global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int 
     st[p] = s;
 }
 
-// One 64-lane workgroup per active pair: lane l solves hypothesis done + l; candidates (fp64) -> global.
-__global__ __launch_bounds__(64, 1) void ransac_solve_kernel(const int* __restrict__ match_count, int mcap,
-                                                             const double2* __restrict__ x1n_all,
-                                                             const double2* __restrict__ x2n_all, uint64_t seed,
-                                                             int pair_id_base, const int* __restrict__ pair_ids,
-                                                             const PairState* __restrict__ st,
-                                                             double* __restrict__ cand, int* __restrict__ nsol) {
+// Stage 1, one 64-lane workgroup per active pair: lane l samples hypothesis done + l, runs the nullspace and the
+// 10 x 20 elimination, and hands N + the reduced rows to stage 2 through `stage` ([P][kStageVals][64], lane-minor so
+// the stores coalesce). nsol = 1 marks a non-degenerate sample for stage 2, 0 a finished one.
+__global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restrict__ match_count, int mcap,
+                                                              const double2* __restrict__ x1n_all,
+                                                              const double2* __restrict__ x2n_all, uint64_t seed,
+                                                              int pair_id_base, const int* __restrict__ pair_ids,
+                                                              const PairState* __restrict__ st,
+                                                              double* __restrict__ stage, int* __restrict__ nsol) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int p = blockIdx.x, lane = threadIdx.x;
     const int M = match_count[p];
@@ -879,8 +914,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve_kernel(const int* __restri
     const double2* x1 = x1n_all + (size_t)p * mcap;
     const double2* x2 = x2n_all + (size_t)p * mcap;
     const SolverMem mem = solver_mem(smem, lane);
-    double* cout = cand + ((size_t)p * kBatch + lane) * (kMaxSol * 9);
-    int ns = 0;
+    int ok = 0;
     int idx[5];
     if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + lane, M, idx)) {
         double s1[10], s2[10];
@@ -890,12 +924,53 @@ __global__ __launch_bounds__(64, 1) void ransac_solve_kernel(const int* __restri
             s1[2 * k] = a.x; s1[2 * k + 1] = a.y;
             s2[2 * k] = b.x; s2[2 * k + 1] = b.y;
         }
-        ns = five_point(s1, s2, mem, [&](int s, const double* E) {
+        double N[4][9], Rt[6][10];
+        if (five_point_stage1(s1, s2, mem, N, Rt)) {
+            ok = 1;
+            double* out = stage + (size_t)p * kStageVals * kLanes + lane;
 #pragma unroll
-            for (int e = 0; e < 9; ++e) cout[9 * s + e] = E[e];
-        });
+            for (int r = 0; r < 6; ++r)
+#pragma unroll
+                for (int j = 0; j < 10; ++j) out[(10 * r + j) * kLanes] = Rt[r][j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < 9; ++j) out[(60 + 9 * k + j) * kLanes] = N[k][j];
+        }
     }
-    nsol[(size_t)p * kBatch + lane] = ns;
+    nsol[(size_t)p * kBatch + lane] = ok;
+}
+
+// Stage 2, one 64-lane workgroup per active pair (three per CU): lane l turns stage 1's output into the candidate
+// essential matrices of hypothesis done + l (fp64) -> cand, nsol.
+__global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restrict__ match_count,
+                                                              const PairState* __restrict__ st,
+                                                              const double* __restrict__ stage,
+                                                              double* __restrict__ cand, int* __restrict__ nsol) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int M = match_count[p];
+    if (M < 6) return;
+    if (st[p].done >= st[p].niters) return;
+    int* ns_out = nsol + (size_t)p * kBatch + lane;
+    if (*ns_out == 0) return;  // degenerate sample: stays 0
+    const RootMem mem = root_mem(smem, lane);
+    double N[4][9], Rt[6][10];
+    const double* in = stage + (size_t)p * kStageVals * kLanes + lane;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int j = 0; j < 10; ++j) Rt[r][j] = in[(10 * r + j) * kLanes];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) N[k][j] = in[(60 + 9 * k + j) * kLanes];
+    double* cout = cand + ((size_t)p * kBatch + lane) * (kMaxSol * 9);
+    const int ns = five_point_stage2(N, Rt, mem, [&](int s, const double* E) {
+#pragma unroll
+        for (int e = 0; e < 9; ++e) cout[9 * s + e] = E[e];
+    });
+    *ns_out = ns;
 }
 
 // One wave per active pair: scores the batch's candidates in (hypothesis, solution) order, exact early exit,
@@ -1078,7 +1153,7 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
 extern "C" {
 
 static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_pts, size_t* off_st, size_t* off_cand,
-                            size_t* off_nsol) {
+                            size_t* off_nsol, size_t* off_stage) {
     const size_t n = (size_t)n_pairs * mcap;
     size_t o = 0;
     o += gtsfm_align_up(n * sizeof(double2), 256);
@@ -1092,13 +1167,15 @@ static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_p
     o += gtsfm_align_up((size_t)n_pairs * kBatch * kMaxSol * 9 * sizeof(double), 256);
     *off_nsol = o;
     o += gtsfm_align_up((size_t)n_pairs * kBatch * sizeof(int), 256);
+    *off_stage = o;
+    o += gtsfm_align_up((size_t)n_pairs * kStageVals * kBatch * sizeof(double), 256);
     return o;
 }
 
 size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap) {
     if (n_pairs <= 0 || mcap <= 0) return 0;
-    size_t a, b, c, d, e;
-    return ransac_layout(n_pairs, mcap, &a, &b, &c, &d, &e);
+    size_t a, b, c, d, e, f;
+    return ransac_layout(n_pairs, mcap, &a, &b, &c, &d, &e, &f);
 }
 
 int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
@@ -1112,8 +1189,8 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
         !d_n_inliers || !d_status || !d_inlier_mask || n_img <= 0 || kmax <= 0 || n_pairs < 0 || mcap <= 0 ||
         max_iters <= 0 || !(thr_px > 0.0))
         return GTSFM_ERR_ARG;
-    size_t o_x2, o_pts, o_st, o_cand, o_nsol;
-    const size_t need = ransac_layout(n_pairs, mcap, &o_x2, &o_pts, &o_st, &o_cand, &o_nsol);
+    size_t o_x2, o_pts, o_st, o_cand, o_nsol, o_stage;
+    const size_t need = ransac_layout(n_pairs, mcap, &o_x2, &o_pts, &o_st, &o_cand, &o_nsol, &o_stage);
     if (workspace_bytes < need) return GTSFM_ERR_CAPACITY;
     unsigned char* ws = (unsigned char*)d_workspace;
     double2* x1n = (double2*)ws;
@@ -1122,20 +1199,23 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     PairState* st = (PairState*)(ws + o_st);
     double* cand = (double*)(ws + o_cand);
     int* nsol = (int*)(ws + o_nsol);
+    double* stage = (double*)(ws + o_stage);
     hipLaunchKernelGGL(normalize_putatives_kernel, dim3((mcap + 255) / 256, n_pairs), dim3(256), 0, stream, d_kp_xy,
                        d_intrinsics, kmax, d_pairs, d_match_idx, d_match_count, mcap, x1n, x2n, pts);
     hipLaunchKernelGGL(ransac_init_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, stream, st, n_pairs, max_iters);
     GTSFM_CHECK_HIP(hipGetLastError());
     static bool lds_set = false;
     if (!lds_set) {
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)ransac_solve_kernel,
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)ransac_solve1_kernel,
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSolveLds));
         lds_set = true;
     }
     const int n_batches = (max_iters + kBatch - 1) / kBatch;
     for (int b = 0; b < n_batches; ++b) {
-        hipLaunchKernelGGL(ransac_solve_kernel, dim3(n_pairs), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
-                           x2n, seed, pair_id_base, d_pair_ids, st, cand, nsol);
+        hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
+                           x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
+        hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs), dim3(64), kRootLds, stream, d_match_count, st, stage,
+                           cand, nsol);
         hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics,
                            d_match_count, mcap, pts, thr_px, prob, cand, nsol, st);
     }

@@ -14,7 +14,8 @@ from typing import Optional
 import torch  # noqa: F401  (must precede the CDLL load: one HIP runtime per process)
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG_DIR, "_lib", "libgtsfm_hip.so")
+# GTSFM_HIP_LIB: development override (instrumented or experimental builds of the same ABI); unset in production
+LIB_PATH = os.environ.get("GTSFM_HIP_LIB") or os.path.join(_PKG_DIR, "_lib", "libgtsfm_hip.so")
 CSRC_DIR = os.path.join(_PKG_DIR, "csrc")
 
 _lib: Optional[ctypes.CDLL] = None

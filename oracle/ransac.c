@@ -32,6 +32,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* isolation stack depth (== gtsfm_amd/csrc/ransac.hip kStack): the DFS holds at most one pending interval per
+ * bisection level, so 24 separates roots down to 2 * bound / 2^23 apart; closer pairs are skipped */
+#define ISO_STACK 24
+
 #define NMONO 20
 #define RANSAC_BATCH 64
 #define MAX_SOL 10
@@ -183,8 +187,8 @@ static int real_roots(const double* pin, int deg, double* roots) {
     }
     const double bound = root_bound_pow2(p, deg);
     /* isolation by bisection with Sturm counts */
-    double st_a[48], st_b[48];
-    int st_va[48], st_vb[48], ns = 0, nr = 0;
+    double st_a[ISO_STACK], st_b[ISO_STACK];
+    int st_va[ISO_STACK], st_vb[ISO_STACK], ns = 0, nr = 0;
     st_a[0] = -bound;
     st_b[0] = bound;
     st_va[0] = sign_changes(&s, -bound);
@@ -231,7 +235,7 @@ static int real_roots(const double* pin, int deg, double* roots) {
         }
         const double mid = 0.5 * (a + b);
         const int vm = sign_changes(&s, mid);
-        if (ns + 2 <= 48) {
+        if (ns + 2 <= ISO_STACK) {
             /* push right then left so that the left interval is processed first (ascending roots) */
             st_a[ns] = mid; st_b[ns] = b; st_va[ns] = vm; st_vb[ns] = vb; ++ns;
             st_a[ns] = a; st_b[ns] = mid; st_va[ns] = va; st_vb[ns] = vm; ++ns;
