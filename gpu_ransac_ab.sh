@@ -9,3 +9,6 @@ rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/pytest_rab.log | tail 
 timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rab.json 2> gpurun_out/bench_rab.err
 rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_rab.err; exit $rc; }
 python -c "import json; d=json.load(open('gpurun_out/bench_rab.json')); print('value', d['value'], 'ms', d['ms_per_step'], 'isp', d['pairs_passing_isp'], 'stage', d['stage_ms'])"
+cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_rab -o run -- python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_rab.log 2>&1
+rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+python $GRAFT_REPO_ROOT/tools_kstats.py $GRAFT_REPO_ROOT/gpurun_out/prof_rab/run_kernel_stats.csv | head -12

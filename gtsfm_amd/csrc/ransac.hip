@@ -80,14 +80,14 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 // kernels so each one's workgroup holds only its own phase's arrays:
 //   stage 1 (sample, 5x9 nullspace, 10x20 Gauss-Jordan): Q (45) | A (200) doubles + column permutation (9 ints)
 //       = 101 KB per 64-lane workgroup (one per CU);
-//   stage 2 (det B(z), Sturm chain, isolation, bisection, E): triangular Sturm rows (66) + prem scratch (11) |
-//       isolation stack (2 x 24) + intervals (2 x 10) doubles, stack counts and chain degrees as bytes
-//       = 42.5 KB per workgroup (three per CU).
+//   stage 2 (det B(z), Sturm chain, isolation, bisection, E): a rolling window of three Sturm rows (3 x 11) + prem
+//       scratch (11) | isolation stack (2 x 24) + intervals (2 x 10) doubles, stack counts and chain degrees as
+//       bytes = 38 KB per workgroup (four per CU). Finished chain rows go straight to the register chain R.
 constexpr int kLanes = 64;
 constexpr int kUnion = 200;   // stage-1 doubles per lane: Q (45) | A (200)
 constexpr int kInts = 9;      // stage-1 ints per lane: column permutation
 constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
-constexpr int kRootDbl = 77;  // stage-2 doubles per lane: Sturm rows (66) + t (11) | stack (48) + intervals (20)
+constexpr int kRootDbl = 68;  // stage-2 doubles per lane: 3 Sturm rows (33) + t (11) | stack (48) + intervals (20)
 constexpr int kRootB = 64;    // stage-2 bytes per lane: stack va/vb (2 x 24) + chain degrees (11), padded
 constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double) + (size_t)kInts * kLanes * sizeof(int);
 constexpr size_t kRootLds = (size_t)kRootDbl * kLanes * sizeof(double) + (size_t)kRootB * kLanes;
@@ -191,29 +191,37 @@ __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
 // isolation step.
 template <typename RootFn>
 __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_root) {
-    LaneArr<double> S = m.u;  // chain row k at row_off(k) (degree <= 10 - k) during construction
-    LaneArr<double> t = m.u.at(kChain);
+    LaneArr<double> S = m.u;  // chain row k in slot k % 3 (11 doubles each) while it is still needed by prem
+    LaneArr<double> t = m.u.at(33);
     LaneArr<uint8_t> sdeg = m.b.at(2 * kStack);
     while (deg > 0 && fabs(pin[deg]) <= 1e-300) --deg;
     if (deg <= 0) return 0;
     for (int i = 0; i <= deg; ++i) S[i] = pin[i] / pin[deg];
     sdeg[0] = (uint8_t)deg;
-    for (int i = 1; i <= deg; ++i) S[row_off(1) + i - 1] = (double)i * S[i];
+    for (int i = 1; i <= deg; ++i) S[11 + i - 1] = (double)i * S[i];
     sdeg[1] = (uint8_t)(deg - 1);
-    int n = 2;
-    while (n < 11 && sdeg[n - 1] > 0) {
-        const int dr = prem(S.at(row_off(n - 2)), sdeg[n - 2], S.at(row_off(n - 1)), sdeg[n - 1], S.at(row_off(n)), t);
-        if (dr < 0) break;
-        for (int i = 0; i <= dr; ++i) S[row_off(n) + i] = -S[row_off(n) + i];
-        sdeg[n] = (uint8_t)dr;
-        n++;
-    }
+    // register chain: rows 0 and 1 now, row n as soon as prem produces it (rows past the chain stay 0)
     double R[kChain];
 #pragma unroll
-    for (int k = 0; k < 11; ++k) {
-        const int dk = k < n ? sdeg[k] : -1;
+    for (int k = 0; k < 2; ++k)
 #pragma unroll
-        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dk ? S[row_off(k) + i] : 0.0;
+        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= (int)sdeg[k] ? S[11 * k + i] : 0.0;
+#pragma unroll
+    for (int i = row_off(2); i < kChain; ++i) R[i] = 0.0;
+    int n = 2;
+    while (n < 11 && sdeg[n - 1] > 0) {
+        const int so = 11 * (n % 3), sa = 11 * ((n - 2) % 3), sb = 11 * ((n - 1) % 3);
+        const int dr = prem(S.at(sa), sdeg[n - 2], S.at(sb), sdeg[n - 1], S.at(so), t);
+        if (dr < 0) break;
+        for (int i = 0; i <= dr; ++i) S[so + i] = -S[so + i];
+        sdeg[n] = (uint8_t)dr;
+#pragma unroll
+        for (int k = 2; k < 11; ++k)
+            if (k == n) {
+#pragma unroll
+                for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dr ? S[so + i] : 0.0;
+            }
+        n++;
     }
     // root bound (== oracle root_bound_pow2): exact exponent arithmetic, a power of two
     double bound;
