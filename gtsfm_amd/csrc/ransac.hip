@@ -981,15 +981,26 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
     *ns_out = ns;
 }
 
-// One wave per active pair: scores the batch's candidates in (hypothesis, solution) order, exact early exit,
-// keeps the first best, applies the OpenCV iteration bound after the batch.
-__global__ __launch_bounds__(64) void ransac_score_kernel(const int* __restrict__ pairs,
-                                                          const double* __restrict__ intr,
-                                                          const int* __restrict__ match_count, int mcap,
-                                                          const float4* __restrict__ pts_all, double thr_px,
-                                                          double prob, const double* __restrict__ cand,
-                                                          const int* __restrict__ nsol, PairState* __restrict__ st) {
-    const int p = blockIdx.x, lane = threadIdx.x;
+// One 4-wave workgroup per active pair: the pair's putatives are staged in LDS once, the batch's candidates
+// (flattened in (hypothesis, solution) order) are dealt round-robin to the waves, each counted by one wave with an
+// exact early exit against the running best. The best is an LDS atomicMax on the key (count + 1, ~index), so the
+// winner is the FIRST candidate in order with the largest count, as in the sequential scan of oracle/ransac.c: a
+// candidate stops once it can no longer beat the current best count, or only tie it from a later index. Then the
+// OpenCV iteration bound is applied after the batch.
+constexpr int kScoreWaves = 4;
+
+__global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,
+                                                                        const double* __restrict__ intr,
+                                                                        const int* __restrict__ match_count, int mcap,
+                                                                        const float4* __restrict__ pts_all,
+                                                                        double thr_px, double prob,
+                                                                        const double* __restrict__ cand,
+                                                                        const int* __restrict__ nsol,
+                                                                        PairState* __restrict__ st) {
+    extern __shared__ float4 spts[];  // [M]
+    __shared__ unsigned long long best_key;
+    __shared__ int flat_off[kBatch + 1];  // candidates of hypotheses < h
+    const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int M = match_count[p];
     if (M < 6) return;
     PairState s = st[p];
@@ -999,36 +1010,70 @@ __global__ __launch_bounds__(64) void ransac_score_kernel(const int* __restrict_
     const double thr = thr_px / fx;
     const float thr2 = (float)(thr * thr);
     const float4* pts = pts_all + (size_t)p * mcap;
-    bool improved = false;
-    int imp_h = 0, imp_s = 0;
-    for (int hl = 0; hl < kBatch; ++hl) {
-        const int nsh = nsol[(size_t)p * kBatch + hl];
-        const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9);
-        for (int sI = 0; sI < nsh; ++sI) {
-            float E[9];
+    for (int i = tid; i < M; i += 64 * kScoreWaves) spts[i] = pts[i];
+    if (wave == 0) {
+        int v = nsol[(size_t)p * kBatch + lane];
 #pragma unroll
-            for (int e = 0; e < 9; ++e) E[e] = (float)ch[9 * sI + e];
-            const int c = wave_count(E, pts, M, thr2, s.best, lane);
-            if (c > s.best) {
-                s.best = c;
-                s.best_h = s.done + hl;
-                s.best_s = sI;
-                improved = true;
-                imp_h = hl;
-                imp_s = sI;
-            }
+        for (int m = 1; m < 64; m <<= 1) {  // inclusive scan over the 64 hypotheses
+            const int o = __shfl_up(v, m);
+            if (lane >= m) v += o;
+        }
+        flat_off[lane + 1] = v;
+        if (lane == 0) {
+            flat_off[0] = 0;
+            best_key = ((unsigned long long)(uint32_t)(s.best + 1) << 32) | 0xFFFFFFFFull;  // index -1: before all
         }
     }
-    if (improved) {
-        const double* ch = cand + ((size_t)p * kBatch + imp_h) * (kMaxSol * 9);
-        for (int e = 0; e < 9; ++e) s.bestE[e] = ch[9 * imp_s + e];
+    __syncthreads();
+    const int total = flat_off[kBatch];
+    for (int ci = wave; ci < total; ci += kScoreWaves) {
+        const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
+        const int sI = ci - flat_off[hl];
+        const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9) + 9 * sI;
+        float E[9];
+#pragma unroll
+        for (int e = 0; e < 9; ++e) E[e] = (float)ch[e];
+        const uint32_t my_low = 0xFFFFFFFEu - (uint32_t)ci;
+        int c = 0;
+        bool alive = true;
+        for (int base = 0; base < M; base += 64) {
+            const int i = base + lane;
+            const bool in = i < M && sampson_inlier(E, spts[i], thr2);
+            c += __popcll(__ballot(in));
+            const int remaining = M - (base + 64);
+            if (remaining > 0) {
+                const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
+                const int bc = (int)(bk >> 32) - 1;
+                if (c + remaining < bc || (c + remaining == bc && my_low < (uint32_t)bk)) {
+                    alive = false;
+                    break;
+                }
+            }
+        }
+        if (alive && lane == 0) atomicMax(&best_key, ((unsigned long long)(uint32_t)(c + 1) << 32) | my_low);
     }
-    s.done += kBatch;
-    if (s.best > 0) {
-        const int upd = update_num_iters(prob, (double)(M - s.best) / M, 5, s.niters);
-        if (upd < s.niters) s.niters = upd;
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long bk = best_key;
+        const uint32_t low = (uint32_t)bk;
+        if (low != 0xFFFFFFFFu) {  // a candidate of this batch beat the previous best
+            const int ci = (int)(0xFFFFFFFEu - low);
+            int hl = 0;
+            while (flat_off[hl + 1] <= ci) ++hl;
+            const int sI = ci - flat_off[hl];
+            s.best = (int)(bk >> 32) - 1;
+            s.best_h = s.done + hl;
+            s.best_s = sI;
+            const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9) + 9 * sI;
+            for (int e = 0; e < 9; ++e) s.bestE[e] = ch[e];
+        }
+        s.done += kBatch;
+        if (s.best > 0) {
+            const int upd = update_num_iters(prob, (double)(M - s.best) / M, 5, s.niters);
+            if (upd < s.niters) s.niters = upd;
+        }
+        st[p] = s;
     }
-    if (lane == 0) st[p] = s;
 }
 
 // Per pair: status, iterative LO from the best hypothesis, final mask, recoverPose.
@@ -1218,13 +1263,24 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSolveLds));
         lds_set = true;
     }
+    const size_t score_lds = (size_t)mcap * sizeof(float4);  // the pair's putatives
+    if (score_lds > 150 * 1024) return GTSFM_ERR_ARG;
+    if (score_lds > 65536) {
+        static size_t score_lds_set = 0;
+        if (score_lds > score_lds_set) {
+            GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)ransac_score_kernel,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)score_lds));
+            score_lds_set = score_lds;
+        }
+    }
     const int n_batches = (max_iters + kBatch - 1) / kBatch;
     for (int b = 0; b < n_batches; ++b) {
         hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
                            x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs), dim3(64), kRootLds, stream, d_match_count, st, stage,
                            cand, nsol);
-        hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics,
+        hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream, d_pairs,
+                           d_intrinsics,
                            d_match_count, mcap, pts, thr_px, prob, cand, nsol, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
