@@ -779,25 +779,86 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
 #pragma unroll
     for (int k = 0; k < 45; ++k)
         for (int m = 1; m < 64; m <<= 1) acc[k] += shfl_xor_d(acc[k], m);
-    if (lane < 45) {
-        int a = 0, k = lane;
-        while (k >= 9 - a) { k -= 9 - a; ++a; }
-        const int b = a + k;
-        double v = acc[0];
-#pragma unroll
-        for (int q = 1; q < 45; ++q) v = q == lane ? acc[q] : v;
-        jac_a[a * 9 + b] = v;
-        jac_a[b * 9 + a] = v;
-    }
-    __syncthreads();
-    jacobi9_lds(jac_a, jac_v, lane);
-    int imin = 0;
-    double wmin = jac_a[0];
-    for (int i = 1; i < 9; ++i)
-        if (jac_a[i * 9 + i] < wmin) { wmin = jac_a[i * 9 + i]; imin = i; }
+    // Smallest eigenvector of the normal matrix: shifted inverse iteration on its Cholesky factor, register-resident
+    // and computed redundantly by every lane (no LDS, no barriers). The shift (1e-12 of the trace) keeps the factor
+    // positive definite; 8 iterations contract the other eigen-directions by ((l1 + s) / (l2 + s))^8. Same
+    // eigenvector as the oracle's Jacobi (oracle/ransac.c refit_essential) to rounding; the LDS Jacobi remains the
+    // fallback when the factor breaks down (uniform across the wave: every lane holds identical values).
     double E[9];
-    for (int k = 0; k < 9; ++k) E[k] = jac_v[k * 9 + imin];
-    __syncthreads();  // every lane has read the result before the LDS is reused
+    {
+        auto A = [&](int i, int j) -> double {  // full symmetric entry from the packed upper triangle (static)
+            const int a = i < j ? i : j, b = i < j ? j : i;
+            return acc[a * 9 - a * (a - 1) / 2 + (b - a)];
+        };
+        double tr = 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i) tr += A(i, i);
+        const double shift = 1e-12 * tr;
+        double L[45];  // packed lower triangle, row i at i (i + 1) / 2
+        bool ok = tr > 0.0;
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+#pragma unroll
+            for (int j = 0; j <= i; ++j) {
+                double v = A(i, j) + (i == j ? shift : 0.0);
+#pragma unroll
+                for (int k = 0; k < j; ++k) v -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+                if (i == j) {
+                    ok = ok && v > 0.0;
+                    L[i * (i + 1) / 2 + i] = sqrt(fmax(v, 1e-300));
+                } else {
+                    L[i * (i + 1) / 2 + j] = v / L[j * (j + 1) / 2 + j];
+                }
+            }
+        if (ok) {
+            double x[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) x[i] = 1.0;
+            for (int it = 0; it < 8; ++it) {
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {  // L y = x
+                    double v = x[i];
+#pragma unroll
+                    for (int k = 0; k < i; ++k) v -= L[i * (i + 1) / 2 + k] * x[k];
+                    x[i] = v / L[i * (i + 1) / 2 + i];
+                }
+#pragma unroll
+                for (int i = 8; i >= 0; --i) {  // L^T z = y
+                    double v = x[i];
+#pragma unroll
+                    for (int k = i + 1; k < 9; ++k) v -= L[k * (k + 1) / 2 + i] * x[k];
+                    x[i] = v / L[i * (i + 1) / 2 + i];
+                }
+                double nrm = 0.0;
+#pragma unroll
+                for (int i = 0; i < 9; ++i) nrm += x[i] * x[i];
+                nrm = 1.0 / sqrt(nrm);
+#pragma unroll
+                for (int i = 0; i < 9; ++i) x[i] *= nrm;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) E[k] = x[k];
+        } else {
+            if (lane < 45) {
+                int a = 0, k = lane;
+                while (k >= 9 - a) { k -= 9 - a; ++a; }
+                const int b = a + k;
+                double v = acc[0];
+#pragma unroll
+                for (int q = 1; q < 45; ++q) v = q == lane ? acc[q] : v;
+                jac_a[a * 9 + b] = v;
+                jac_a[b * 9 + a] = v;
+            }
+            __syncthreads();
+            jacobi9_lds(jac_a, jac_v, lane);
+            int imin = 0;
+            double wmin = jac_a[0];
+            for (int i = 1; i < 9; ++i)
+                if (jac_a[i * 9 + i] < wmin) { wmin = jac_a[i * 9 + i]; imin = i; }
+            for (int k = 0; k < 9; ++k) E[k] = jac_v[k * 9 + imin];
+            __syncthreads();  // every lane has read the result before the LDS is reused
+        }
+    }
     double U[9], s[3], Vv[9];
     svd3(E, U, s, Vv);
     double nrm = 0.0;
