@@ -562,7 +562,11 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
         const float expf_scale = -1.f / (2.f * sigma * sigma);
         const float* img = G.g[rf.layer] + (size_t)rf.img * H * W;
         const int side = 2 * radius + 1;
-        for (int k = lane; k < side * side; k += 64) {
+        // Each lane takes a contiguous chunk of the patch, so the 64 concurrent LDS atomics of one instruction land on
+        // bins of 64 different neighbourhoods instead of the same few bins (fixed-point sums: order-independent).
+        const int total = side * side, chunk = (total + 63) / 64;
+        const int kbeg = lane * chunk, kend = min(kbeg + chunk, total);
+        for (int k = kbeg; k < kend; ++k) {
             const int i = k / side - radius, j = k % side - radius;
             const int y = rf.r + i, x = rf.c + j;
             if (y <= 0 || y >= H - 1 || x <= 0 || x >= W - 1) continue;
@@ -756,6 +760,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
     constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
     __shared__ unsigned long long hist[HB];
     __shared__ float dst[128];
+    __shared__ float dnorm;
     const int lane = threadIdx.x;
     for (int slot = blockIdx.x; slot < n_img * max_kpts; slot += gridDim.x) {
         const int img = slot / max_kpts, q = slot % max_kpts;
@@ -781,7 +786,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
         cos_t /= hist_width;
         sin_t /= hist_width;
         const int side = 2 * radius + 1;
-        for (int k = lane; k < side * side; k += 64) {
+        for (int k = lane; k < side * side; k += 64) {  // consecutive lanes: consecutive pixels (coalesced reads)
             const int i = k / side - radius, j = k % side - radius;
             const float c_rot = j * cos_t - i * sin_t;
             const float r_rot = j * sin_t + i * cos_t;
@@ -823,29 +828,38 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             atomicAdd(&hist[idx + (d + 3) * (n + 2) + 1], to_fix(v_rco111));
         }
         __syncthreads();
+        // finalisation: the element-wise steps run one element per lane, the two norms are sequential sums in the
+        // oracle's order (lane 0), so every value is bit-identical
+        for (int e = lane; e < d * d * n; e += 64) {
+            const int cell = e / n, k = e % n;
+            const int idx = ((cell / d + 1) * (d + 2) + (cell % d + 1)) * (n + 2);
+            float v = from_fix(hist[idx + k]);
+            if (k < 2) v += from_fix(hist[idx + n + k]);  // circular wrap of the orientation bins
+            dst[e] = v;
+        }
+        __syncthreads();
         if (lane == 0) {
-            for (int i = 0; i < d; i++)
-                for (int j = 0; j < d; j++) {
-                    const int idx = ((i + 1) * (d + 2) + (j + 1)) * (n + 2);
-                    float h[10];
-                    for (int k = 0; k < n + 2; ++k) h[k] = from_fix(hist[idx + k]);
-                    h[0] += h[n];
-                    h[1] += h[n + 1];
-                    for (int k = 0; k < n; k++) dst[(i * d + j) * n + k] = h[k];
-                }
             float nrm2 = 0;
             for (int k = 0; k < 128; k++) nrm2 += dst[k] * dst[k];
-            const float thr = sqrtf(nrm2) * kDescrMagThr;
-            nrm2 = 0;
-            for (int i = 0; i < 128; i++) {
-                const float val = fminf(dst[i], thr);
-                dst[i] = val;
-                nrm2 += val * val;
-            }
-            nrm2 = kIntDescrFctr / fmaxf(sqrtf(nrm2), FLT_EPSILON);
-            for (int k = 0; k < 128; k++) {
-                const int v = (int)rintf(dst[k] * nrm2);
-                dst[k] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
+            dnorm = sqrtf(nrm2) * kDescrMagThr;
+        }
+        __syncthreads();
+        {
+            const float thr = dnorm;
+            for (int e = lane; e < 128; e += 64) dst[e] = fminf(dst[e], thr);
+        }
+        __syncthreads();
+        if (lane == 0) {
+            float nrm2 = 0;
+            for (int i = 0; i < 128; i++) nrm2 += dst[i] * dst[i];
+            dnorm = kIntDescrFctr / fmaxf(sqrtf(nrm2), FLT_EPSILON);
+        }
+        __syncthreads();
+        {
+            const float scale = dnorm;
+            for (int e = lane; e < 128; e += 64) {
+                const int v = (int)rintf(dst[e] * scale);
+                dst[e] = (float)(v < 0 ? 0 : v > 255 ? 255 : v);
             }
         }
         __syncthreads();
