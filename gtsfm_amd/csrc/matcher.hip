@@ -45,7 +45,15 @@ inline int index_bits(int kmax) {
 
 // ---------------------------------------------------------------------------------------------
 // Pack float descriptors into the two fp16 MFMA operand forms (norm digits folded into K).
+// A form: row-major [img][kpad][da]. B form: fragment-major per 32-row chunk, [img][chunk][s][h][r][8] with
+// k = 16 s + 8 h + e: the 64 16-B granules one MFMA k-step reads (rows r = 0..31 x halves h) are one contiguous
+// KiB, so a linear LDS-DMA copy of the chunk gives conflict-free ds_read_b128 at lane * 16.
 // ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ size_t b_form_index(int img, int row, int k, int kpad, int da) {
+    const size_t chunk = (size_t)img * kpad + (row & ~31);
+    return chunk * da + (size_t)(k >> 4) * 512 + ((k >> 3) & 1) * 256 + (row & 31) * 8 + (k & 7);
+}
+
 __global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __restrict__ counts, int kmax, int dim,
                                  int kpad, int da, _Float16* __restrict__ a_form, _Float16* __restrict__ b_form) {
     const int img = blockIdx.y;
@@ -54,11 +62,10 @@ __global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __re
     const int lane = threadIdx.x;
     const int n = counts[img];
     _Float16* ar = a_form + ((size_t)img * kpad + row) * da;
-    _Float16* br = b_form + ((size_t)img * kpad + row) * da;
     if (row >= n) {  // padding rows: all-zero operands (masked in the epilogue)
         for (int k = lane; k < da; k += 64) {
             ar[k] = (_Float16)0.f;
-            br[k] = (_Float16)0.f;
+            b_form[b_form_index(img, row, k, kpad, da)] = (_Float16)0.f;
         }
         return;
     }
@@ -68,7 +75,7 @@ __global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __re
         float v = src[k];
         sq += v * v;  // integer-valued: exact
         ar[k] = (_Float16)v;
-        br[k] = (_Float16)(-2.f * v);
+        b_form[b_form_index(img, row, k, kpad, da)] = (_Float16)(-2.f * v);
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
@@ -83,7 +90,7 @@ __global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __re
         else if (e == 3) { av = 2048.f; bv = hi; }
         else if (e == 4) { av = 2048.f; bv = 4096.f; }  // + 2^23: accumulator bits = 0x4B000000 | d2
         ar[k] = (_Float16)av;
-        br[k] = (_Float16)bv;
+        b_form[b_form_index(img, row, k, kpad, da)] = (_Float16)bv;
     }
 }
 
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
             // Both 32-column chunks of the super-chunk against both row tiles (acc[sub][t]), so every row sees two
             // new distances per epilogue and takes them with one paired top-2 insert (3 VALU per 2 distances).
             // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows.
-            const unsigned char* bb = bbuf + buf * kSupBytes + lrow * Cfg::kRowBytes + half * 16;
+            const unsigned char* bb = bbuf + buf * kSupBytes + lane * 16;
             f32x16 acc[kSub][2];
 #pragma unroll
             for (int sub = 0; sub < kSub; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
@@ -218,7 +225,7 @@ __global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* _
             for (int s = 0; s < NK; ++s) {
 #pragma unroll
                 for (int sub = 0; sub < kSub; ++sub) {
-                    const half8 bf = *(const half8*)(bb + sub * Cfg::kBufBytes + 32 * s);
+                    const half8 bf = *(const half8*)(bb + sub * Cfg::kBufBytes + 1024 * s);
                     acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc[sub][0], 0, 0, 0);
                     acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc[sub][1], 0, 0, 0);
                 }
