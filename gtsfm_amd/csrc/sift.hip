@@ -134,14 +134,17 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 // ------------------------------------------------------------------ kernels: pyramid
 // Octave-0 base sample: gray conversion (cv::cvtColor fixed point) + 2x INTER_LINEAR upsampling, evaluated on the fly
 // by the first blur (gtsfm/frontend/detector_descriptor/sift.py:44-66 -> cv2 SIFT_create().detectAndCompute).
-// Separable Gaussian (cv::GaussianBlur, BORDER_REFLECT_101: rows then columns) fused in one pass: the input tile
-// and its halo are staged once in LDS, the row pass (4 outputs per thread from ds_read_b128 windows) writes an LDS
-// buffer, the column pass (8 outputs per thread from one register window) writes the level. Every output is the
-// same fmaf chain as the oracle (acc = k0*c; acc = fmaf(kj, l + r, acc)), so the pyramid stays bit-exact.
+// Separable Gaussian (cv::GaussianBlur, BORDER_REFLECT_101: rows then columns) fused in one pass over a 64 x 64
+// output tile: the input tile and its halo are staged once in LDS; the row pass (8 outputs per thread from one
+// ds_read_b128 window, 18 B of LDS reads per output at R = 13) writes its results back in place -- the 8 lanes of a
+// row are lanes of one wave whose window reads all precede their writes, so no barrier is needed -- and the column
+// pass (16 outputs per thread from one register window) writes the level. Every output is the same fmaf chain as
+// the oracle (acc = k0*c; acc = fmaf(kj, l + r, acc)), so the pyramid stays bit-exact.
 // kFromU8: the input is the 2x-upsampled gray image, computed from a gray tile of the u8 source staged in LDS.
 // Tiles are mapped XCD-contiguously (consecutive workgroups land on different XCDs; each XCD gets a contiguous run
 // of tiles so halos are shared through its own L2).
-constexpr int kBlurTX = 64, kBlurTY = 32, kBlurTYT = 4, kBlurColRows = kBlurTY / kBlurTYT;
+constexpr int kBlurTX = 64, kBlurTY = 64, kBlurTYT = 4, kBlurColRows = kBlurTY / kBlurTYT;
+constexpr int kBlurRowOut = 8, kBlurRowThr = kBlurTX / kBlurRowOut;  // row pass: outputs per thread, threads per row
 typedef float pf2 __attribute__((ext_vector_type(2)));
 constexpr int kBlurMaxR = 16;
 
@@ -149,8 +152,7 @@ __host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 3 
 __host__ __device__ constexpr int blur_gh(int r) { return (kBlurTY + 2 * r) / 2 + 4; }
 __host__ __device__ constexpr int blur_gw(int r) { return (kBlurTX + 2 * r) / 2 + 4; }
 __host__ __device__ constexpr size_t blur_lds_bytes(int r, bool u8) {
-    return (size_t)((kBlurTY + 2 * r) * blur_iwp(r) + (kBlurTY + 2 * r) * kBlurTX + (u8 ? blur_gh(r) * blur_gw(r) : 0)) *
-           sizeof(float);
+    return (size_t)((kBlurTY + 2 * r) * blur_iwp(r) + (u8 ? blur_gh(r) * blur_gw(r) : 0)) * sizeof(float);
 }
 
 __device__ __forceinline__ float gray_at(const uint8_t* __restrict__ s, int C, int W, int yy, int xx) {
@@ -178,9 +180,9 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
                                                                   int n_tx, int n_ty, int n_img, Taps t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int IW = kBlurTX + 2 * R, IH = kBlurTY + 2 * R, IWP = blur_iwp(R);
-    constexpr int NV = (4 + 2 * R + 3) / 4;  // float4 words per row-pass window
-    float* in = lds;                          // IH x IWP
-    float* rb = lds + IH * IWP;               // IH x kBlurTX (row-blurred)
+    constexpr int NV = (kBlurRowOut + 2 * R + 3) / 4;  // float4 words per row-pass window
+    static_assert((kBlurRowThr - 1) * kBlurRowOut + 4 * NV <= IWP, "row-pass window past the LDS row");
+    float* in = lds;  // IH x IWP: input tile, then (columns 0..63) the row-blurred tile
     const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * kBlurTX + tx;
     // XCD-contiguous tile order
     const int total = n_tx * n_ty * n_img;
@@ -198,7 +200,7 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
 #pragma unroll
     for (int q = 0; q < (IW + kBlurTX - 1) / kBlurTX; ++q) xx[q] = reflect101(x0 - R + tx + q * kBlurTX, W);
     if constexpr (kFromU8) {
-        float* g = rb + IH * kBlurTX;
+        float* g = in + IH * IWP;
         constexpr int GW = blur_gw(R);
         const int ylo = max(y0 - R, 0), yhi = min(y0 + kBlurTY + R, H) - 1;
         const int xlo = max(x0 - R, 0), xhi = min(x0 + kBlurTX + R, W) - 1;
@@ -266,10 +268,12 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
         }
     }
     __syncthreads();
-    // row pass: 16 threads per row, 4 consecutive outputs each
-    for (int iy = tid >> 4; iy < IH; iy += kBlurTX * kBlurTYT / 16) {
-        const int g4 = (tid & 15) * 4;
-        const float4* wp = (const float4*)(in + iy * IWP + g4);
+    // row pass: kBlurRowThr threads per row (consecutive lanes of one wave), kBlurRowOut consecutive outputs each,
+    // written back in place at columns [g8, g8 + 8) (output column x sits at input column x + R)
+    for (int iy = tid / kBlurRowThr; iy < IH; iy += kBlurTX * kBlurTYT / kBlurRowThr) {
+        const int g8 = (tid % kBlurRowThr) * kBlurRowOut;
+        float* rowp = in + iy * IWP;
+        const float4* wp = (const float4*)(rowp + g8);
         float v[4 * NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
@@ -277,9 +281,9 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
             v[4 * q] = w4.x; v[4 * q + 1] = w4.y; v[4 * q + 2] = w4.z; v[4 * q + 3] = w4.w;
         }
         // two outputs per packed-fp32 op (v_pk_add_f32 / v_pk_fma_f32); per-lane rounding unchanged
-        pf2 o[2];
+        pf2 o[kBlurRowOut / 2];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < kBlurRowOut / 2; ++h) {
             const int q = 2 * h;
             pf2 acc = pf2{k[0], k[0]} * pf2{v[R + q], v[R + q + 1]};
 #pragma unroll
@@ -289,7 +293,9 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
                                                 acc);
             o[h] = acc;
         }
-        *(float4*)(rb + iy * kBlurTX + g4) = make_float4(o[0].x, o[0].y, o[1].x, o[1].y);
+#pragma unroll
+        for (int h = 0; h < kBlurRowOut / 2; h += 2)
+            *(float4*)(rowp + g8 + 2 * h) = make_float4(o[h].x, o[h].y, o[h + 1].x, o[h + 1].y);
     }
     __syncthreads();
     // column pass: kBlurColRows consecutive outputs per thread
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
     const int ly0 = ty * kBlurColRows;
     float c[kBlurColRows + 2 * R];
 #pragma unroll
-    for (int i = 0; i < kBlurColRows + 2 * R; ++i) c[i] = rb[(ly0 + i) * kBlurTX + tx];
+    for (int i = 0; i < kBlurColRows + 2 * R; ++i) c[i] = in[(ly0 + i) * IWP + tx];
 #pragma unroll
     for (int q = 0; q < kBlurColRows; q += 2) {
         pf2 acc = pf2{k[0], k[0]} * pf2{c[R + q], c[R + q + 1]};
@@ -345,98 +351,122 @@ struct GaussSet {
 
 // DoG levels are never stored: DoG_l = G_{l+1} - G_l is recomputed from the Gaussian levels (the same fp32
 // subtraction cv::subtract performs), which removes 5 level writes per octave.
-constexpr int kExTX = 64, kExTY = 16, kExTYT = 4;
-// Candidate list sharded over kCandShards counters/segments: one global atomic per tile on a single counter
-// serialises at ~11 ns each (800k tiles per octave-0 launch); sharding spreads them over independent lines.
+// Extrema scan: each wave sweeps a strip of kExStrip rows down 64 consecutive columns (lanes 1..62 produce outputs,
+// lanes 0 and 63 are the left/right halo), one image row per step. Per row a lane loads the 6 Gaussian levels at its
+// pixel (coalesced 256-B rows, saddr + 32-bit offset), forms the 5 DoG values, gets its horizontal neighbours by
+// wave-wide DPP shifts, and keeps per DoG level the 3-wide row max/min of the last three rows in registers (rolling
+// slots, the loop unrolled by three so no register moves). The 27-neighbourhood test "val >= every neighbour" is
+// val == max over the 3x3x3 block (the centre included), from those max3/min3 partials. Each pixel's levels are read
+// once (plus 2 halo rows per strip and 2 halo lanes per wave): the HBM-bound minimum is 24 B per pixel.
+constexpr int kExWaves = 4, kExOut = 62, kExStrip = 64;
+// Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
+constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
 
-__global__ __launch_bounds__(kExTX* kExTYT) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane l gets lane l-1's value (lane 0: its own)
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane l gets lane l+1's value (lane 63: its own)
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+__global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
                                                                 int* __restrict__ n_cand, int cap) {
-    __shared__ float D[kDogs][kExTY + 2][kExTX + 2];
-    __shared__ Cand list[kExTX * kExTY * kLayers / 4];
+    __shared__ Cand list[kExList];
     __shared__ int n_list, gbase;
-    const int tx = threadIdx.x, ty = threadIdx.y, b = blockIdx.z;
-    const int x0 = blockIdx.x * kExTX, y0 = blockIdx.y * kExTY;
-    const size_t base = (size_t)b * H * W;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, b = blockIdx.z;
+    const int c = (blockIdx.x * kExWaves + wave) * kExOut + lane - 1;  // this lane's column
+    const int y0 = blockIdx.y * kExStrip;
     const int shard = (int)((blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z)) %
                             kCandShards);  // cap is per shard
-    if (tx == 0 && ty == 0) n_list = 0;
-    {
-        constexpr int NR = (kExTY + 2 + kExTYT - 1) / kExTYT, NQ = 2;
-        float v[NR][NQ][kLevels];
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int iy = ty + i * kExTYT, ix = tx + q * kExTX;
-                const int y = min(max(y0 - 1 + iy, 0), H - 1), x = min(max(x0 - 1 + ix, 0), W - 1);
-                const size_t o = base + (size_t)y * W + x;
-                const bool ok = iy < kExTY + 2 && ix < kExTX + 2;
-#pragma unroll
-                for (int l = 0; l < kLevels; ++l) v[i][q][l] = ok ? G.g[l][o] : 0.f;
-            }
-#pragma unroll
-        for (int i = 0; i < NR; ++i)
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int iy = ty + i * kExTYT, ix = tx + q * kExTX;
-                if (iy < kExTY + 2 && ix < kExTX + 2)
-#pragma unroll
-                    for (int l = 0; l < kDogs; ++l) D[l][iy][ix] = v[i][q][l + 1] - v[i][q][l];
-            }
-    }
+    if (threadIdx.x == 0) n_list = 0;
     __syncthreads();
-    // Each thread owns a strip of kExRows rows of one column. The 27-neighbourhood test "val >= every neighbour"
-    // is val == max over the 3x3x3 block (the centre included), computed with shared max3/min3 partials:
-    // per-row 3-wide extrema -> 3x3 box extrema -> across the three DoG levels.
-    constexpr int kExRows = kExTY / kExTYT;
+    const float* gl[kLevels];
+#pragma unroll
+    for (int l = 0; l < kLevels; ++l) gl[l] = G.g[l] + (size_t)b * H * W;
+    const int cx = min(max(c, 0), W - 1);
+    const bool col_ok = lane >= 1 && lane <= kExOut && c >= kBorder && c < W - kBorder;
     const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
-    const int c = x0 + tx;
-    const int ly0 = ty * kExRows;
-    float rmax[kDogs][kExRows + 2], rmin[kDogs][kExRows + 2], ctr[kDogs][kExRows];
+
+    float hmax[kDogs][3], hmin[kDogs][3], ctr[kLayers][3];
+    // Row y (clamped) of the 6 levels -> g; then into slot s: DoG values, their 3-wide row extrema, and the centre
+    // values of layers 1..3.
+    auto fetch = [&](int y, float (&g)[kLevels]) {
+        const uint32_t off = (uint32_t)(min(max(y, 0), H - 1) * W + cx);
 #pragma unroll
-    for (int l = 0; l < kDogs; ++l)
+        for (int l = 0; l < kLevels; ++l) g[l] = gl[l][off];
+    };
+    auto finish = [&](const float (&g)[kLevels], auto slot) {
+        constexpr int s = decltype(slot)::value;
 #pragma unroll
-        for (int i = 0; i < kExRows + 2; ++i) {
-            const float a0 = D[l][ly0 + i][tx], a1 = D[l][ly0 + i][tx + 1], a2 = D[l][ly0 + i][tx + 2];
-            rmax[l][i] = fmaxf(fmaxf(a0, a1), a2);
-            rmin[l][i] = fminf(fminf(a0, a1), a2);
-            if (i >= 1 && i <= kExRows) ctr[l][i - 1] = a1;
+        for (int l = 0; l < kDogs; ++l) {
+            const float d = g[l + 1] - g[l];
+            const float lf = dpp_from_left(d), rt = dpp_from_right(d);
+            hmax[l][s] = fmaxf(fmaxf(lf, d), rt);
+            hmin[l][s] = fminf(fminf(lf, d), rt);
+            if (l >= 1 && l <= kLayers) ctr[l - 1][s] = d;
         }
-    const bool col_ok = c >= kBorder && c < W - kBorder;
-#pragma unroll
-    for (int q = 0; q < kExRows; ++q) {
-        const int r = y0 + ly0 + q;
-        if (!col_ok || r < kBorder || r >= H - kBorder) continue;
+    };
+    // Test row y: the three slots hold DoG rows y-1, y, y+1, row y in `slot`.
+    auto test_row = [&](int y, auto slot) {
+        constexpr int s = decltype(slot)::value;
+        if (!col_ok || y < kBorder || y >= H - kBorder) return;
         float bmax[kDogs], bmin[kDogs];
 #pragma unroll
         for (int l = 0; l < kDogs; ++l) {
-            bmax[l] = fmaxf(fmaxf(rmax[l][q], rmax[l][q + 1]), rmax[l][q + 2]);
-            bmin[l] = fminf(fminf(rmin[l][q], rmin[l][q + 1]), rmin[l][q + 2]);
+            bmax[l] = fmaxf(fmaxf(hmax[l][0], hmax[l][1]), hmax[l][2]);
+            bmin[l] = fminf(fminf(hmin[l][0], hmin[l][1]), hmin[l][2]);
         }
 #pragma unroll
         for (int layer = 1; layer <= kLayers; ++layer) {
-            const float val = ctr[layer][q];
+            const float val = ctr[layer - 1][s];
             if (!(fabsf(val) > threshold)) continue;
             const float mx = fmaxf(fmaxf(bmax[layer - 1], bmax[layer]), bmax[layer + 1]);
             const float mn = fminf(fminf(bmin[layer - 1], bmin[layer]), bmin[layer + 1]);
             const bool ismax = val > 0 && val >= mx, ismin = val < 0 && val <= mn;
             if (!ismax && !ismin) continue;
-            const int slot = atomicAdd(&n_list, 1);
-            if (slot < (int)(sizeof(list) / sizeof(Cand))) {
-                list[slot] = Cand{b, layer, r, c};
-            } else {  // plateau-heavy tile: spill straight to the global list
-                const int g = atomicAdd(&n_cand[shard], 1);
-                if (g < cap) cands[(size_t)shard * cap + g] = Cand{b, layer, r, c};
+            const int slot_i = atomicAdd(&n_list, 1);
+            if (slot_i < kExList) {
+                list[slot_i] = Cand{b, layer, y, c};
+            } else {  // plateau-heavy block: spill straight to the global list
+                const int gi = atomicAdd(&n_cand[shard], 1);
+                if (gi < cap) cands[(size_t)shard * cap + gi] = Cand{b, layer, y, c};
             }
         }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    using S2 = std::integral_constant<int, 2>;
+    // rows y0-1 (slot 0) and y0 (slot 1) first; then row y0+1+3k+j goes to slot (2+j)%3 and completes the window of
+    // row y0+3k+j, whose centre sits in slot (1+j)%3.
+    // The three rows of an iteration are fetched up front (18 loads in flight per wave).
+    {
+        float ga[kLevels], gb[kLevels];
+        fetch(y0 - 1, ga);
+        fetch(y0, gb);
+        finish(ga, S0{});
+        finish(gb, S1{});
+    }
+    const int y_end = min(y0 + kExStrip, H);
+    for (int y = y0; y < y_end; y += 3) {
+        float g1[kLevels], g2[kLevels], g3[kLevels];
+        fetch(y + 1, g1);
+        fetch(y + 2, g2);
+        fetch(y + 3, g3);
+        finish(g1, S2{});
+        test_row(y, S1{});
+        if (y + 1 >= y_end) break;
+        finish(g2, S0{});
+        test_row(y + 1, S2{});
+        if (y + 2 >= y_end) break;
+        finish(g3, S1{});
+        test_row(y + 2, S0{});
     }
     __syncthreads();
-    const int n = min(n_list, (int)(sizeof(list) / sizeof(Cand)));
-    const int t = ty * kExTX + tx;
-    if (t == 0) gbase = n ? atomicAdd(&n_cand[shard], n) : 0;
+    const int n = min(n_list, kExList);
+    if (threadIdx.x == 0) gbase = n ? atomicAdd(&n_cand[shard], n) : 0;
     __syncthreads();
-    for (int i = t; i < n; i += kExTX * kExTYT)
+    for (int i = threadIdx.x; i < n; i += 64 * kExWaves)
         if (gbase + i < cap) cands[(size_t)shard * cap + gbase + i] = list[i];
 }
 
@@ -1034,8 +1064,9 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
         GaussSet G;
         for (int i = 0; i < kLevels; ++i) G.g[i] = F(L.g[o][i]);
         const int shard_cap = (int)((size_t)B * kCandCapPerImg / kCandShards);
-        hipLaunchKernelGGL(extrema_kernel, dim3((w + kExTX - 1) / kExTX, (h + kExTY - 1) / kExTY, B),
-                           dim3(kExTX, kExTYT), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap);
+        hipLaunchKernelGGL(extrema_kernel, dim3((w + kExWaves * kExOut - 1) / (kExWaves * kExOut),
+                                                (h + kExStrip - 1) / kExStrip, B),
+                           dim3(64 * kExWaves), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap);
         hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
                            shard_cap, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg);
