@@ -135,10 +135,10 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 // Octave-0 base sample: gray conversion (cv::cvtColor fixed point) + 2x INTER_LINEAR upsampling, evaluated on the fly
 // by the first blur (gtsfm/frontend/detector_descriptor/sift.py:44-66 -> cv2 SIFT_create().detectAndCompute).
 // Separable Gaussian (cv::GaussianBlur, BORDER_REFLECT_101: rows then columns) fused in one pass over a 64 x 64
-// output tile: the input tile and its halo are staged once in LDS; the row pass (8 outputs per thread from one
-// ds_read_b128 window, 18 B of LDS reads per output at R = 13) writes its results back in place -- the 8 lanes of a
-// row are lanes of one wave whose window reads all precede their writes, so no barrier is needed -- and the column
-// pass (16 outputs per thread from one register window) writes the level. Every output is the same fmaf chain as
+// output tile: the input tile and its halo are staged once in LDS (interior tiles by LDS-DMA); the row pass (8 outputs
+// per thread from one conflict-free ds_read_b64 window, 17 B of LDS reads per output at R = 13) writes its results
+// back in place -- the 8 lanes of a row are lanes of one wave whose window reads are all issued before any of its
+// writes (LDS executes a wave's operations in order), so no barrier is needed -- and the column pass (16 outputs per thread from one register window) writes the level. Every output is the same fmaf chain as
 // the oracle (acc = k0*c; acc = fmaf(kj, l + r, acc)), so the pyramid stays bit-exact.
 // kFromU8: the input is the 2x-upsampled gray image, computed from a gray tile of the u8 source staged in LDS.
 // Tiles are mapped XCD-contiguously (consecutive workgroups land on different XCDs; each XCD gets a contiguous run
@@ -148,7 +148,9 @@ constexpr int kBlurRowOut = 8, kBlurRowThr = kBlurTX / kBlurRowOut;  // row pass
 typedef float pf2 __attribute__((ext_vector_type(2)));
 constexpr int kBlurMaxR = 16;
 
-__host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 3 + 3) / 4 * 4; }
+// LDS row stride of the input tile: >= 64 + 2r and = 2 (mod 8), so the row pass's ds_read_b64 windows (8 lanes per
+// row at 32-B steps, four rows per 32-lane group) hit 64 distinct banks
+__host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 5) / 8 * 8 + 2; }
 __host__ __device__ constexpr int blur_gh(int r) { return (kBlurTY + 2 * r) / 2 + 4; }
 __host__ __device__ constexpr int blur_gw(int r) { return (kBlurTX + 2 * r) / 2 + 4; }
 __host__ __device__ constexpr size_t blur_lds_bytes(int r, bool u8) {
@@ -180,8 +182,8 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
                                                                   int n_tx, int n_ty, int n_img, Taps t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int IW = kBlurTX + 2 * R, IH = kBlurTY + 2 * R, IWP = blur_iwp(R);
-    constexpr int NV = (kBlurRowOut + 2 * R + 3) / 4;  // float4 words per row-pass window
-    static_assert((kBlurRowThr - 1) * kBlurRowOut + 4 * NV <= IWP, "row-pass window past the LDS row");
+    constexpr int NV = (kBlurRowOut + 2 * R) / 2;  // float2 words per row-pass window
+    static_assert((kBlurRowThr - 1) * kBlurRowOut + 2 * NV <= IWP, "row-pass window past the LDS row");
     float* in = lds;  // IH x IWP: input tile, then (columns 0..63) the row-blurred tile
     const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * kBlurTX + tx;
     // XCD-contiguous tile order
@@ -248,8 +250,21 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
                 }
             }
         }
+    } else if (x0 - R >= 0 && x0 + kBlurTX + R <= W && y0 - R >= 0 && y0 + kBlurTY + R <= H) {
+        // interior tile: rows straight from HBM into LDS (global_load_lds, no VGPR round trip, no ds_write)
+        const float* srow0 = src + base + (size_t)(y0 - R) * W + (x0 - R) + tx;
+        for (int iy = ty; iy < IH; iy += kBlurTYT) {
+            const float* g = srow0 + (size_t)iy * W;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                             (__attribute__((address_space(3))) void*)(in + iy * IWP), 4, 0, 0);
+            if (tx < IW - kBlurTX)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g + kBlurTX),
+                                                 (__attribute__((address_space(3))) void*)(in + iy * IWP + kBlurTX),
+                                                 4, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-        // every load of the tile issued before any LDS store (memory-level parallelism)
+        // border tile (reflected halo): every load of the tile issued before any LDS store
         constexpr int NR = (IH + kBlurTYT - 1) / kBlurTYT, NQ = (IW + kBlurTX - 1) / kBlurTX;
         float v[NR][NQ];
 #pragma unroll
@@ -273,13 +288,14 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
     for (int iy = tid / kBlurRowThr; iy < IH; iy += kBlurTX * kBlurTYT / kBlurRowThr) {
         const int g8 = (tid % kBlurRowThr) * kBlurRowOut;
         float* rowp = in + iy * IWP;
-        const float4* wp = (const float4*)(rowp + g8);
-        float v[4 * NV];
+        const float2* wp = (const float2*)(rowp + g8);
+        float v[2 * NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
-            const float4 w4 = wp[q];
-            v[4 * q] = w4.x; v[4 * q + 1] = w4.y; v[4 * q + 2] = w4.z; v[4 * q + 3] = w4.w;
+            const float2 w2 = wp[q];
+            v[2 * q] = w2.x; v[2 * q + 1] = w2.y;
         }
+        asm volatile("" ::: "memory");  // all window reads issue before the in-place writes (neighbour lanes' windows)
         // two outputs per packed-fp32 op (v_pk_add_f32 / v_pk_fma_f32); per-lane rounding unchanged
         pf2 o[kBlurRowOut / 2];
 #pragma unroll
@@ -294,8 +310,7 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
             o[h] = acc;
         }
 #pragma unroll
-        for (int h = 0; h < kBlurRowOut / 2; h += 2)
-            *(float4*)(rowp + g8 + 2 * h) = make_float4(o[h].x, o[h].y, o[h + 1].x, o[h + 1].y);
+        for (int h = 0; h < kBlurRowOut / 2; ++h) *(float2*)(rowp + g8 + 2 * h) = make_float2(o[h].x, o[h].y);
     }
     __syncthreads();
     // column pass: kBlurColRows consecutive outputs per thread
