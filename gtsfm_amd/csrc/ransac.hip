@@ -78,18 +78,19 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 // The solver's dynamically indexed arrays live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit
 // consecutive words, so every access is bank-conflict free, and nothing spills to scratch. The solver runs in two
 // kernels so each one's workgroup holds only its own phase's arrays:
-//   stage 1 (sample, 5x9 nullspace, 10x20 Gauss-Jordan): Q (45) | A (200) doubles + column permutation (9 ints)
-//       = 101 KB per 64-lane workgroup (one per CU);
+//   stage 1 (sample, 5x9 nullspace, 10x20 Gauss-Jordan), two lanes per hypothesis: Q (45) + column permutation
+//       (9 ints) | this lane's half of A (10 x 10) = 51 KB per 64-lane workgroup (three per CU);
 //   stage 2 (det B(z), Sturm chain, isolation, bisection, E): a rolling window of three Sturm rows (3 x 11) + prem
 //       scratch (11) | isolation stack (2 x 24) + intervals (2 x 10) doubles, stack counts and chain degrees as
 //       bytes = 38 KB per workgroup (four per CU). Finished chain rows go straight to the register chain R.
 constexpr int kLanes = 64;
-constexpr int kUnion = 200;   // stage-1 doubles per lane: Q (45) | A (200)
-constexpr int kInts = 9;      // stage-1 ints per lane: column permutation
+constexpr int kUnion = 100;   // stage-1 doubles per lane: Q (45) + V (9) + permutation ints (at slot 64) | half of A
+constexpr int kPermSlot = 64; // double slot where the nullspace's column permutation (9 ints) starts
 constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
 constexpr int kRootDbl = 68;  // stage-2 doubles per lane: 3 Sturm rows (33) + t (11) | stack (48) + intervals (20)
 constexpr int kRootB = 64;    // stage-2 bytes per lane: stack va/vb (2 x 24) + chain degrees (11), padded
-constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double) + (size_t)kInts * kLanes * sizeof(int);
+constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double);
+static_assert(kPermSlot >= 54 && kPermSlot * 8 + 9 * 4 <= kUnion * 8, "permutation ints overlap Q/V or overflow");
 constexpr size_t kRootLds = (size_t)kRootDbl * kLanes * sizeof(double) + (size_t)kRootB * kLanes;
 
 template <typename T>
@@ -123,12 +124,12 @@ __device__ int prem(LaneArr<double> a, int da, LaneArr<double> b, int db, LaneAr
 
 struct SolverMem {
     LaneArr<double> u;  // kUnion doubles
-    LaneArr<int> iv;    // kInts ints
+    LaneArr<int> iv;    // 9 ints inside u, past Q and V (nullspace only)
 };
 
 __device__ __forceinline__ SolverMem solver_mem(unsigned char* smem, int lane) {
     double* d = (double*)smem;
-    int* iv = (int*)(smem + (size_t)kUnion * kLanes * sizeof(double));
+    int* iv = (int*)(smem + (size_t)kPermSlot * kLanes * sizeof(double));
     return SolverMem{LaneArr<double>{d + lane}, LaneArr<int>{iv + lane}};
 }
 
@@ -378,11 +379,23 @@ __device__ __forceinline__ void addmul_ql_lds(const double* q, const double* l, 
         for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += s * (q[i] * l[j]);
 }
 
+// Lanes 2k and 2k+1 solve one hypothesis together; the even lane holds columns 0..9 of the 10 x 20 matrix, the odd
+// lane columns 10..19. Every pivot, pivot value and elimination factor comes from a column < 10, i.e. from the even
+// lane, and reaches the odd one by a DPP quad permutation (no LDS, no waitcnt).
+__device__ __forceinline__ int pair_lo(int v) { return __builtin_amdgcn_mov_dpp(v, 0xA0, 0xf, 0xf, false); }
+__device__ __forceinline__ double pair_lo(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = pair_lo((int)(b & 0xffffffffll)), hi = pair_lo((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // Nister 5-point, stage 1: 5 correspondences -> nullspace basis N (4 x 9) and rows 4..9, columns 10..19 of the
-// Gauss-Jordan-reduced 10 x 20 constraint matrix (all that stage 2 reads). False for a degenerate sample.
+// Gauss-Jordan-reduced 10 x 20 constraint matrix (all that stage 2 reads; valid in the odd lane of the pair). The
+// arithmetic per element is the single-lane elimination's, so the result is bit-identical to it. False for a
+// degenerate sample (uniform over the pair).
 constexpr int kStageVals = 6 * 10 + 4 * 9;  // doubles handed from stage 1 to stage 2 per hypothesis
 
-__device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem m, double N[4][9],
+__device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem m, int part, double N[4][9],
                                   double Rt[6][10]) {
     if (!nullspace_5x9(x1, x2, m, N)) return false;
     double E[9][4];
@@ -393,7 +406,11 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         E[e][2] = N[2][e];
         E[e][3] = N[3][e];
     }
-    LaneArr<double> A = m.u;  // [10][20]; each row is accumulated in registers, then stored once
+    LaneArr<double> A = m.u;  // [10][10]: this lane's half; each row is accumulated in registers, then stored once
+    auto store_row = [&](int r, const double(&row)[20]) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) A[10 * r + k] = part ? row[10 + k] : row[k];
+    };
     {
         double row[20], q[10];
 #pragma unroll
@@ -404,8 +421,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         mul_ll(E[5], E[6], q); addmul_ql(q, E[1], 1.0, row);
         mul_ll(E[3], E[7], q); addmul_ql(q, E[2], 1.0, row);
         mul_ll(E[4], E[6], q); addmul_ql(q, E[2], -1.0, row);
-#pragma unroll
-        for (int k = 0; k < 20; ++k) A[k] = row[k];
+        store_row(0, row);
     }
     double EEt[3][3][10], tr[10], tmp[10];
 #pragma unroll
@@ -436,51 +452,51 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
 #pragma unroll
             for (int k = 0; k < 3; ++k) addmul_ql(EEt[i][k], E[3 * k + j], 2.0, row);
             addmul_ql(tr, E[3 * i + j], -1.0, row);
-            const int r0 = 20 * (1 + 3 * i + j);
-#pragma unroll
-            for (int k = 0; k < 20; ++k) A[r0 + k] = row[k];
+            store_row(1 + 3 * i + j, row);
         }
-    // Gauss-Jordan with partial pivoting; every row is moved through registers whole (loads issued together)
+    // Gauss-Jordan with partial pivoting on the lane's half rows; every row is moved through registers whole
 #pragma unroll
     for (int c = 0; c < 10; ++c) {
         int pr = c;
-        double best = fabs(A[20 * c + c]);
+        double best = fabs(A[10 * c + c]);  // meaningful in the even lane (column c)
         for (int r = c + 1; r < 10; ++r) {
-            const double v = fabs(A[20 * r + c]);
+            const double v = fabs(A[10 * r + c]);
             if (v > best) { best = v; pr = r; }
         }
+        pr = pair_lo(pr);
+        best = pair_lo(best);
         if (best < 1e-14) return false;
-        double prow[20];
+        double prow[10];
 #pragma unroll
-        for (int j = 0; j < 20; ++j) prow[j] = A[20 * pr + j];
+        for (int j = 0; j < 10; ++j) prow[j] = A[10 * pr + j];
         if (pr != c) {
-            double crow[20];
+            double crow[10];
 #pragma unroll
-            for (int j = 0; j < 20; ++j) crow[j] = A[20 * c + j];
+            for (int j = 0; j < 10; ++j) crow[j] = A[10 * c + j];
 #pragma unroll
-            for (int j = 0; j < 20; ++j) A[20 * pr + j] = crow[j];
+            for (int j = 0; j < 10; ++j) A[10 * pr + j] = crow[j];
         }
-        const double inv = 1.0 / prow[c];
+        const double inv = 1.0 / pair_lo(prow[c]);
 #pragma unroll
-        for (int j = 0; j < 20; ++j) prow[j] *= inv;
+        for (int j = 0; j < 10; ++j) prow[j] *= inv;
 #pragma unroll
-        for (int j = 0; j < 20; ++j) A[20 * c + j] = prow[j];
+        for (int j = 0; j < 10; ++j) A[10 * c + j] = prow[j];
         for (int r = 0; r < 10; ++r) {
             if (r == c) continue;
-            double row[20];
+            double row[10];
 #pragma unroll
-            for (int j = 0; j < 20; ++j) row[j] = A[20 * r + j];
-            const double f = row[c];
+            for (int j = 0; j < 10; ++j) row[j] = A[10 * r + j];
+            const double f = pair_lo(row[c]);
 #pragma unroll
-            for (int j = 0; j < 20; ++j) row[j] -= f * prow[j];
+            for (int j = 0; j < 10; ++j) row[j] -= f * prow[j];
 #pragma unroll
-            for (int j = 0; j < 20; ++j) A[20 * r + j] = row[j];
+            for (int j = 0; j < 10; ++j) A[10 * r + j] = row[j];
         }
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int j = 0; j < 10; ++j) Rt[r][j] = A[20 * (4 + r) + 10 + j];
+        for (int j = 0; j < 10; ++j) Rt[r][j] = A[10 * (4 + r) + j];
     return true;
 }
 
@@ -965,9 +981,10 @@ __global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int 
     st[p] = s;
 }
 
-// Stage 1, one 64-lane workgroup per active pair: lane l samples hypothesis done + l, runs the nullspace and the
-// 10 x 20 elimination, and hands N + the reduced rows to stage 2 through `stage` ([P][kStageVals][64], lane-minor so
-// the stores coalesce). nsol = 1 marks a non-degenerate sample for stage 2, 0 a finished one.
+// Stage 1, two 64-lane workgroups per active pair (blockIdx.y = half of the batch): lanes 2k, 2k+1 sample hypothesis
+// h = done + 32 blockIdx.y + k, both run the nullspace, and split the 10 x 20 elimination by column halves; N (even
+// lane) + the reduced rows (odd lane) go to stage 2 through `stage` ([P][kStageVals][64], hypothesis-minor).
+// nsol = 1 marks a non-degenerate sample for stage 2, 0 a finished one.
 __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restrict__ match_count, int mcap,
                                                               const double2* __restrict__ x1n_all,
                                                               const double2* __restrict__ x2n_all, uint64_t seed,
@@ -976,6 +993,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
                                                               double* __restrict__ stage, int* __restrict__ nsol) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int p = blockIdx.x, lane = threadIdx.x;
+    const int part = lane & 1, hyp = blockIdx.y * (kLanes / 2) + (lane >> 1);
     const int M = match_count[p];
     if (M < 6) return;
     const int done = st[p].done;
@@ -985,7 +1003,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
     const SolverMem mem = solver_mem(smem, lane);
     int ok = 0;
     int idx[5];
-    if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + lane, M, idx)) {
+    if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + hyp, M, idx)) {
         double s1[10], s2[10];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -994,20 +1012,23 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
             s2[2 * k] = b.x; s2[2 * k + 1] = b.y;
         }
         double N[4][9], Rt[6][10];
-        if (five_point_stage1(s1, s2, mem, N, Rt)) {
+        if (five_point_stage1(s1, s2, mem, part, N, Rt)) {
             ok = 1;
-            double* out = stage + (size_t)p * kStageVals * kLanes + lane;
+            double* out = stage + (size_t)p * kStageVals * kBatch + hyp;
+            if (part) {
 #pragma unroll
-            for (int r = 0; r < 6; ++r)
+                for (int r = 0; r < 6; ++r)
 #pragma unroll
-                for (int j = 0; j < 10; ++j) out[(10 * r + j) * kLanes] = Rt[r][j];
+                    for (int j = 0; j < 10; ++j) out[(10 * r + j) * kBatch] = Rt[r][j];
+            } else {
 #pragma unroll
-            for (int k = 0; k < 4; ++k)
+                for (int k = 0; k < 4; ++k)
 #pragma unroll
-                for (int j = 0; j < 9; ++j) out[(60 + 9 * k + j) * kLanes] = N[k][j];
+                    for (int j = 0; j < 9; ++j) out[(60 + 9 * k + j) * kBatch] = N[k][j];
+            }
         }
     }
-    nsol[(size_t)p * kBatch + lane] = ok;
+    if (!part) nsol[(size_t)p * kBatch + hyp] = ok;
 }
 
 // Stage 2, one 64-lane workgroup per active pair (three per CU): lane l turns stage 1's output into the candidate
@@ -1336,7 +1357,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     }
     const int n_batches = (max_iters + kBatch - 1) / kBatch;
     for (int b = 0; b < n_batches; ++b) {
-        hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
+        hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs, kBatch / (kLanes / 2)), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
                            x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs), dim3(64), kRootLds, stream, d_match_count, st, stage,
                            cand, nsol);
