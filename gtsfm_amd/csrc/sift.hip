@@ -85,23 +85,27 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
     const float p1 = 0.9997878412794807f * 57.29577951308232f, p3 = -0.3258083974640975f * 57.29577951308232f,
                 p5 = 0.1555786518463281f * 57.29577951308232f, p7 = -0.04432655554792128f * 57.29577951308232f;
     const float ax = fabsf(x), ay = fabsf(y);
-    float a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + (float)DBL_EPSILON);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + (float)DBL_EPSILON);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
+    // both octants in one evaluation (one division): c = min / (max + eps), a = poly(c) or 90 - poly(c)
+    const bool xmaj = ax >= ay;
+    const float c = (xmaj ? ay : ax) / ((xmaj ? ax : ay) + (float)DBL_EPSILON);
+    const float c2 = c * c;
+    const float t = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    float a = xmaj ? t : 90.f - t;
     if (x < 0) a = 180.f - a;
     if (y < 0) a = 360.f - a;
     return a;
 }
 
-__device__ __forceinline__ unsigned long long to_fix(float v) { return (unsigned long long)(long long)(v * kFixScale); }
 __device__ __forceinline__ float from_fix(unsigned long long v) { return (float)(long long)v * (1.0f / kFixScale); }
+// Fixed-point histogram value (long long)(v 2^24) as in oracle/sift.c, for v >= 0 (every contribution is a magnitude
+// times non-negative weights), without the signed 64-bit conversion sequence: x = v 2^24 splits exactly into hi = floor(x / 2^32) and lo = x - hi 2^32 (a multiple of ulp(x)
+// below 2^32), both truncated by v_cvt_u32_f32 -- the same integer as (long long)x.
+__device__ __forceinline__ unsigned long long to_fix_nn(float v) {
+    const float x = v * kFixScale;
+    const uint32_t hi = (uint32_t)(x * 2.3283064365386963e-10f);
+    const uint32_t lo = (uint32_t)__builtin_fmaf(-(float)hi, 4294967296.0f, x);
+    return ((unsigned long long)hi << 32) | lo;
+}
 
 __device__ __forceinline__ int reflect101(int i, int n) {
     if (n == 1) return 0;
@@ -623,7 +627,7 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
             int bin = (int)rintf((kOriBins / 360.f) * ori);
             if (bin >= kOriBins) bin -= kOriBins;
             if (bin < 0) bin += kOriBins;
-            atomicAdd(&hist[bin], to_fix(w * mag));
+            atomicAdd(&hist[bin], to_fix_nn(w * mag));
         }
         __syncthreads();
         if (lane == 0) {
@@ -797,13 +801,19 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __rest
 }
 
 // ------------------------------------------------------------------ descriptors: one wave per kept keypoint
+constexpr int kDescChunk = 512;
+
 __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict__ kps, int kp_cap,
                                                         const int* __restrict__ sel, const int* __restrict__ n_sel,
                                                         int n_img, int max_kpts, LevelTable L,
                                                         float* __restrict__ out_xy, float* __restrict__ out_attr,
                                                         float* __restrict__ out_desc) {
     constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
-    __shared__ unsigned long long hist[HB];
+    // kCopies private histograms (lane & 1 picks one): adjacent samples usually land in the same bins, and same-address
+    // LDS atomics of one instruction serialise. Integer (fixed-point) sums, so merging the copies is exact.
+    constexpr int kCopies = 2, HBP = HB + 1;  // +1: copies start on different banks
+    __shared__ unsigned long long hist[kCopies * HBP];
+    __shared__ int slist[kDescChunk];  // valid samples of the current chunk, (i << 16) | (j & 0xffff)
     __shared__ float dst[128];
     __shared__ float dnorm;
     const int lane = threadIdx.x;
@@ -811,7 +821,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
         const int img = slot / max_kpts, q = slot % max_kpts;
         if (q >= n_sel[img]) continue;  // uniform per block
         const KeyRec kp = kps[(size_t)img * kp_cap + sel[(size_t)img * max_kpts + q]];
-        for (int i = lane; i < HB; i += 64) hist[i] = 0ull;
+        for (int i = lane; i < kCopies * HBP; i += 64) hist[i] = 0ull;
         __syncthreads();
         const int H = L.H[kp.o], W = L.W[kp.o];
         const float* img_p = L.g[kp.o][kp.layer - 1] + (size_t)img * L.img_stride[kp.o];
@@ -831,15 +841,43 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
         cos_t /= hist_width;
         sin_t /= hist_width;
         const int side = 2 * radius + 1;
-        for (int k = lane; k < side * side; k += 64) {  // consecutive lanes: consecutive pixels (coalesced reads)
-            const int i = k / side - radius, j = k % side - radius;
+        unsigned long long* hc = hist + (lane & (kCopies - 1)) * HBP;
+        const int di = 64 / side, dj = 64 % side;
+        int ii = lane / side, jj = lane % side;  // (row, column) of sample k, advanced incrementally
+        const int ss = side * side;
+        // Half of the side x side square lies outside the rotated descriptor window: each chunk of kDescChunk samples
+        // is first tested (consecutive lanes: consecutive pixels), the valid ones are compacted into slist by a wave
+        // ballot, and only those run the gradient / weight / histogram work with every lane busy.
+        for (int base = 0; base < ss; base += kDescChunk) {
+            int nv = 0;
+            for (int cc = 0; cc < kDescChunk; cc += 64) {
+                const int i = ii - radius, j = jj - radius;
+                ii += di;
+                jj += dj;
+                if (jj >= side) {
+                    jj -= side;
+                    ++ii;
+                }
+                const float c_rot = j * cos_t - i * sin_t;
+                const float r_rot = j * sin_t + i * cos_t;
+                const float rbin = r_rot + d / 2 - 0.5f;
+                const float cbin = c_rot + d / 2 - 0.5f;
+                const int r = py + i, c = px + j;
+                const bool ok = base + cc + lane < ss && rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 &&
+                                r < H - 1 && c > 0 && c < W - 1;
+                const unsigned long long m = __ballot(ok);
+                if (ok) slist[nv + __popcll(m & ((1ull << lane) - 1))] = (i << 16) | (j & 0xffff);
+                nv += __popcll(m);
+            }
+            __syncthreads();
+            for (int t = lane; t < nv; t += 64) {
+            const int sv = slist[t];
+            const int i = sv >> 16, j = (short)(sv & 0xffff);
             const float c_rot = j * cos_t - i * sin_t;
             const float r_rot = j * sin_t + i * cos_t;
             float rbin = r_rot + d / 2 - 0.5f;
             float cbin = c_rot + d / 2 - 0.5f;
             const int r = py + i, c = px + j;
-            if (!(rbin > -1 && rbin < d && cbin > -1 && cbin < d && r > 0 && r < H - 1 && c > 0 && c < W - 1))
-                continue;
             const float dx = img_p[(size_t)r * W + c + 1] - img_p[(size_t)r * W + c - 1];
             const float dy = img_p[(size_t)(r - 1) * W + c] - img_p[(size_t)(r + 1) * W + c];
             const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
@@ -863,23 +901,30 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             const float v_rco011 = v_rc01 * obin, v_rco010 = v_rc01 - v_rco011;
             const float v_rco001 = v_rc00 * obin, v_rco000 = v_rc00 - v_rco001;
             const int idx = ((r0 + 1) * (d + 2) + c0 + 1) * (n + 2) + o0;
-            atomicAdd(&hist[idx], to_fix(v_rco000));
-            atomicAdd(&hist[idx + 1], to_fix(v_rco001));
-            atomicAdd(&hist[idx + (n + 2)], to_fix(v_rco010));
-            atomicAdd(&hist[idx + (n + 3)], to_fix(v_rco011));
-            atomicAdd(&hist[idx + (d + 2) * (n + 2)], to_fix(v_rco100));
-            atomicAdd(&hist[idx + (d + 2) * (n + 2) + 1], to_fix(v_rco101));
-            atomicAdd(&hist[idx + (d + 3) * (n + 2)], to_fix(v_rco110));
-            atomicAdd(&hist[idx + (d + 3) * (n + 2) + 1], to_fix(v_rco111));
+            atomicAdd(&hc[idx], to_fix_nn(v_rco000));
+            atomicAdd(&hc[idx + 1], to_fix_nn(v_rco001));
+            atomicAdd(&hc[idx + (n + 2)], to_fix_nn(v_rco010));
+            atomicAdd(&hc[idx + (n + 3)], to_fix_nn(v_rco011));
+            atomicAdd(&hc[idx + (d + 2) * (n + 2)], to_fix_nn(v_rco100));
+            atomicAdd(&hc[idx + (d + 2) * (n + 2) + 1], to_fix_nn(v_rco101));
+            atomicAdd(&hc[idx + (d + 3) * (n + 2)], to_fix_nn(v_rco110));
+            atomicAdd(&hc[idx + (d + 3) * (n + 2) + 1], to_fix_nn(v_rco111));
+            }
+            __syncthreads();  // slist is rewritten by the next chunk
         }
-        __syncthreads();
         // finalisation: the element-wise steps run one element per lane, the two norms are sequential sums in the
         // oracle's order (lane 0), so every value is bit-identical
         for (int e = lane; e < d * d * n; e += 64) {
             const int cell = e / n, k = e % n;
             const int idx = ((cell / d + 1) * (d + 2) + (cell % d + 1)) * (n + 2);
-            float v = from_fix(hist[idx + k]);
-            if (k < 2) v += from_fix(hist[idx + n + k]);  // circular wrap of the orientation bins
+            unsigned long long a = 0, w = 0;
+#pragma unroll
+            for (int c = 0; c < kCopies; ++c) {
+                a += hist[c * HBP + idx + k];
+                w += hist[c * HBP + idx + n + (k & 1)];
+            }
+            float v = from_fix(a);
+            if (k < 2) v += from_fix(w);  // circular wrap of the orientation bins
             dst[e] = v;
         }
         __syncthreads();
