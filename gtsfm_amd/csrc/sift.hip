@@ -157,8 +157,12 @@ constexpr int kBlurMaxR = 16;
 __host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 5) / 8 * 8 + 2; }
 __host__ __device__ constexpr int blur_gh(int r) { return (kBlurTY + 2 * r) / 2 + 4; }
 __host__ __device__ constexpr int blur_gw(int r) { return (kBlurTX + 2 * r) / 2 + 4; }
+// u8 variant: input tile | per-row upsampling table (float4 per tile row) | gray source tile
+__host__ __device__ constexpr int blur_rtab_off(int r) { return ((kBlurTY + 2 * r) * blur_iwp(r) + 3) / 4 * 4; }
 __host__ __device__ constexpr size_t blur_lds_bytes(int r, bool u8) {
-    return (size_t)((kBlurTY + 2 * r) * blur_iwp(r) + (u8 ? blur_gh(r) * blur_gw(r) : 0)) * sizeof(float);
+    return (size_t)(u8 ? blur_rtab_off(r) + 4 * (kBlurTY + 2 * r) + blur_gh(r) * blur_gw(r)
+                       : (kBlurTY + 2 * r) * blur_iwp(r)) *
+           sizeof(float);
 }
 
 __device__ __forceinline__ float gray_at(const uint8_t* __restrict__ s, int C, int W, int yy, int xx) {
@@ -206,7 +210,8 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
 #pragma unroll
     for (int q = 0; q < (IW + kBlurTX - 1) / kBlurTX; ++q) xx[q] = reflect101(x0 - R + tx + q * kBlurTX, W);
     if constexpr (kFromU8) {
-        float* g = in + IH * IWP;
+        float4* rtab = (float4*)(in + blur_rtab_off(R));  // per tile row: gray row offsets of sy0 / sy1, fy, 1 - fy
+        float* g = in + blur_rtab_off(R) + 4 * IH;
         constexpr int GW = blur_gw(R);
         const int ylo = max(y0 - R, 0), yhi = min(y0 + kBlurTY + R, H) - 1;
         const int xlo = max(x0 - R, 0), xhi = min(x0 + kBlurTX + R, W) - 1;
@@ -228,29 +233,34 @@ __global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* 
                 if (gy <= gy1 && gx <= gx1) g[(gy - gy0) * GW + tx] = gv[i];
             }
         }
+        if (tid < IH) {  // the row half of the upsampling coordinates, once per tile row
+            int sy0, sy1;
+            float fy;
+            up_coord(reflect101(y0 - R + tid, H), H0, sy0, sy1, fy);
+            rtab[tid] = make_float4(__int_as_float((sy0 - gy0) * GW), __int_as_float((sy1 - gy0) * GW), fy, 1.f - fy);
+        }
         __syncthreads();
         constexpr int NQ = (IW + kBlurTX - 1) / kBlurTX;
         int cx0[NQ], cx1[NQ];
-        float cfx[NQ];
+        float cfx[NQ], cfx1[NQ];
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             up_coord(xx[q], W0, cx0[q], cx1[q], cfx[q]);
             cx0[q] -= gx0;
             cx1[q] -= gx0;
+            cfx1[q] = 1.f - cfx[q];
         }
         for (int iy = ty; iy < IH; iy += kBlurTYT) {
-            int sy0, sy1;
-            float fy;
-            up_coord(reflect101(y0 - R + iy, H), H0, sy0, sy1, fy);
-            const float* r0p = g + (sy0 - gy0) * GW;
-            const float* r1p = g + (sy1 - gy0) * GW;
+            const float4 rt = rtab[iy];  // same address across the wave: broadcast
+            const float* r0p = g + __float_as_int(rt.x);
+            const float* r1p = g + __float_as_int(rt.y);
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
                 const int ix = tx + q * kBlurTX;
                 if (ix < IW) {
-                    const float r0 = r0p[cx0[q]] * (1.f - cfx[q]) + r0p[cx1[q]] * cfx[q];
-                    const float r1 = r1p[cx0[q]] * (1.f - cfx[q]) + r1p[cx1[q]] * cfx[q];
-                    in[iy * IWP + ix] = r0 * (1.f - fy) + r1 * fy;
+                    const float r0 = r0p[cx0[q]] * cfx1[q] + r0p[cx1[q]] * cfx[q];
+                    const float r1 = r1p[cx0[q]] * cfx1[q] + r1p[cx1[q]] * cfx[q];
+                    in[iy * IWP + ix] = r0 * rt.w + r1 * rt.z;
                 }
             }
         }
