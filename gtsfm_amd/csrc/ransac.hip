@@ -1108,23 +1108,31 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
     }
     __syncthreads();
     const int total = flat_off[kBatch];
-    for (int ci = wave; ci < total; ci += kScoreWaves) {
+    // candidate ci's E (fp64 in HBM); the next one of this wave is fetched while the current one is counted
+    auto fetch = [&](int ci, double (&e)[9]) {
         const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
-        const int sI = ci - flat_off[hl];
-        const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9) + 9 * sI;
+        const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9) + 9 * (ci - flat_off[hl]);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) e[k] = ch[k];
+    };
+    double en[9];
+    if (wave < total) fetch(wave, en);
+    for (int ci = wave; ci < total; ci += kScoreWaves) {
         float E[9];
 #pragma unroll
-        for (int e = 0; e < 9; ++e) E[e] = (float)ch[e];
+        for (int e = 0; e < 9; ++e) E[e] = (float)en[e];
+        if (ci + kScoreWaves < total) fetch(ci + kScoreWaves, en);
         const uint32_t my_low = 0xFFFFFFFEu - (uint32_t)ci;
         int c = 0;
         bool alive = true;
         for (int base = 0; base < M; base += 64) {
+            // read before the test so the LDS latency hides under it; a stale best is smaller, so the exit stays exact
+            const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
             const int i = base + lane;
             const bool in = i < M && sampson_inlier(E, spts[i], thr2);
             c += __popcll(__ballot(in));
             const int remaining = M - (base + 64);
             if (remaining > 0) {
-                const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
                 const int bc = (int)(bk >> 32) - 1;
                 if (c + remaining < bc || (c + remaining == bc && my_low < (uint32_t)bk)) {
                     alive = false;
