@@ -147,7 +147,11 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 // kFromU8: the input is the 2x-upsampled gray image, computed from a gray tile of the u8 source staged in LDS.
 // Tiles are mapped XCD-contiguously (consecutive workgroups land on different XCDs; each XCD gets a contiguous run
 // of tiles so halos are shared through its own L2).
-constexpr int kBlurTX = 64, kBlurTY = 64, kBlurTYT = 4, kBlurColRows = kBlurTY / kBlurTYT;
+constexpr int kBlurTX = 64;
+// Tile height per radius: 64 rows x 4 waves, or for the wide kernels (and the upsampling one) 96 rows x 8 waves, where
+// the smaller row-pass halo share pays for the coarser tiling (measured per radius on octave 0).
+__host__ __device__ constexpr int blur_ty(int r, bool u8) { return (u8 || r >= 9) ? 96 : 64; }
+__host__ __device__ constexpr int blur_tyt(int r, bool u8) { return blur_ty(r, u8) == 96 ? 8 : 4; }
 constexpr int kBlurRowOut = 8, kBlurRowThr = kBlurTX / kBlurRowOut;  // row pass: outputs per thread, threads per row
 typedef float pf2 __attribute__((ext_vector_type(2)));
 constexpr int kBlurMaxR = 16;
@@ -155,13 +159,13 @@ constexpr int kBlurMaxR = 16;
 // LDS row stride of the input tile: >= 64 + 2r and = 2 (mod 8), so the row pass's ds_read_b64 windows (8 lanes per
 // row at 32-B steps, four rows per 32-lane group) hit 64 distinct banks
 __host__ __device__ constexpr int blur_iwp(int r) { return (kBlurTX + 2 * r + 5) / 8 * 8 + 2; }
-__host__ __device__ constexpr int blur_gh(int r) { return (kBlurTY + 2 * r) / 2 + 4; }
+__host__ __device__ constexpr int blur_gh(int r) { return (blur_ty(r, true) + 2 * r) / 2 + 4; }
 __host__ __device__ constexpr int blur_gw(int r) { return (kBlurTX + 2 * r) / 2 + 4; }
 // u8 variant: input tile | per-row upsampling table (float4 per tile row) | gray source tile
-__host__ __device__ constexpr int blur_rtab_off(int r) { return ((kBlurTY + 2 * r) * blur_iwp(r) + 3) / 4 * 4; }
+__host__ __device__ constexpr int blur_rtab_off(int r) { return ((blur_ty(r, true) + 2 * r) * blur_iwp(r) + 3) / 4 * 4; }
 __host__ __device__ constexpr size_t blur_lds_bytes(int r, bool u8) {
-    return (size_t)(u8 ? blur_rtab_off(r) + 4 * (kBlurTY + 2 * r) + blur_gh(r) * blur_gw(r)
-                       : (kBlurTY + 2 * r) * blur_iwp(r)) *
+    return (size_t)(u8 ? blur_rtab_off(r) + 4 * (blur_ty(r, true) + 2 * r) + blur_gh(r) * blur_gw(r)
+                       : (blur_ty(r, false) + 2 * r) * blur_iwp(r)) *
            sizeof(float);
 }
 
@@ -184,11 +188,12 @@ __device__ __forceinline__ void up_coord(int x, int W, int& s0, int& s1, float& 
 }
 
 template <int R, bool kFromU8>
-__global__ __launch_bounds__(kBlurTX* kBlurTYT) void blur2d_kernel(const float* __restrict__ src,
+__global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(const float* __restrict__ src,
                                                                   const uint8_t* __restrict__ img8, int C, int H0,
                                                                   int W0, float* __restrict__ dst, int H, int W,
                                                                   int n_tx, int n_ty, int n_img, Taps t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int kBlurTY = blur_ty(R, kFromU8), kBlurTYT = blur_tyt(R, kFromU8), kBlurColRows = kBlurTY / kBlurTYT;
     constexpr int IW = kBlurTX + 2 * R, IH = kBlurTY + 2 * R, IWP = blur_iwp(R);
     constexpr int NV = (kBlurRowOut + 2 * R) / 2;  // float2 words per row-pass window
     static_assert((kBlurRowThr - 1) * kBlurRowOut + 2 * NV <= IWP, "row-pass window past the LDS row");
@@ -1098,10 +1103,11 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
     for (int i = 0; i < kLevels; ++i)
         if (taps[i].r < 1 || taps[i].r > kBlurMaxR) return GTSFM_ERR_ARG;
     auto blur = [&](const float* src, float* dst, int h, int w, const Taps& t) -> int {
-        const int n_tx = (w + kBlurTX - 1) / kBlurTX, n_ty = (h + kBlurTY - 1) / kBlurTY;
+        const bool u8 = src == nullptr;
+        const int ty = blur_ty(t.r, u8), tyt = blur_tyt(t.r, u8);
+        const int n_tx = (w + kBlurTX - 1) / kBlurTX, n_ty = (h + ty - 1) / ty;
         const int total = n_tx * n_ty * B;
         const dim3 grid((unsigned)((total + 7) / 8 * 8));
-        const bool u8 = src == nullptr;
         const void* fn = u8 ? (const void*)BlurTable<true>::get(t.r) : (const void*)BlurTable<false>::get(t.r);
         const size_t lds = blur_lds_bytes(t.r, u8);
         if (lds > 65536) {
@@ -1109,10 +1115,10 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
             if (e != hipSuccess) return GTSFM_ERR_HIP;
         }
         if (u8)
-            hipLaunchKernelGGL(BlurTable<true>::get(t.r), grid, dim3(kBlurTX, kBlurTYT), lds, stream, nullptr,
+            hipLaunchKernelGGL(BlurTable<true>::get(t.r), grid, dim3(kBlurTX, tyt), lds, stream, nullptr,
                                d_images, channels, H, W, dst, h, w, n_tx, n_ty, B, t);
         else
-            hipLaunchKernelGGL(BlurTable<false>::get(t.r), grid, dim3(kBlurTX, kBlurTYT), lds, stream, src, nullptr, 0,
+            hipLaunchKernelGGL(BlurTable<false>::get(t.r), grid, dim3(kBlurTX, tyt), lds, stream, src, nullptr, 0,
                                0, 0, dst, h, w, n_tx, n_ty, B, t);
         return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
     };
