@@ -22,7 +22,9 @@
 
 namespace {
 
-constexpr int kBatch = 64;
+constexpr int kBatch = 64;      // hypotheses per chunk: the iteration bound is re-evaluated after each chunk
+constexpr int kMaxGroups = 8;   // chunks one solve/score launch may cover
+constexpr int kMaxHyp = kBatch * kMaxGroups;  // per-pair stride of the stage / nsol / cand buffers
 constexpr int kMaxSol = 10;
 constexpr int kLoSteps = 4;
 constexpr int kLoIrls = 3;
@@ -916,7 +918,7 @@ __device__ int wave_cheirality(const double* R, const double* t, const double2* 
     return good;
 }
 
-__device__ int update_num_iters(double p, double ep, int model_points, int max_iters) {
+__device__ __attribute__((noinline)) int update_num_iters(double p, double ep, int model_points, int max_iters) {
     p = fmax(p, 0.0); p = fmin(p, 1.0);
     ep = fmax(ep, 0.0); ep = fmin(ep, 1.0);
     double num = fmax(1.0 - p, 2.2250738585072014e-308);
@@ -981,10 +983,12 @@ __global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int 
     st[p] = s;
 }
 
-// Stage 1, two 64-lane workgroups per active pair (blockIdx.y = half of the batch): lanes 2k, 2k+1 sample hypothesis
-// h = done + 32 blockIdx.y + k, both run the nullspace, and split the 10 x 20 elimination by column halves; N (even
-// lane) + the reduced rows (odd lane) go to stage 2 through `stage` ([P][kStageVals][64], hypothesis-minor).
-// nsol = 1 marks a non-degenerate sample for stage 2, 0 a finished one.
+// Stage 1, two 64-lane workgroups per chunk of an active pair (blockIdx.y = half of a chunk): lanes 2k, 2k+1 sample
+// hypothesis h = done + 32 blockIdx.y + k, both run the nullspace, and split the 10 x 20 elimination by column halves;
+// N (even lane) + the reduced rows (odd lane) go to stage 2 through `stage` ([P][kStageVals][kMaxHyp],
+// hypothesis-minor). nsol = 1 marks a non-degenerate sample for stage 2, 0 a finished one. A launch covers
+// gridDim.y / 2 chunks; a chunk that starts at or past the pair's current iteration bound is skipped (the bound only
+// falls, so the score kernel never reaches it).
 __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restrict__ match_count, int mcap,
                                                               const double2* __restrict__ x1n_all,
                                                               const double2* __restrict__ x2n_all, uint64_t seed,
@@ -997,7 +1001,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
     const int M = match_count[p];
     if (M < 6) return;
     const int done = st[p].done;
-    if (done >= st[p].niters) return;
+    if (done + (hyp & ~(kBatch - 1)) >= st[p].niters) return;
     const double2* x1 = x1n_all + (size_t)p * mcap;
     const double2* x2 = x2n_all + (size_t)p * mcap;
     const SolverMem mem = solver_mem(smem, lane);
@@ -1014,25 +1018,25 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
         double N[4][9], Rt[6][10];
         if (five_point_stage1(s1, s2, mem, part, N, Rt)) {
             ok = 1;
-            double* out = stage + (size_t)p * kStageVals * kBatch + hyp;
+            double* out = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
             if (part) {
 #pragma unroll
                 for (int r = 0; r < 6; ++r)
 #pragma unroll
-                    for (int j = 0; j < 10; ++j) out[(10 * r + j) * kBatch] = Rt[r][j];
+                    for (int j = 0; j < 10; ++j) out[(10 * r + j) * kMaxHyp] = Rt[r][j];
             } else {
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
 #pragma unroll
-                    for (int j = 0; j < 9; ++j) out[(60 + 9 * k + j) * kBatch] = N[k][j];
+                    for (int j = 0; j < 9; ++j) out[(60 + 9 * k + j) * kMaxHyp] = N[k][j];
             }
         }
     }
-    if (!part) nsol[(size_t)p * kBatch + hyp] = ok;
+    if (!part) nsol[(size_t)p * kMaxHyp + hyp] = ok;
 }
 
-// Stage 2, one 64-lane workgroup per active pair (three per CU): lane l turns stage 1's output into the candidate
-// essential matrices of hypothesis done + l (fp64) -> cand, nsol.
+// Stage 2, one 64-lane workgroup per chunk of an active pair (blockIdx.y = chunk): lane l turns stage 1's output into
+// the candidate essential matrices of hypothesis done + 64 blockIdx.y + l (fp64) -> cand, nsol.
 __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restrict__ match_count,
                                                               const PairState* __restrict__ st,
                                                               const double* __restrict__ stage,
@@ -1041,21 +1045,22 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
     const int p = blockIdx.x, lane = threadIdx.x;
     const int M = match_count[p];
     if (M < 6) return;
-    if (st[p].done >= st[p].niters) return;
-    int* ns_out = nsol + (size_t)p * kBatch + lane;
+    const int hyp = blockIdx.y * kBatch + lane;
+    if (st[p].done + (int)blockIdx.y * kBatch >= st[p].niters) return;
+    int* ns_out = nsol + (size_t)p * kMaxHyp + hyp;
     if (*ns_out == 0) return;  // degenerate sample: stays 0
     const RootMem mem = root_mem(smem, lane);
     double N[4][9], Rt[6][10];
-    const double* in = stage + (size_t)p * kStageVals * kLanes + lane;
+    const double* in = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int j = 0; j < 10; ++j) Rt[r][j] = in[(10 * r + j) * kLanes];
+        for (int j = 0; j < 10; ++j) Rt[r][j] = in[(10 * r + j) * kMaxHyp];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
 #pragma unroll
-        for (int j = 0; j < 9; ++j) N[k][j] = in[(60 + 9 * k + j) * kLanes];
-    double* cout = cand + ((size_t)p * kBatch + lane) * (kMaxSol * 9);
+        for (int j = 0; j < 9; ++j) N[k][j] = in[(60 + 9 * k + j) * kMaxHyp];
+    double* cout = cand + ((size_t)p * kMaxHyp + hyp) * (kMaxSol * 9);
     const int ns = five_point_stage2(N, Rt, mem, [&](int s, const double* E) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) cout[9 * s + e] = E[e];
@@ -1063,12 +1068,13 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
     *ns_out = ns;
 }
 
-// One 4-wave workgroup per active pair: the pair's putatives are staged in LDS once, the batch's candidates
-// (flattened in (hypothesis, solution) order) are dealt round-robin to the waves, each counted by one wave with an
-// exact early exit against the running best. The best is an LDS atomicMax on the key (count + 1, ~index), so the
-// winner is the FIRST candidate in order with the largest count, as in the sequential scan of oracle/ransac.c: a
-// candidate stops once it can no longer beat the current best count, or only tie it from a later index. Then the
-// OpenCV iteration bound is applied after the batch.
+// One 4-wave workgroup per active pair: the pair's putatives are staged in LDS once, then the launch's chunks are
+// scored in order. A chunk's candidates (flattened in (hypothesis, solution) order) are dealt round-robin to the
+// waves, each counted by one wave with an exact early exit against the running best. The best is an LDS atomicMax on
+// the key (count + 1, ~index), so the winner is the FIRST candidate in order with the largest count, as in the
+// sequential scan of oracle/ransac.c: a candidate stops once it can no longer beat the current best count, or only tie
+// it from a later index. The OpenCV iteration bound is applied after every chunk, and the pair stops there once
+// done >= niters, exactly as the oracle's batch loop (oracle/ransac.c:679-706).
 constexpr int kScoreWaves = 4;
 
 __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,
@@ -1077,92 +1083,115 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
                                                                         const float4* __restrict__ pts_all,
                                                                         double thr_px, double prob,
                                                                         const double* __restrict__ cand,
-                                                                        const int* __restrict__ nsol,
+                                                                        const int* __restrict__ nsol, int n_chunks,
                                                                         PairState* __restrict__ st) {
     extern __shared__ float4 spts[];  // [M]
     __shared__ unsigned long long best_key;
     __shared__ int flat_off[kBatch + 1];  // candidates of hypotheses < h
+    __shared__ int sh_bound[2];           // best count, iteration bound after the chunk (from thread 0)
     const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int M = match_count[p];
     if (M < 6) return;
-    PairState s = st[p];
-    if (s.done >= s.niters) return;
+    // thread 0 updates the pair state after each chunk; the others follow best / niters / done
+    int best = st[p].best, best_h = st[p].best_h, best_s = st[p].best_s, done = st[p].done, niters = st[p].niters;
+    if (done >= niters) return;
     const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
     const double fx = fmax(intr[3 * i1], intr[3 * i2]);  // opencv_verifier_base.py:86
     const double thr = thr_px / fx;
     const float thr2 = (float)(thr * thr);
     const float4* pts = pts_all + (size_t)p * mcap;
     for (int i = tid; i < M; i += 64 * kScoreWaves) spts[i] = pts[i];
-    if (wave == 0) {
-        int v = nsol[(size_t)p * kBatch + lane];
+    long best_off = -1;  // cand offset of a winner found by this launch
+#pragma unroll 1
+    for (int g = 0; g < n_chunks && done < niters; ++g) {
+        const size_t hbase = (size_t)p * kMaxHyp + (size_t)g * kBatch;  // the chunk's first hypothesis slot
+        if (wave == 0) {
+            int v = nsol[hbase + lane];
 #pragma unroll
-        for (int m = 1; m < 64; m <<= 1) {  // inclusive scan over the 64 hypotheses
-            const int o = __shfl_up(v, m);
-            if (lane >= m) v += o;
-        }
-        flat_off[lane + 1] = v;
-        if (lane == 0) {
-            flat_off[0] = 0;
-            best_key = ((unsigned long long)(uint32_t)(s.best + 1) << 32) | 0xFFFFFFFFull;  // index -1: before all
-        }
-    }
-    __syncthreads();
-    const int total = flat_off[kBatch];
-    // candidate ci's E (fp64 in HBM); the next one of this wave is fetched while the current one is counted
-    auto fetch = [&](int ci, double (&e)[9]) {
-        const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
-        const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9) + 9 * (ci - flat_off[hl]);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) e[k] = ch[k];
-    };
-    double en[9];
-    if (wave < total) fetch(wave, en);
-    for (int ci = wave; ci < total; ci += kScoreWaves) {
-        float E[9];
-#pragma unroll
-        for (int e = 0; e < 9; ++e) E[e] = (float)en[e];
-        if (ci + kScoreWaves < total) fetch(ci + kScoreWaves, en);
-        const uint32_t my_low = 0xFFFFFFFEu - (uint32_t)ci;
-        int c = 0;
-        bool alive = true;
-        for (int base = 0; base < M; base += 64) {
-            // read before the test so the LDS latency hides under it; a stale best is smaller, so the exit stays exact
-            const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
-            const int i = base + lane;
-            const bool in = i < M && sampson_inlier(E, spts[i], thr2);
-            c += __popcll(__ballot(in));
-            const int remaining = M - (base + 64);
-            if (remaining > 0) {
-                const int bc = (int)(bk >> 32) - 1;
-                if (c + remaining < bc || (c + remaining == bc && my_low < (uint32_t)bk)) {
-                    alive = false;
-                    break;
-                }
+            for (int m = 1; m < 64; m <<= 1) {  // inclusive scan over the 64 hypotheses
+                const int o = __shfl_up(v, m);
+                if (lane >= m) v += o;
+            }
+            flat_off[lane + 1] = v;
+            if (lane == 0) {
+                flat_off[0] = 0;
+                best_key = ((unsigned long long)(uint32_t)(best + 1) << 32) | 0xFFFFFFFFull;  // index -1: before all
             }
         }
-        if (alive && lane == 0) atomicMax(&best_key, ((unsigned long long)(uint32_t)(c + 1) << 32) | my_low);
+        __syncthreads();
+        const int total = flat_off[kBatch];
+        // candidate ci's E (fp64 in HBM); the next one of this wave is fetched while the current one is counted
+        auto fetch = [&](int ci, double (&e)[9]) {
+            const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
+            const double* ch = cand + (hbase + hl) * (kMaxSol * 9) + 9 * (ci - flat_off[hl]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) e[k] = ch[k];
+        };
+        double en[9];
+        if (wave < total) fetch(wave, en);
+#pragma unroll 1
+        for (int ci = wave; ci < total; ci += kScoreWaves) {
+            float E[9];
+#pragma unroll
+            for (int e = 0; e < 9; ++e) E[e] = (float)en[e];
+            if (ci + kScoreWaves < total) fetch(ci + kScoreWaves, en);
+            const uint32_t my_low = 0xFFFFFFFEu - (uint32_t)ci;
+            int c = 0;
+            bool alive = true;
+#pragma unroll 1
+            for (int base = 0; base < M; base += 64) {
+                // read before the test so the LDS latency hides under it; a stale best is smaller, so the exit stays
+                // exact
+                const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
+                const int i = base + lane;
+                const bool in = i < M && sampson_inlier(E, spts[i], thr2);
+                c += __popcll(__ballot(in));
+                const int remaining = M - (base + 64);
+                if (remaining > 0) {
+                    const int bc = (int)(bk >> 32) - 1;
+                    if (c + remaining < bc || (c + remaining == bc && my_low < (uint32_t)bk)) {
+                        alive = false;
+                        break;
+                    }
+                }
+            }
+            if (alive && lane == 0) atomicMax(&best_key, ((unsigned long long)(uint32_t)(c + 1) << 32) | my_low);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned long long bk = best_key;
+            const uint32_t low = (uint32_t)bk;
+            if (low != 0xFFFFFFFFu) {  // a candidate of this chunk beat the previous best
+                const int ci = (int)(0xFFFFFFFEu - low);
+                int hl = 0;
+                while (flat_off[hl + 1] <= ci) ++hl;
+                const int sI = ci - flat_off[hl];
+                best = (int)(bk >> 32) - 1;
+                best_h = done + hl;
+                best_s = sI;
+                best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
+            }
+            if (best > 0) {
+                const int upd = update_num_iters(prob, (double)(M - best) / M, 5, niters);
+                if (upd < niters) niters = upd;
+            }
+            sh_bound[0] = best;
+            sh_bound[1] = niters;
+        }
+        __syncthreads();  // flat_off / best_key are rewritten by the next chunk
+        best = sh_bound[0];
+        niters = sh_bound[1];
+        done += kBatch;
     }
-    __syncthreads();
     if (tid == 0) {
-        const unsigned long long bk = best_key;
-        const uint32_t low = (uint32_t)bk;
-        if (low != 0xFFFFFFFFu) {  // a candidate of this batch beat the previous best
-            const int ci = (int)(0xFFFFFFFEu - low);
-            int hl = 0;
-            while (flat_off[hl + 1] <= ci) ++hl;
-            const int sI = ci - flat_off[hl];
-            s.best = (int)(bk >> 32) - 1;
-            s.best_h = s.done + hl;
-            s.best_s = sI;
-            const double* ch = cand + ((size_t)p * kBatch + hl) * (kMaxSol * 9) + 9 * sI;
-            for (int e = 0; e < 9; ++e) s.bestE[e] = ch[e];
-        }
-        s.done += kBatch;
-        if (s.best > 0) {
-            const int upd = update_num_iters(prob, (double)(M - s.best) / M, 5, s.niters);
-            if (upd < s.niters) s.niters = upd;
-        }
-        st[p] = s;
+        PairState& o = st[p];
+        o.best = best;
+        o.best_h = best_h;
+        o.best_s = best_s;
+        o.done = done;
+        o.niters = niters;
+        if (best_off >= 0)
+            for (int e = 0; e < 9; ++e) o.bestE[e] = cand[best_off + e];
     }
 }
 
@@ -1307,11 +1336,11 @@ static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_p
     *off_st = o;
     o += gtsfm_align_up((size_t)n_pairs * sizeof(PairState), 256);
     *off_cand = o;
-    o += gtsfm_align_up((size_t)n_pairs * kBatch * kMaxSol * 9 * sizeof(double), 256);
+    o += gtsfm_align_up((size_t)n_pairs * kMaxHyp * kMaxSol * 9 * sizeof(double), 256);
     *off_nsol = o;
-    o += gtsfm_align_up((size_t)n_pairs * kBatch * sizeof(int), 256);
+    o += gtsfm_align_up((size_t)n_pairs * kMaxHyp * sizeof(int), 256);
     *off_stage = o;
-    o += gtsfm_align_up((size_t)n_pairs * kStageVals * kBatch * sizeof(double), 256);
+    o += gtsfm_align_up((size_t)n_pairs * kStageVals * kMaxHyp * sizeof(double), 256);
     return o;
 }
 
@@ -1363,15 +1392,19 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
             score_lds_set = score_lds;
         }
     }
+    // Chunks of 64 hypotheses, as the oracle; launches cover 1, 1, 2, 4, 8, 8, ... chunks. Most pairs stop within the
+    // first two chunks; the pairs that run on are few, so their later chunks are solved together (speculatively: a
+    // chunk the score kernel does not reach is discarded) to give the solver kernels enough waves.
     const int n_batches = (max_iters + kBatch - 1) / kBatch;
-    for (int b = 0; b < n_batches; ++b) {
-        hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs, kBatch / (kLanes / 2)), dim3(64), kSolveLds, stream, d_match_count, mcap, x1n,
-                           x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
-        hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs), dim3(64), kRootLds, stream, d_match_count, st, stage,
-                           cand, nsol);
+    for (int b = 0, g = 1, launch = 0; b < n_batches; b += g, ++launch) {
+        g = launch < 2 ? 1 : std::min(kMaxGroups, 1 << (launch - 1));
+        g = std::min(g, n_batches - b);
+        hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs, g * kBatch / (kLanes / 2)), dim3(64), kSolveLds, stream,
+                           d_match_count, mcap, x1n, x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
+        hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs, g), dim3(64), kRootLds, stream, d_match_count, st,
+                           stage, cand, nsol);
         hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream, d_pairs,
-                           d_intrinsics,
-                           d_match_count, mcap, pts, thr_px, prob, cand, nsol, st);
+                           d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask};

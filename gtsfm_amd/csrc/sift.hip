@@ -694,6 +694,7 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
 
 // ------------------------------------------------------------------ top-k per image
 constexpr int kTopkThreads = 1024;
+constexpr int kTopkTieCap = 512;  // tie slots after the np2 sort slots
 
 struct SortRec {
     unsigned long long key;  // (~response bits) << 32 | location code
@@ -738,7 +739,7 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __rest
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int* hdr = (int*)smem;                         // [0] n_less, [1] n_eq, [2] scratch
     int* histo = (int*)(smem + 16);                // [256]
-    SortRec* recs = (SortRec*)(smem + 16 + 1024);  // [pow2(max_kpts)]
+    SortRec* recs = (SortRec*)(smem + 16 + 1024);  // [pow2(max_kpts) + kTopkTieCap]
     const int img = blockIdx.x, tid = threadIdx.x;
     const int N = min(kp_counts[img], kp_cap);
     const KeyRec* K = kps + (size_t)img * kp_cap;
@@ -785,25 +786,56 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __rest
     __syncthreads();
     const int n_less = hdr[0];
     if (N > max_kpts) {
-        // ties at the threshold (rare, few): collect after the strict set, sort them, keep the first (k - n_less)
+        // ties at the threshold: the (k - n_less) smallest in (location, angle, index) order. They are collected after
+        // the strict set into the np2 + kTopkTieCap slots (ties are usually a handful: the orientations of one
+        // location share its response) and selection-sorted; should they overflow the slots, they are instead picked
+        // one at a time by block-wide minimum, each strictly after the previous pick in the total order.
+        const int take = k - n_less;
         for (int i = tid; i < N; i += kTopkThreads) {
             const uint32_t hi = ~__float_as_uint(K[i].response);
             if (hi == T) {
                 const int s = atomicAdd(&hdr[1], 1);
-                if (n_less + s < np2) recs[n_less + s] = make_rec(K[i], i);
+                if (n_less + s < np2 + kTopkTieCap) recs[n_less + s] = make_rec(K[i], i);
             }
         }
         __syncthreads();
-        const int n_eq = min(hdr[1], np2 - n_less);
-        // selection sort of the tie group by (key, angle) is enough: ties are a handful of keypoints
-        if (tid == 0) {
-            for (int a = 0; a < n_eq; ++a) {
-                int m = a;
-                for (int b = a + 1; b < n_eq; ++b)
-                    if (rec_less(recs[n_less + b], recs[n_less + m])) m = b;
-                const SortRec t = recs[n_less + a];
-                recs[n_less + a] = recs[n_less + m];
-                recs[n_less + m] = t;
+        const int n_eq = hdr[1];
+        if (n_less + n_eq <= np2 + kTopkTieCap) {
+            if (tid == 0) {
+                for (int a = 0; a < take; ++a) {
+                    int m = a;
+                    for (int b = a + 1; b < n_eq; ++b)
+                        if (rec_less(recs[n_less + b], recs[n_less + m])) m = b;
+                    const SortRec t = recs[n_less + a];
+                    recs[n_less + a] = recs[n_less + m];
+                    recs[n_less + m] = t;
+                }
+            }
+        } else {
+            SortRec* red = recs + np2;  // [kTopkThreads / 64] per-wave minima (the tie slots are not needed here)
+            SortRec prev{0, 0, -1};
+            for (int a = 0; a < take; ++a) {
+                SortRec best{~0ull, ~0u, 0x7FFFFFFF};
+                for (int i = tid; i < N; i += kTopkThreads) {
+                    if (~__float_as_uint(K[i].response) != T) continue;
+                    const SortRec r = make_rec(K[i], i);
+                    if ((a == 0 || rec_less(prev, r)) && rec_less(r, best)) best = r;
+                }
+                for (int m = 32; m > 0; m >>= 1) {
+                    SortRec o;
+                    o.key = __shfl_xor(best.key, m);
+                    o.angle = __shfl_xor(best.angle, m);
+                    o.idx = __shfl_xor(best.idx, m);
+                    if (rec_less(o, best)) best = o;
+                }
+                if ((tid & 63) == 0) red[tid >> 6] = best;
+                __syncthreads();
+                best = red[0];
+                for (int w = 1; w < kTopkThreads / 64; ++w)
+                    if (rec_less(red[w], best)) best = red[w];
+                __syncthreads();
+                if (tid == 0) recs[n_less + a] = best;
+                prev = best;
             }
         }
         __syncthreads();
@@ -1153,7 +1185,7 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
     }
     int np2 = 1;
     while (np2 < max_kpts) np2 <<= 1;
-    const size_t topk_lds = 16 + 1024 + (size_t)np2 * sizeof(SortRec);
+    const size_t topk_lds = 16 + 1024 + (size_t)(np2 + kTopkTieCap) * sizeof(SortRec);
     if (topk_lds > 160 * 1024) return GTSFM_ERR_ARG;
     if (topk_lds > 65536)
         GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)topk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -114,6 +114,7 @@ def test_batched_parity_with_oracle(dev, oracle_mod):
     R_all = res.R.cpu().numpy()
     t_all = res.t.cpu().numpy()
     mask = res.mask.cpu().numpy()
+    n_hyp = res.n_hyp.cpu().numpy()
     for p in range(n_pairs):
         K = Ks[p]
         a, b = kps[p]
@@ -121,7 +122,9 @@ def test_batched_parity_with_oracle(dev, oracle_mod):
         x2 = (b.astype(np.float32).astype(np.float64) - K[:2, 2]) / K[0, 0]
         ref = oracle_mod.ransac_E(x1, x2, 4.0 / K[0, 0], pair_id=p)
         assert status[p] == native.RANSAC_STATUS_OK, p
-        _, rmask, rR, rt, rn, _ = ref
+        _, rmask, rR, rt, rn, rh = ref
+        # hypotheses evaluated: chunks of 64 with the bound re-evaluated per chunk, whatever chunks a launch covers
+        assert int(n_hyp[p]) == rh, (p, n_hyp[p], rh)
         assert abs(int(n_inl[p]) - rn) <= max(1, 0.01 * rn), (p, n_inl[p], rn)
         agree = (mask[p, : Ms[p]] == rmask).mean()
         assert agree >= 0.99, (p, agree)
