@@ -35,6 +35,9 @@ namespace {
 // d2 saturates at 2^(32-ib)-1; finalize recomputes any row/column whose top-2 touched the saturated value.
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 constexpr int kMaxKmaxPacked = 8192;   // fast path
+// Correctly rounded fp32 square root, as the oracle's sqrtf (HIP's __fsqrt_rn is the ~1-ulp native sqrt).
+__device__ __forceinline__ float sqrt_cr(float x) { return __builtin_sqrtf(x); }
+
 constexpr int kMaxKmax = 65535;        // exact path (16-bit indices in the sort key)
 
 inline int index_bits(int kmax) {
@@ -326,6 +329,7 @@ struct ExactTop2 {
 
 __global__ void exact_top2_kernel(const float* __restrict__ desc, const int* __restrict__ counts, int kmax, int dim,
                                   const int* __restrict__ pairs, int swap, ExactTop2* __restrict__ out) {
+#pragma clang fp contract(off)  // sequential, unfused (a-b)^2 sums: the oracle's arithmetic (oracle/twoway.c)
     const int p = blockIdx.y;
     const int iq = pairs[2 * p + (swap ? 1 : 0)], it = pairs[2 * p + (swap ? 0 : 1)];
     const int nq = counts[iq], nt = counts[it];
@@ -339,10 +343,10 @@ __global__ void exact_top2_kernel(const float* __restrict__ desc, const int* __r
         const float* t = T + (size_t)j * dim;
         float acc = 0.f;
         for (int k = 0; k < dim; ++k) {
-            const float df = __fsub_rn(q[k], t[k]);
-            acc = __fadd_rn(acc, __fmul_rn(df, df));
+            const float df = q[k] - t[k];
+            acc = acc + df * df;  // unfused: contract(off) above
         }
-        const float d = __fsqrt_rn(acc);
+        const float d = sqrt_cr(acc);
         if (d < b2) {
             if (d < b1) {
                 b2 = b1;
@@ -370,6 +374,7 @@ __device__ __forceinline__ bool ratio_ok(float d1, float d2, double ratio) {
 // rows/columns whose packed keys saturated). Same arithmetic as exact_top2_kernel.
 __device__ void block_exact_top2(const float* __restrict__ q, const float* __restrict__ T, int nt, int dim,
                                  float* red_d, int* red_j, float& d1, float& d2, int& j1) {
+#pragma clang fp contract(off)
     const int tid = threadIdx.x;
     float b1 = __builtin_inff(), b2 = __builtin_inff();
     int bj = -1;
@@ -377,10 +382,10 @@ __device__ void block_exact_top2(const float* __restrict__ q, const float* __res
         const float* t = T + (size_t)j * dim;
         float acc = 0.f;
         for (int k = 0; k < dim; ++k) {
-            const float df = __fsub_rn(q[k], t[k]);
-            acc = __fadd_rn(acc, __fmul_rn(df, df));
+            const float df = q[k] - t[k];
+            acc = acc + df * df;  // unfused: contract(off) above
         }
-        const float d = __fsqrt_rn(acc);
+        const float d = sqrt_cr(acc);
         if (d < b2) {
             if (d < b1) { b2 = b1; b1 = d; bj = j; } else { b2 = d; }
         }
@@ -466,7 +471,7 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
         for (int j = tid; j < n2 && n1 > 0; j += kFinThreads) {
             const uint2 v = s2[j];
             if (v.x == kNoKey || v.x != v.y) continue;
-            const float d = __fsqrt_rn((float)(v.x & kMant));
+            const float d = sqrt_cr((float)(v.x & kMant));
             if (ratio_ok(d, d, ratio)) redo[atomicAdd(&hdr[1], 1)] = j;
         }
         for (int i = tid; i < n1 && n2 > 0; i += kFinThreads) {
@@ -476,9 +481,9 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
             const uint32_t d = k.x >> ib;
             const uint2 v = s2[j];
             if (v.x == v.y || (v.x & kMant) != d) continue;  // j tied (redo) or j's nearest is not i
-            const float d1r = __fsqrt_rn((float)d);
-            const float d2r = (k.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(k.y >> ib));
-            const float d2c = (v.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(v.y & kMant));
+            const float d1r = sqrt_cr((float)d);
+            const float d2r = (k.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(k.y >> ib));
+            const float d2c = (v.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(v.y & kMant));
             if (ratio_ok(d1r, d2r, ratio) && ratio_ok(d1r, d2c, ratio)) push(i, j, d1r);
         }
         __syncthreads();
@@ -508,11 +513,11 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
                 redo[atomicAdd(&hdr[1], 1)] = i;
                 continue;
             }
-            d1r = __fsqrt_rn((float)(r.x >> ib));
-            d2r = (r.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(r.y >> ib));
+            d1r = sqrt_cr((float)(r.x >> ib));
+            d2r = (r.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(r.y >> ib));
             ic = (int)(c.x & imask);
-            d1c = __fsqrt_rn((float)(c.x >> ib));
-            d2c = (c.y == kNoKey) ? __builtin_inff() : __fsqrt_rn((float)(c.y >> ib));
+            d1c = sqrt_cr((float)(c.x >> ib));
+            d2c = (c.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(c.y >> ib));
         } else {
             const ExactTop2 r = ((const ExactTop2*)rowres_v)[(size_t)p * kmax + i];
             if (r.j1 < 0) continue;
@@ -626,6 +631,369 @@ int launch_finalize(const void* side1, const void* side2, const float* desc, con
 
 hipEvent_t g_mnn_events[2] = {nullptr, nullptr};  // gtsfm_match_set_kernel_events
 
+// ---------------------------------------------------------------------------------------------
+// Float-descriptor path (GTSFM_MATCH_F16_RERANK, e.g. SuperPoint's 256-D unit vectors). An fp16 MFMA distance GEMM
+// shortlists each keypoint's kFlCand nearest candidates on the other side (approximate keys |b|^2 - 2 a.b, fp32
+// accumulation); fl_rerank_kernel recomputes the shortlist with exact_top2_kernel's arithmetic, in index order, and
+// certifies it: with eps a bound on |approx - exact| squared distance (fp16 rounding of both operands, fp32
+// accumulation and norms), every keypoint outside the shortlist has approx key >= the shortlist's last, so once
+// (last + |a|^2) - eps clears the shortlist's exact second distance by a relative margin no outside keypoint can enter
+// the top 2 or tie it. Rows without the certificate (or on an image with values outside the fp16 range) are rescanned
+// exactly. The (d1, d2, j1) per keypoint, and so the matches, are bit-identical to GTSFM_MATCH_EXACT_F32.
+// ---------------------------------------------------------------------------------------------
+constexpr int kFlCand = 8;
+constexpr int kFlRows = 64;   // train rows per LDS chunk (two 32-row MFMA tiles)
+constexpr int kFlQ = 128;     // queries per workgroup: 4 waves x 32
+constexpr int kFlMaxDim = 256;
+
+__host__ __device__ inline int fl_dpad(int dim) { return dim <= 64 ? 64 : dim <= 128 ? 128 : 256; }
+__host__ __device__ inline int fl_kpad(int kmax) { return (kmax + kFlQ - 1) / kFlQ * kFlQ; }
+
+// One wave per descriptor row: fp16 form (zero-padded to dpad), fp32 squared norm (+inf for padding rows), the
+// image's largest norm and an "unsafe" flag for values fp16 cannot hold within the error bound.
+__global__ __launch_bounds__(256) void fl_prep_kernel(const float* __restrict__ desc, const int* __restrict__ counts,
+                                                      int kmax, int dim, int kpad, int dpad,
+                                                      _Float16* __restrict__ form, float* __restrict__ norm2,
+                                                      unsigned* __restrict__ img_maxnorm, unsigned* __restrict__ img_unsafe) {
+    const int img = blockIdx.y, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int n = counts[img];
+    const bool valid = row < n && row < kmax;
+    const float* d = desc + ((size_t)img * kmax + row) * dim;
+    _Float16* f = form + ((size_t)img * kpad + row) * dpad;
+    float sq = 0.f;
+    bool bad = false;
+    for (int k = lane; k < dpad; k += 64) {
+        const float v = (valid && k < dim) ? d[k] : 0.f;
+        bad |= !(fabsf(v) <= 60000.f);
+        sq = fmaf(v, v, sq);
+        f[k] = (_Float16)v;
+    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) sq += __shfl_xor(sq, m);
+    const bool any_bad = __ballot(bad) != 0ull;
+    if (lane == 0) {
+        norm2[(size_t)img * kpad + row] = valid ? sq : __builtin_inff();
+        if (valid) {
+            atomicMax(&img_maxnorm[img], __float_as_uint(sqrtf(sq)));
+            if (any_bad || !(sq <= 3.0e38f)) atomicOr(&img_unsafe[img], 1u);
+        }
+    }
+}
+
+typedef _Float16 fl_half8 __attribute__((ext_vector_type(8)));
+typedef unsigned fl_u32x4 __attribute__((ext_vector_type(4)));
+typedef float fl_float16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void fl_insert(float x, int j, float (&v)[kFlCand], int (&id)[kFlCand]) {
+    // v sorted ascending and x < v[kFlCand - 1]: branch-free insertion (each slot takes its left neighbour, x or itself)
+#pragma unroll
+    for (int m = kFlCand - 1; m > 0; --m) {
+        const bool sh = x < v[m - 1], here = x < v[m];
+        v[m] = sh ? v[m - 1] : (here ? x : v[m]);
+        id[m] = sh ? id[m - 1] : (here ? j : id[m]);
+    }
+    if (x < v[0]) { v[0] = x; id[0] = j; }
+}
+
+template <int NV, int DP>
+__device__ __forceinline__ void fl_fetch(fl_u32x4 (&pre)[NV], float& pn, const _Float16* __restrict__ tbase,
+                                         const float* __restrict__ nbase, int c0, int tid) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int vid = tid + 256 * k, row = vid / (DP / 8), c8 = vid % (DP / 8);
+        pre[k] = *(const fl_u32x4*)(tbase + (size_t)(c0 + row) * DP + 8 * c8);
+    }
+    if (tid < kFlRows) pn = nbase[c0 + tid];
+}
+
+template <int NV, int DP>
+__device__ __forceinline__ void fl_stash(const fl_u32x4 (&pre)[NV], float pn, _Float16* tl, float* nbl, int buf, int tid) {
+    constexpr int RS = DP + 8;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const int vid = tid + 256 * k, row = vid / (DP / 8), c8 = vid % (DP / 8);
+        *(fl_u32x4*)(tl + buf * kFlRows * RS + row * RS + 8 * c8) = pre[k];
+    }
+    if (tid < kFlRows) nbl[buf * kFlRows + tid] = pn;
+}
+
+// grid (kpad / 128, P, 2 sides). Queries (image pairs[2p + side]) sit on the MFMA's N axis: lane l keeps the
+// shortlist of query l & 31 over the train rows of its half (l >> 5) of every 32-row tile; the halves merge at the end.
+// Train rows stream through LDS in double-buffered 64-row chunks (row stride dpad + 8 halfs: conflict-free b128 reads).
+template <int NS>
+__global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __restrict__ form,
+                                                              const float* __restrict__ norm2,
+                                                              const int* __restrict__ counts,
+                                                              const int* __restrict__ pairs, int n_pairs, int kpad,
+                                                              int kmax, int* __restrict__ cand,
+                                                              float* __restrict__ tkey) {
+    constexpr int DP = NS * 16, RS = DP + 8, NV = DP / 32;  // NV: 16-byte loads per thread per chunk
+    extern __shared__ __attribute__((aligned(16))) unsigned char fl_smem[];
+    _Float16* tl = (_Float16*)fl_smem;                                  // [2][kFlRows * RS]
+    float* nbl = (float*)(fl_smem + 2 * kFlRows * RS * sizeof(_Float16));  // [2][kFlRows]
+    const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 5;
+    const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
+    const int nq = counts[iq], nt = counts[it];
+    const int q0 = blockIdx.x * kFlQ;
+    if (q0 >= nq) return;
+    const int qn = q0 + w * 32 + (l & 31);
+    fl_half8 bq[NS];
+    const _Float16* qrow = form + ((size_t)iq * kpad + qn) * DP + 8 * h;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) bq[s] = *(const fl_half8*)(qrow + 16 * s);
+    float v[kFlCand];
+    int id[kFlCand];
+#pragma unroll
+    for (int c = 0; c < kFlCand; ++c) { v[c] = __builtin_inff(); id[c] = -1; }
+    const _Float16* tbase = form + (size_t)it * kpad * DP;
+    const float* nbase = norm2 + (size_t)it * kpad;
+    fl_u32x4 pre[NV];
+    float pn = 0.f;
+    const int n_chunks = (nt + kFlRows - 1) / kFlRows;
+    if (n_chunks > 0) {
+        fl_fetch<NV, DP>(pre, pn, tbase, nbase, 0, tid);
+        fl_stash<NV, DP>(pre, pn, tl, nbl, 0, tid);
+    }
+    __syncthreads();
+    for (int c = 0; c < n_chunks; ++c) {
+        const int buf = c & 1, c0 = c * kFlRows;
+        if (c + 1 < n_chunks) {
+            fl_fetch<NV, DP>(pre, pn, tbase, nbase, c0 + kFlRows, tid);
+        }
+        const _Float16* tb = tl + buf * kFlRows * RS;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            fl_float16 acc = {};
+            const _Float16* arow = tb + (t * 32 + (l & 31)) * RS + 8 * h;
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const fl_half8*)(arow + 16 * s), bq[s], acc, 0, 0, 0);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float4 nb = *(const float4*)(nbl + buf * kFlRows + t * 32 + 8 * g + 4 * h);
+                const float k0 = fmaf(-2.f, acc[4 * g], nb.x), k1 = fmaf(-2.f, acc[4 * g + 1], nb.y);
+                const float k2 = fmaf(-2.f, acc[4 * g + 2], nb.z), k3 = fmaf(-2.f, acc[4 * g + 3], nb.w);
+                const float kmin = fminf(fminf(k0, k1), fminf(k2, k3));
+                if (__ballot(kmin < v[kFlCand - 1]) == 0ull) continue;
+                const int jb = c0 + t * 32 + 8 * g + 4 * h;
+                if (k0 < v[kFlCand - 1]) fl_insert(k0, jb, v, id);
+                if (k1 < v[kFlCand - 1]) fl_insert(k1, jb + 1, v, id);
+                if (k2 < v[kFlCand - 1]) fl_insert(k2, jb + 2, v, id);
+                if (k3 < v[kFlCand - 1]) fl_insert(k3, jb + 3, v, id);
+            }
+        }
+        if (c + 1 < n_chunks) {
+            fl_stash<NV, DP>(pre, pn, tl, nbl, buf ^ 1, tid);
+        }
+        __syncthreads();
+    }
+    // merge the two halves of each query's shortlist
+#pragma unroll
+    for (int c = 0; c < kFlCand; ++c) {
+        const float pv = __shfl_xor(v[c], 32);
+        const int pj = __shfl_xor(id[c], 32);
+        if (h == 0 && pv < v[kFlCand - 1]) fl_insert(pv, pj, v, id);
+    }
+    if (h == 0 && qn < nq) {
+        const size_t o = ((size_t)side * n_pairs + p) * kmax + qn;
+#pragma unroll
+        for (int c = 0; c < kFlCand; ++c) cand[o * kFlCand + c] = id[c];
+        tkey[o] = v[kFlCand - 1];
+    }
+}
+
+// grid (kpad / 32, P, 2 sides), 256 threads: thread (r, c) = (tid / 8, tid % 8) sums keypoint i0 + r's distance to
+// its c-th shortlisted candidate straight from HBM/L2 (float4 row walks, many loads in flight), sequentially and
+// unfused: exact_top2_kernel's arithmetic. Then one thread per keypoint scans its 8 candidates in index order (the
+// exact scan's b1 / j1 / b2 updates) and checks the certificate; uncertified keypoints go to `redo`.
+constexpr int kFlRerankRows = 256 / kFlCand;
+__global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict__ desc, const int* __restrict__ counts,
+                                                        int kmax, int dim, const int* __restrict__ pairs, int n_pairs,
+                                                        int kpad, const float* __restrict__ norm2,
+                                                        const unsigned* __restrict__ img_maxnorm,
+                                                        const unsigned* __restrict__ img_unsafe,
+                                                        const int* __restrict__ cand, const float* __restrict__ tkey,
+                                                        ExactTop2* __restrict__ rowres, ExactTop2* __restrict__ colres,
+                                                        int* __restrict__ redo_count, int4* __restrict__ redo) {
+#pragma clang fp contract(off)
+    __shared__ float sacc[kFlRerankRows][kFlCand];
+    __shared__ int sj[kFlRerankRows][kFlCand];
+    const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x;
+    const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
+    const int nq = counts[iq], nt = counts[it];
+    const int i0 = blockIdx.x * kFlRerankRows;
+    if (i0 >= nq) return;
+    const int r = tid / kFlCand, c = tid % kFlCand, i = i0 + r;
+    int j = -1;
+    float acc = __builtin_inff();
+    if (i < nq) {
+        j = cand[(((size_t)side * n_pairs + p) * kmax + i) * kFlCand + c];
+        if (j >= nt) j = -1;
+        if (j >= 0) {
+            const float* q = desc + ((size_t)iq * kmax + i) * dim;
+            const float* t = desc + ((size_t)it * kmax + j) * dim;
+            acc = 0.f;
+            if ((dim & 3) == 0) {
+                const float4* q4 = (const float4*)q;
+                const float4* t4 = (const float4*)t;
+#pragma unroll 8
+                for (int k = 0; k < dim / 4; ++k) {
+                    const float4 a = q4[k], b = t4[k];
+                    const float e0 = a.x - b.x, e1 = a.y - b.y, e2 = a.z - b.z, e3 = a.w - b.w;
+                    acc = acc + e0 * e0;  // unfused, in index order: contract(off) above
+                    acc = acc + e1 * e1;
+                    acc = acc + e2 * e2;
+                    acc = acc + e3 * e3;
+                }
+            } else {
+                for (int k = 0; k < dim; ++k) {
+                    const float df = q[k] - t[k];
+                    acc = acc + df * df;
+                }
+            }
+        }
+    }
+    sacc[r][c] = acc;
+    sj[r][c] = j;
+    __syncthreads();
+    if (tid >= kFlRerankRows) return;
+    const int ii = i0 + tid;
+    if (ii >= nq) return;
+    // the shortlist in index order (insertion sort of 8 (j, acc) records; -1 = empty goes last)
+    int js[kFlCand];
+    float as[kFlCand];
+#pragma unroll
+    for (int m = 0; m < kFlCand; ++m) { js[m] = sj[tid][m]; as[m] = sacc[tid][m]; }
+#pragma unroll
+    for (int a = 0; a < kFlCand; ++a)
+#pragma unroll
+        for (int b = 0; b + 1 < kFlCand - a; ++b)
+            if ((unsigned)js[b] > (unsigned)js[b + 1]) {
+                const int x = js[b]; js[b] = js[b + 1]; js[b + 1] = x;
+                const float y = as[b]; as[b] = as[b + 1]; as[b + 1] = y;
+            }
+    float b1 = __builtin_inff(), b2 = __builtin_inff(), a1 = __builtin_inff(), a2 = __builtin_inff();
+    int j1 = -1;
+#pragma unroll
+    for (int m = 0; m < kFlCand; ++m) {
+        if (js[m] < 0) continue;
+        const float d = sqrt_cr(as[m]);
+        if (d < b2) {
+            if (d < b1) { b2 = b1; a2 = a1; b1 = d; a1 = as[m]; j1 = js[m]; }
+            else { b2 = d; a2 = as[m]; }
+        }
+    }
+    bool certified = nt <= kFlCand;
+    if (!certified && img_unsafe[iq] == 0u && img_unsafe[it] == 0u) {
+        const float na = norm2[(size_t)iq * kpad + ii];
+        const float an = sqrtf(na), bn = __uint_as_float(img_maxnorm[it]);
+        const float u = 1.f / 2048.f, eta = 1.f / 33554432.f, D = (float)dim;
+        const float e_dot = (2.f * u + u * u + D * 1.01f / 16777216.f) * an * bn + eta * sqrtf(D) * (an + bn) +
+                            D * eta * eta;
+        const float eps = 1.5f * (2.f * e_dot + (D + 4.f) * 2.f / 16777216.f * (na + bn * bn));
+        certified = (na + tkey[((size_t)side * n_pairs + p) * kmax + ii]) - eps > a2 * (1.f + 1e-4f) + eps;
+    }
+    if (!certified) redo[atomicAdd(redo_count, 1)] = make_int4(side, p, ii, 0);
+    (side ? colres : rowres)[(size_t)p * kmax + ii] = ExactTop2{b1, b2, j1, certified ? 0 : 1};
+}
+
+// Exact rescan of the uncertified keypoints: one 256-thread block per keypoint (block_exact_top2).
+__global__ __launch_bounds__(kFinThreads) void fl_rescan_kernel(const float* __restrict__ desc,
+                                                                const int* __restrict__ counts, int kmax, int dim,
+                                                                const int* __restrict__ pairs,
+                                                                const int* __restrict__ redo_count,
+                                                                const int4* __restrict__ redo,
+                                                                ExactTop2* __restrict__ rowres,
+                                                                ExactTop2* __restrict__ colres) {
+    __shared__ float red_d[2 * kFinThreads];
+    __shared__ int red_j[kFinThreads];
+    const int n = *redo_count;
+    for (int e = blockIdx.x; e < n; e += gridDim.x) {
+        const int4 r = redo[e];
+        const int side = r.x, p = r.y, i = r.z;
+        const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
+        float d1, d2;
+        int j1;
+        block_exact_top2(desc + ((size_t)iq * kmax + i) * dim, desc + (size_t)it * kmax * dim, counts[it], dim, red_d,
+                         red_j, d1, d2, j1);
+        if (threadIdx.x == 0) (side ? colres : rowres)[(size_t)p * kmax + i] = ExactTop2{d1, d2, j1, 1};
+    }
+}
+
+size_t fl_layout(int n_img, int kmax, int dim, int n_pairs, size_t* off) {
+    const int kpad = fl_kpad(kmax), dpad = fl_dpad(dim);
+    size_t o = 0;
+    off[0] = o; o += gtsfm_align_up((size_t)n_img * kpad * dpad * sizeof(_Float16), 256);  // form
+    off[1] = o; o += gtsfm_align_up((size_t)n_img * kpad * sizeof(float), 256);             // norm2
+    off[2] = o; o += gtsfm_align_up((size_t)2 * n_img * sizeof(unsigned), 256);             // maxnorm, unsafe
+    off[3] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * kFlCand * sizeof(int), 256);  // cand
+    off[4] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * sizeof(float), 256);       // tkey
+    off[5] = o; o += gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);       // rowres
+    off[6] = o; o += gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);       // colres
+    off[7] = o; o += 256;                                                                     // redo count
+    off[8] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * sizeof(int4), 256);        // redo list
+    return o;
+}
+
+template <int NS>
+int launch_fl_shortlist(const _Float16* form, const float* norm2, const int* counts, const int* pairs, int n_pairs,
+                        int kpad, int kmax, int* cand, float* tkey, hipStream_t stream) {
+    const size_t lds = 2 * kFlRows * (NS * 16 + 8) * sizeof(_Float16) + 2 * kFlRows * sizeof(float);
+    static bool set = false;
+    if (!set) {
+        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)fl_shortlist_kernel<NS>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        set = true;
+    }
+    hipLaunchKernelGGL(fl_shortlist_kernel<NS>, dim3(kpad / kFlQ, n_pairs, 2), dim3(256), lds, stream, form, norm2,
+                       counts, pairs, n_pairs, kpad, kmax, cand, tkey);
+    return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
+}
+
+int run_fl_match(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim, const int* d_pairs,
+                 int n_pairs, double ratio, unsigned char* ws, uint32_t* d_out_idx, int* d_out_count,
+                 hipStream_t stream) {
+    size_t off[9];
+    fl_layout(n_img, kmax, dim, n_pairs, off);
+    const int kpad = fl_kpad(kmax), dpad = fl_dpad(dim);
+    _Float16* form = (_Float16*)(ws + off[0]);
+    float* norm2 = (float*)(ws + off[1]);
+    unsigned* maxnorm = (unsigned*)(ws + off[2]);
+    unsigned* unsafe = maxnorm + n_img;
+    int* cand = (int*)(ws + off[3]);
+    float* tkey = (float*)(ws + off[4]);
+    ExactTop2* rowres = (ExactTop2*)(ws + off[5]);
+    ExactTop2* colres = (ExactTop2*)(ws + off[6]);
+    int* redo_count = (int*)(ws + off[7]);
+    int4* redo = (int4*)(ws + off[8]);
+    GTSFM_CHECK_HIP(hipMemsetAsync(maxnorm, 0, 2 * (size_t)n_img * sizeof(unsigned), stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(redo_count, 0, sizeof(int), stream));
+    hipLaunchKernelGGL(fl_prep_kernel, dim3(kpad / 4, n_img), dim3(256), 0, stream, d_desc, d_counts, kmax, dim, kpad,
+                       dpad, form, norm2, maxnorm, unsafe);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    int rc;
+    if (g_mnn_events[0]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[0], stream));
+    switch (dpad) {
+        case 64: rc = launch_fl_shortlist<4>(form, norm2, d_counts, d_pairs, n_pairs, kpad, kmax, cand, tkey, stream); break;
+        case 128: rc = launch_fl_shortlist<8>(form, norm2, d_counts, d_pairs, n_pairs, kpad, kmax, cand, tkey, stream); break;
+        default: rc = launch_fl_shortlist<16>(form, norm2, d_counts, d_pairs, n_pairs, kpad, kmax, cand, tkey, stream); break;
+    }
+    if (rc != GTSFM_OK) return rc;
+    if (g_mnn_events[1]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[1], stream));
+    hipLaunchKernelGGL(fl_rerank_kernel, dim3((kmax + kFlRerankRows - 1) / kFlRerankRows, n_pairs, 2), dim3(256), 0,
+                       stream, d_desc, d_counts, kmax, dim, d_pairs, n_pairs, kpad, norm2, maxnorm, unsafe, cand, tkey,
+                       rowres, colres, redo_count, redo);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(fl_rescan_kernel, dim3(2048), dim3(kFinThreads), 0, stream, d_desc, d_counts, kmax, dim,
+                       d_pairs, redo_count, redo, rowres, colres);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    return launch_finalize<kResExact>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, 0, ratio,
+                                      d_out_idx, d_out_count, stream);
+}
+
+
+
 }  // namespace
 
 extern "C" {
@@ -642,6 +1010,10 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
         const size_t forms = 2 * gtsfm_align_up((size_t)n_img * pack_kpad(kmax) * pack_da(dim) * sizeof(_Float16), 256);
         const size_t res = 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(uint2), 256);
         return forms + res;
+    }
+    if (mode == GTSFM_MATCH_F16_RERANK && dim <= kFlMaxDim) {
+        size_t off[9];
+        return fl_layout(n_img, kmax, dim, n_pairs, off);
     }
     return 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
 }
@@ -686,7 +1058,10 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
         return launch_finalize<kResKeys>(colres, rowres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
                                          d_out_idx, d_out_count, stream);
     }
-    if (mode != GTSFM_MATCH_EXACT_F32) return GTSFM_ERR_ARG;
+    if (mode == GTSFM_MATCH_F16_RERANK && dim <= kFlMaxDim)
+        return run_fl_match(d_desc, d_counts, n_img, kmax, dim, d_pairs, n_pairs, ratio, ws, d_out_idx, d_out_count,
+                            stream);
+    if (mode != GTSFM_MATCH_EXACT_F32 && mode != GTSFM_MATCH_F16_RERANK) return GTSFM_ERR_ARG;
     const size_t res_bytes = gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
     ExactTop2* rowres = (ExactTop2*)ws;
     ExactTop2* colres = (ExactTop2*)(ws + res_bytes);

@@ -30,17 +30,20 @@ class MatchingDistanceType(Enum):
 
 
 def select_match_mode(d1: np.ndarray, d2: np.ndarray) -> int:
-    """INT_F16 (MFMA) when every descriptor is an integer in [0, 1023] with |d|^2 < 2^19, else EXACT_F32."""
+    """INT_F16 (exact-integer MFMA) when every descriptor is an integer in [0, 1023] with |d|^2 < 2^19; otherwise
+    F16_RERANK (fp16 MFMA shortlist + certified exact re-rank) up to 256 dims, else EXACT_F32. All three give the
+    same matches."""
     kmax = max(d1.shape[0], d2.shape[0])
+    float_mode = native.GTSFM_MATCH_F16_RERANK if d1.shape[1] <= 256 else native.GTSFM_MATCH_EXACT_F32
     if d1.shape[1] > 139 or kmax > 8192:
-        return native.GTSFM_MATCH_EXACT_F32
+        return float_mode
     for d in (d1, d2):
         if d.size == 0:
             continue
         if d.min() < 0.0 or d.max() > _INT_MAX_VALUE or not np.array_equal(d, np.round(d)):
-            return native.GTSFM_MATCH_EXACT_F32
+            return float_mode
         if float(np.max(np.sum(d.astype(np.float64) ** 2, axis=1))) >= _INT_MAX_NORM_SQ:
-            return native.GTSFM_MATCH_EXACT_F32
+            return float_mode
     return native.GTSFM_MATCH_INT_F16
 
 

@@ -34,6 +34,7 @@ GTSFM_ERR_HIP = -2
 GTSFM_ERR_CAPACITY = -3
 GTSFM_MATCH_EXACT_F32 = 0
 GTSFM_MATCH_INT_F16 = 1
+GTSFM_MATCH_F16_RERANK = 2
 RANSAC_STATUS_OK = 0
 RANSAC_STATUS_TOO_FEW = 1
 RANSAC_STATUS_NO_MODEL = 2

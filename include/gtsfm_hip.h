@@ -56,9 +56,15 @@ const char* gtsfm_hip_target(void);
  *      (every SIFT descriptor). One fp16 MFMA distance GEMM per pair with the norms folded into
  *      extra K columns, fused row/column top-2. Exact integer arithmetic: bit-identical to EXACT_F32.
  *      kmax <= 8192, dim <= 139. (EXACT_F32: kmax <= 65535.)
+ * mode GTSFM_MATCH_F16_RERANK: any float descriptors with dim <= 256 (e.g. SuperPoint's 256-D unit vectors).
+ *      An fp16 MFMA distance GEMM shortlists 4 candidates per keypoint and side, an exact fp32 re-rank with
+ *      EXACT_F32's arithmetic recomputes them, and a rounding-error certificate proves the shortlist holds the
+ *      exact top 2; uncertified keypoints (and images with |value| > 60000 or non-finite values) are rescanned
+ *      exactly. Bit-identical to EXACT_F32. dim > 256 runs the EXACT_F32 kernels. kmax <= 65535.
  * ---------------------------------------------------------------------------------------------- */
 #define GTSFM_MATCH_EXACT_F32 0
 #define GTSFM_MATCH_INT_F16 1
+#define GTSFM_MATCH_F16_RERANK 2
 
 size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, int mode);
 
