@@ -929,7 +929,32 @@ __device__ __attribute__((noinline)) int update_num_iters(double p, double ep, i
     return (denom >= 0 || -num >= max_iters * (-denom)) ? max_iters : (int)llround(num / denom);
 }
 
+// The bound update_num_iters(p, (M - b) / M, 5, n) for every best count b, without the clamp to n: the caller's
+// min(n, T[b]) equals `upd = update_num_iters(..., n); if (upd < n) n = upd` (the clamp test -num >= n * (-denom) and
+// num / denom >= n differ only within rounding of a quotient <= 1000, never across a llround boundary).
+__device__ int num_iters_bound(double p, double ep, int model_points) {
+    p = fmax(p, 0.0); p = fmin(p, 1.0);
+    ep = fmax(ep, 0.0); ep = fmin(ep, 1.0);
+    double num = fmax(1.0 - p, 2.2250738585072014e-308);
+    double denom = 1.0 - pow(1.0 - ep, (double)model_points);
+    if (denom < 2.2250738585072014e-308) return 0;
+    num = log(num);
+    denom = log(denom);
+    if (denom >= 0) return 0x7FFFFFFF;
+    const double q = num / denom;
+    return q >= 1073741824.0 ? 0x7FFFFFFF : (int)llround(q);
+}
+
 // ------------------------------------------------------------------ kernels
+// Per pair, the iteration bound for every best count 0..M (table[p][b]), so the scoring loop needs no logarithms.
+__global__ void ransac_bound_table_kernel(const int* __restrict__ match_count, int mcap, double prob,
+                                          int* __restrict__ table) {
+    const int p = blockIdx.y, b = blockIdx.x * blockDim.x + threadIdx.x;
+    const int M = match_count[p];
+    if (b > M || M < 6) return;
+    table[(size_t)p * (mcap + 1) + b] = b > 0 ? num_iters_bound(prob, (double)(M - b) / M, 5) : 0x7FFFFFFF;
+}
+
 // Gather + normalise the putatives of every pair: x = (uv - (u0, v0)) / f per image (utils/features.py:40-50).
 __global__ void normalize_putatives_kernel(const float* __restrict__ kp_xy, const double* __restrict__ intr, int kmax,
                                            const int* __restrict__ pairs, const uint32_t* __restrict__ match_idx,
@@ -1084,6 +1109,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
                                                                         double thr_px, double prob,
                                                                         const double* __restrict__ cand,
                                                                         const int* __restrict__ nsol, int n_chunks,
+                                                                        const int* __restrict__ bound_tab,
                                                                         PairState* __restrict__ st) {
     extern __shared__ float4 spts[];  // [M]
     __shared__ unsigned long long best_key;
@@ -1171,10 +1197,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
                 best_s = sI;
                 best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
             }
-            if (best > 0) {
-                const int upd = update_num_iters(prob, (double)(M - best) / M, 5, niters);
-                if (upd < niters) niters = upd;
-            }
+            if (best > 0) niters = min(niters, bound_tab[(size_t)p * (mcap + 1) + best]);
             sh_bound[0] = best;
             sh_bound[1] = niters;
         }
@@ -1341,6 +1364,7 @@ static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_p
     o += gtsfm_align_up((size_t)n_pairs * kMaxHyp * sizeof(int), 256);
     *off_stage = o;
     o += gtsfm_align_up((size_t)n_pairs * kStageVals * kMaxHyp * sizeof(double), 256);
+    o += gtsfm_align_up((size_t)n_pairs * (mcap + 1) * sizeof(int), 256);  // bound table (last)
     return o;
 }
 
@@ -1372,6 +1396,9 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     double* cand = (double*)(ws + o_cand);
     int* nsol = (int*)(ws + o_nsol);
     double* stage = (double*)(ws + o_stage);
+    int* bound_tab = (int*)(ws + o_stage + gtsfm_align_up((size_t)n_pairs * kStageVals * kMaxHyp * sizeof(double), 256));
+    hipLaunchKernelGGL(ransac_bound_table_kernel, dim3((mcap + 1 + 255) / 256, n_pairs), dim3(256), 0, stream,
+                       d_match_count, mcap, prob, bound_tab);
     hipLaunchKernelGGL(normalize_putatives_kernel, dim3((mcap + 255) / 256, n_pairs), dim3(256), 0, stream, d_kp_xy,
                        d_intrinsics, kmax, d_pairs, d_match_idx, d_match_count, mcap, x1n, x2n, pts);
     hipLaunchKernelGGL(ransac_init_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, stream, st, n_pairs, max_iters);
@@ -1404,7 +1431,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs, g), dim3(64), kRootLds, stream, d_match_count, st,
                            stage, cand, nsol);
         hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream, d_pairs,
-                           d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, st);
+                           d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask};
