@@ -12,6 +12,10 @@ grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work consta
 cut into one contiguous block per rank, images dealt round-robin for extraction.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--images n] [--kpts 2048] [--no-cpu-baseline]
+
+--config c3-match: configs[2]'s matcher on SURVEY.md §8(d)'s synthetic descriptors -- 200 images x 4096 SuperPoint-like
+256-D unit vectors (30 % of each image's rows planted from a shared latent set), all 19900 pairs through the fp16 MFMA
+shortlist + certified exact re-rank (GTSFM_MATCH_F16_RERANK) with the ratio test; value = matched image-pairs/s.
 """
 import argparse
 import json
@@ -149,6 +153,106 @@ def cpu_baseline(scene, kpts: int, threads: int = 16, n_sift: int = 16, n_pairs:
                       f"({t_pair * 1e3:.0f} ms/pair wall), scaled to {n_img} images / {P} pairs"}
 
 
+def c3_descriptors(n_img: int, k: int, d: int, dev) -> torch.Tensor:
+    """SuperPoint-like unit descriptors with planted matches (seeded; SURVEY.md 8(d) matcher microbench)."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    latent = torch.nn.functional.normalize(torch.randn(k, d, device=dev, generator=g), dim=1)
+    desc = torch.nn.functional.normalize(torch.randn(n_img, k, d, device=dev, generator=g), dim=2)
+    m = int(0.3 * k)
+    for i in range(n_img):
+        rows = torch.randperm(k, device=dev, generator=g)[:m]
+        src = torch.randperm(k, device=dev, generator=g)[:m]
+        noise = 0.15 / d ** 0.5 * torch.randn(m, d, device=dev, generator=g)
+        desc[i, rows] = torch.nn.functional.normalize(latent[src] + noise, dim=1)
+    return desc.contiguous()
+
+
+def c3_cpu_baseline(desc: torch.Tensor, threads: int = 16, n_pairs: int = 16) -> dict:
+    """Oracle TwoWayMatcher restatement (oracle/twoway.c) on `threads` host threads over n_pairs pairs."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle
+
+    h = desc[: n_pairs + 1].cpu().numpy()
+    pairs = [(0, j) for j in range(1, n_pairs + 1)]
+    with ThreadPoolExecutor(threads) as pool:
+        t0 = time.time()
+        list(pool.map(lambda p: oracle.twoway_match(h[p[0]], h[p[1]], RATIO), pairs))
+        dt = time.time() - t0
+    return {"value": len(pairs) / dt, "unit": "matched image-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"oracle twoway_match (oracle/twoway.c, {threads} threads), {len(pairs)} pairs of "
+                      f"{h.shape[1]}x{h.shape[2]} descriptors, {dt:.1f} s wall"}
+
+
+def main_c3(args, world, rank, dev):
+    """configs[2] matcher: all pairs of 200 x 4096 x 256-D float descriptors, F16_RERANK + ratio 0.8."""
+    n_img, k, d = args.images or 200, args.kpts if args.kpts != 2048 else 4096, 256
+    desc = c3_descriptors(n_img, k, d, dev)
+    cnt = torch.full((n_img,), k, dtype=torch.int32, device=dev)
+    all_pairs = sharding.all_pairs(n_img)
+    mine = all_pairs[sharding.rank_pairs(all_pairs, world, rank)]
+    pairs = torch.from_numpy(mine.astype(np.int32)).to(dev)
+    mode = native.GTSFM_MATCH_F16_RERANK
+
+    def step():
+        return hip.match_pairs(desc, cnt, pairs, RATIO, mode)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        _, m = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_pairs = len(all_pairs)
+    # shortlist GEMM kernel timed on the call's stream (median of 3)
+    lib = native.lib()
+    kms = []
+    for _ in range(3):
+        kev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        for e in kev:
+            e.record()
+        native.check(lib.gtsfm_match_set_kernel_events(kev[0].cuda_event, kev[1].cuda_event), "set_kernel_events")
+        step()
+        torch.cuda.synchronize()
+        native.check(lib.gtsfm_match_set_kernel_events(None, None), "set_kernel_events")
+        kms.append(kev[0].elapsed_time(kev[1]))
+    kernel_ms = float(np.median(kms))
+    flops = 2 * 2.0 * k * k * d * len(mine)
+    tf = flops / (kernel_ms * 1e-3) / 1e12
+    out = {
+        "metric": "matched image-pairs/sec (all-pairs SuperPoint-descriptor matching, configs[2])",
+        "value": round(total_pairs / (elapsed / args.steps), 2), "unit": "image-pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak" if world > 1 else "strong", "vs_baseline": None,
+        "dtype": "fp16 MFMA shortlist / fp32 exact re-rank", "data": "synthetic (seeded unit Gaussian, 30% planted)",
+        "config": {"workload": f"C3 matcher: {n_img} images x {k} x {d}-D float descriptors, all {total_pairs} "
+                               f"pairs, mutual NN + ratio {RATIO}", "images": n_img, "pairs": total_pairs, "kpts": k,
+                   "parallelism": f"pair blocks x{world}"},
+        "mean_matches": round(float(m.float().mean().item()), 1),
+        "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None,
+                     "kernel": "fl_shortlist_kernel<16> (one launch per step)", "kernel_ms": round(kernel_ms, 3),
+                     "work": "2 sides x 2*K1*K2*D flop per pair"},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = c3_cpu_baseline(desc)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -159,6 +263,7 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--kpts", type=int, default=2048)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default="c2", choices=["c2", "c3-match"])
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,6 +274,8 @@ def main():
     if world > 1:
         torch.distributed.init_process_group("nccl", device_id=dev)
     native.lib()
+    if args.config == "c3-match":
+        return main_c3(args, world, rank, dev)
     n_img = args.images or images_for(world)
 
     # every rank renders the same seeded scene but keeps only its own images resident
