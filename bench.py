@@ -99,7 +99,7 @@ class FrontEnd:
 
 def pmc_traffic():
     """HBM bytes per mnn_mfma_kernel launch from the committed rocprofv3 --pmc summary of this bench's command
-    (profiles/*_mnn_pmc.json, written by tools_pmc_summary.py --json): FETCH_SIZE doubled per MI355X_MICROARCH.md
+    (profiles/*_mnn_pmc.json, written by tools/pmc_summary.py --json): FETCH_SIZE doubled per MI355X_MICROARCH.md
     (gfx950 tallies 128-B reads at 64 B) + WRITE_SIZE, in bytes. None when no summary is committed."""
     import glob
 

@@ -1,7 +1,7 @@
-"""Builds gtsfm_amd/_lib/prof/libgtsfm_hip.so: ransac.hip with phase timers (s_memtime) for tools_ransac_phases.py.
+"""Builds gtsfm_amd/_lib/prof/libgtsfm_hip.so: ransac.hip with phase timers (s_memtime) for tools/ransac_phases.py.
 Not part of the product; the instrumented copy lives in /tmp."""
 import os, subprocess
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 s = open(os.path.join(REPO, "gtsfm_amd/csrc/ransac.hip")).read()
 anchors = [  # (text that starts a line, mark id) -- mark k times the code since the previous mark
     ("    if (!nullspace_5x9(x1, x2, m, N)) return 0;", 0),

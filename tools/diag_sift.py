@@ -1,7 +1,7 @@
 """Diagnostic: SIFT run-to-run and batch-composition determinism on the bench scene (valid rows only)."""
 import os, sys
 import numpy as np, torch
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 from gtsfm_amd import device as hip, synthetic
 n = 100

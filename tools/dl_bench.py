@@ -7,7 +7,9 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "tests"))
+_REPO = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+sys.path.insert(0, _REPO)
+sys.path.insert(0, __import__("os").path.join(_REPO, "tests"))
 from gtsfm_amd import device, native, synthetic  # noqa: E402
 from gtsfm_amd.frontend.detector_descriptor.superpoint import pack_superpoint_weights  # noqa: E402
 from gtsfm_amd.frontend.matcher.superglue_matcher import pack_superglue_weights  # noqa: E402

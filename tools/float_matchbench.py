@@ -8,7 +8,7 @@ import time
 import numpy as np
 import torch
 
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 from gtsfm_amd import device, native  # noqa: E402
 

@@ -11,7 +11,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA
   name=$(echo $grp | cut -d' ' -f1)
   (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/pmc_${TAG}_$name -o run -- python $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc_${TAG}_$name.log 2>&1)
   rc=$?; echo "pmc $name rc=$rc"; [ $rc -eq 0 ] || { tail -5 $R/gpurun_out/pmc_${TAG}_$name.log; exit $rc; }
-  python $R/tools_pmc_summary.py $R/gpurun_out/pmc_${TAG}_$name > $R/gpurun_out/pmc_${TAG}_$name.txt
+  python $R/tools/pmc_summary.py $R/gpurun_out/pmc_${TAG}_$name > $R/gpurun_out/pmc_${TAG}_$name.txt
   dirs="$dirs $R/gpurun_out/pmc_${TAG}_$name"
 done
-python $R/tools_pmc_summary.py --json $R/gpurun_out/${TAG}_mnn_pmc.json --kernel mnn_mfma_kernel $dirs && rm -rf $dirs
+python $R/tools/pmc_summary.py --json $R/gpurun_out/${TAG}_mnn_pmc.json --kernel mnn_mfma_kernel $dirs && rm -rf $dirs

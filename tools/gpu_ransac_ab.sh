@@ -11,4 +11,4 @@ rc=$?; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_rab.err; exit $rc; }
 python -c "import json; d=json.load(open('gpurun_out/bench_rab.json')); print('value', d['value'], 'ms', d['ms_per_step'], 'isp', d['pairs_passing_isp'], 'stage', d['stage_ms'])"
 cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_rab -o run -- python $GRAFT_REPO_ROOT/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_rab.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
-python $GRAFT_REPO_ROOT/tools_kstats.py $GRAFT_REPO_ROOT/gpurun_out/prof_rab/run_kernel_stats.csv > $GRAFT_REPO_ROOT/gpurun_out/kstats_rab.txt; head -12 $GRAFT_REPO_ROOT/gpurun_out/kstats_rab.txt
+python $GRAFT_REPO_ROOT/tools/kstats.py $GRAFT_REPO_ROOT/gpurun_out/prof_rab/run_kernel_stats.csv > $GRAFT_REPO_ROOT/gpurun_out/kstats_rab.txt; head -12 $GRAFT_REPO_ROOT/gpurun_out/kstats_rab.txt

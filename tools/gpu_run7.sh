@@ -10,4 +10,4 @@ timeout -k 10 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpuru
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_full.log | cut -c1-200; grep -o '"stage_ms[^}]*}' gpurun_out/bench_full.log
 [ $rc -eq 0 ] || exit $rc
 [ -n "$2" ] || exit 0
-./gpu_prof.sh $2
+bash tools/gpu_prof.sh $2

@@ -1,7 +1,7 @@
 """Temporary matcher-stage microbench (superseded by bench.py)."""
 import sys, time, json
 import numpy as np, torch
-import os; sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import os; sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gtsfm_amd import device, native
 n_img = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 K = 2048

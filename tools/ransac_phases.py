@@ -1,7 +1,7 @@
 """Phase timing of ransac_solve_kernel (instrumented build in gtsfm_amd/_lib/prof, not the product)."""
 import ctypes, os, sys, time
 import numpy as np, torch
-REPO = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 from gtsfm_amd import native
 native.LIB_PATH = os.path.join(REPO, "gtsfm_amd", "_lib", "prof", "libgtsfm_hip.so")
