@@ -132,11 +132,23 @@ def run_two_view_estimator_as_futures(
     """
     verifier = two_view_estimator._verifier
     gt = list(gt_cameras) if gt_cameras is not None else [None] * len(keypoints_list)
+    # a TwoViewEstimatorCacher answers hits from disk; only the misses go through the batched verifier
+    cached = getattr(two_view_estimator, "cache_lookup", None)
+    results: Dict[Tuple[int, int], TWO_VIEW_OUTPUT] = {}
+    if cached is not None:
+        for (i1, i2), m in putative_corr_idxs_dict.items():
+            hit = cached(keypoints_list[i1], keypoints_list[i2], m)
+            if hit is not None:
+                results[(i1, i2)] = hit
+    todo = {k: m for k, m in putative_corr_idxs_dict.items() if k not in results}
     if hasattr(verifier, "verify_batch"):
-        verified = verifier.verify_batch(keypoints_list, putative_corr_idxs_dict, camera_intrinsics)
+        verified = verifier.verify_batch(keypoints_list, todo, camera_intrinsics)
     else:
         verified = {(i1, i2): verifier.verify(keypoints_list[i1], keypoints_list[i2], m, camera_intrinsics[i1],
                                               camera_intrinsics[i2])
-                    for (i1, i2), m in putative_corr_idxs_dict.items()}
-    return {(i1, i2): two_view_estimator._finish(verified[(i1, i2)], gt[i1], gt[i2])
-            for (i1, i2) in putative_corr_idxs_dict}
+                    for (i1, i2), m in todo.items()}
+    for (i1, i2), m in todo.items():
+        results[(i1, i2)] = two_view_estimator._finish(verified[(i1, i2)], gt[i1], gt[i2])
+        if cached is not None:
+            two_view_estimator.cache_store(keypoints_list[i1], keypoints_list[i2], m, results[(i1, i2)])
+    return {k: results[k] for k in putative_corr_idxs_dict}
