@@ -352,6 +352,12 @@ def main():
             "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
             "kernel": "mnn_mfma_kernel (one launch per step)", "kernel_ms": round(mnn_ms, 3),
             "work": "2*K1*K2*128 flop per pair, summed over the launch's pairs (GFLOP: %.1f)" % (match_flops / 1e9)}
+    if traffic:
+        # FETCH_SIZE counts L2 -> fabric requests, Infinity Cache hits included (MI355X_MICROARCH.md, HBM section)
+        roof["traffic_note"] = ("L2-miss bytes, Infinity-Cache hits included: the A operand (image i2) of each pair is "
+                                "re-read past the 4 MiB XCD L2, from a %.0f MB operand set that fits the 256 MiB "
+                                "Infinity Cache; %.2f TB/s at kernel_ms, not the bound"
+                                % (2 * n_rows * kpad * 144 * 2 / 1e6, traffic[0] / (mnn_ms * 1e-3) / 1e12))
 
     out = {
         "metric": "verified image-pairs/sec (all-pairs front-end), N images @ 2048 kpts/img",
