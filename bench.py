@@ -1,21 +1,28 @@
 #!/usr/bin/env python
 """bench.py — verified image-pairs/sec of the all-pairs two-view front-end on MI355X (BASELINE.json `metric`).
 
-One step = the whole front-end over one synthetic scene already resident in HBM:
-    SIFT (2048 kpts/img) on this rank's images -> [N>1: one all-gather of keypoints+descriptors over RCCL]
-    -> mutual-NN + ratio matching of this rank's pairs (fp16 MFMA distance GEMM) -> 5-point RANSAC + LO +
-    recoverPose of the same pairs -> inlier-support filter (>= 15 inliers, ratio >= 0.1), all on device.
-value = all pairs pushed through match + verify (every rank) / max-over-ranks step time.
+One step = SURVEY.md §8(d)'s unit: this rank's images in (pinned) host memory -> per-pair (R, t, v_corr, inlier
+count) in host memory. Inside the step (gtsfm_amd/frontend/all_pairs.py):
+    H2D of the images in chunks on a copy stream, overlapped with SIFT (2048 kpts/img) of the previous chunk
+    -> [N>1: one all-gather of keypoints + descriptors over RCCL] -> mutual-NN + ratio matching of this rank's pairs
+    (fp16 MFMA distance GEMM) -> 5-point RANSAC + LO + recoverPose -> compaction of the verified rows + the
+    inlier-support filter (>= 15 inliers, ratio >= 0.1) -> D2H of the compact results.
+value = all pairs pushed through match + verify (every rank) / max-over-ranks step time. The same steps with the
+images already in HBM and the results left there are reported as `value_device_resident`.
 
-Workload (configs[1] of BASELINE.json): 100 rendered 1920x1080 images, all 4950 pairs, at N=1. For N GPUs the scene
-grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work constant: "scaling": "weak"); pairs are
-cut into one contiguous block per rank, images dealt round-robin for extraction.
+Workloads:
+  --config c2 (default; configs[1] of BASELINE.json): 100 rendered 1920x1080 images, all 4950 pairs, at N=1. For
+      N GPUs the scene grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work constant:
+      "scaling": "weak").
+  --config c4 (configs[3]): 1000 rendered 1080p images, all 499,500 pairs, split over the N ranks ("strong").
+  --config c3-match: configs[2]'s matcher on SURVEY.md §8(d)'s synthetic descriptors -- 200 images x 4096
+      SuperPoint-like 256-D unit vectors, all 19900 pairs through the fp16 MFMA shortlist + certified exact re-rank.
+Pairs are cut into one contiguous block per rank, images dealt round-robin for extraction.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--images n] [--kpts 2048] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c3-match] [--images n] [--no-cpu-baseline]
 
---config c3-match: configs[2]'s matcher on SURVEY.md §8(d)'s synthetic descriptors -- 200 images x 4096 SuperPoint-like
-256-D unit vectors (30 % of each image's rows planted from a shared latent set), all 19900 pairs through the fp16 MFMA
-shortlist + certified exact re-rank (GTSFM_MATCH_F16_RERANK) with the ratio test; value = matched image-pairs/s.
+--gpus N > 1 without a launcher starts N fresh rank processes first (gtsfm_amd/launch.py), before anything touches
+a GPU; under `torch.distributed.run` the ranks come from the environment.
 """
 import argparse
 import json
@@ -29,12 +36,13 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from gtsfm_amd import device as hip  # noqa: E402
-from gtsfm_amd import native, synthetic  # noqa: E402
-from gtsfm_amd.frontend import sharding  # noqa: E402
+from gtsfm_amd import launch  # noqa: E402
+
+# everything that may touch the GPU is imported lazily, after the launcher has run (see main)
 
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16, MI355X_MICROARCH.md
-HBM_PEAK_GBS = 8000.0
+HBM_PEAK_GBS = 8000.0  # HBM3E spec, MI355X_MICROARCH.md
+VALU_F32_PEAK_TFLOPS = 157.3  # vector fp32, MI355X_MICROARCH.md (SURVEY.md §8(d) grades RANSAC against it)
 RATIO = 0.8
 THRESH_PX = 4.0
 MIN_INLIERS = 15
@@ -47,54 +55,6 @@ def images_for(n_gpus: int, base: int = 100) -> int:
     while n * (n - 1) // 2 < target:
         n += 1
     return n
-
-
-class FrontEnd:
-    """Device-resident all-pairs front-end for one rank."""
-
-    def __init__(self, scene_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, kpts: int, rank: int,
-                 world: int):
-        self.rank, self.world, self.kpts, self.n_img = rank, world, kpts, n_img
-        self.dev = scene_images.device
-        self.n_per = sharding.images_per_rank(n_img, world)
-        self.local_images = scene_images  # (n_local, H, W, 3): images rank, rank + world, ...
-        slot = sharding.global_slots(n_img, world)  # rank-major rows after the all-gather
-        pairs = sharding.all_pairs(n_img)
-        self.total_pairs = len(pairs)
-        block = sharding.rank_pairs(pairs, world, rank)
-        self.pair_id_base = int(block[0]) if len(block) else 0  # global pair index keys the RANSAC sampler
-        mine = pairs[block]
-        self.my_pairs_orig = mine
-        self.pairs = torch.from_numpy(slot[mine].astype(np.int32)).to(self.dev)
-        intr = np.zeros((world * self.n_per, 3))
-        intr[slot] = intrinsics
-        self.intr = torch.from_numpy(intr).to(self.dev)
-        self.sift_ws = None
-
-    def step(self, events=None):
-        ev = events or {}
-        if "t0" in ev:
-            ev["t0"].record()
-        feats = hip.sift_extract(self.local_images, self.kpts)
-        if "t1" in ev:
-            ev["t1"].record()
-        # the one exchange step (N > 1): padded feature blocks, rank-major
-        xy_all, desc_all, cnt_all = sharding.allgather_features((feats.xy, feats.desc, feats.count), self.n_per)
-        if "t2" in ev:
-            ev["t2"].record()
-        idx, mcnt = hip.match_pairs(desc_all, cnt_all, self.pairs, RATIO, native.GTSFM_MATCH_INT_F16)
-        if "t3" in ev:
-            ev["t3"].record()
-        res = hip.ransac_essential(xy_all, self.intr, self.pairs, idx, mcnt, THRESH_PX,
-                                   pair_id_base=self.pair_id_base)
-        if "t4" in ev:
-            ev["t4"].record()
-        # inlier-support processor (frontend/inlier_support_processor.py:73-87), on device
-        m = mcnt.clamp(min=1).to(torch.float64)
-        ratio = res.n_inliers.to(torch.float64) / m
-        ok = (res.status == native.RANSAC_STATUS_OK) & (ratio >= MIN_INLIER_RATIO) & (res.n_inliers >= MIN_INLIERS)
-        n_ok = ok.sum()
-        return n_ok, (feats, idx, mcnt, res)
 
 
 def pmc_traffic():
@@ -111,17 +71,17 @@ def pmc_traffic():
     return float(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
 
 
-def cpu_baseline(scene, kpts: int, threads: int = 16, n_sift: int = 16, n_pairs: int = 64) -> dict:
+def cpu_baseline(images, K: np.ndarray, n_img: int, kpts: int, threads: int = 16, n_sift: int = 16,
+                 n_pairs: int = 64) -> dict:
     """Oracle restatement (oracle/*.c through ctypes, which drops the GIL) timed on `threads` host threads -- the
     box's CPU share for one GPU -- over a bounded sample: SIFT of n_sift images, then match + verify of n_pairs pairs
-    among them, each stage wall-clocked across the thread pool and scaled to the full workload."""
+    among them, each stage wall-clocked across the thread pool and scaled to n_img images / all their pairs."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle
 
-    n_sift = min(n_sift, scene.images.shape[0])
-    imgs = scene.images[:n_sift].cpu().numpy()
-    K = scene.K
+    n_sift = min(n_sift, images.shape[0])
+    imgs = np.asarray(images[:n_sift])
     rng = np.random.default_rng(0)
     oracle.ransac_E(rng.normal(size=(8, 2)), rng.normal(size=(8, 2)), 1e-3)  # one-time solver tables, untimed
     pairs = [(i1, i2) for i1 in range(n_sift) for i2 in range(i1 + 1, n_sift)][:n_pairs]
@@ -144,7 +104,6 @@ def cpu_baseline(scene, kpts: int, threads: int = 16, n_sift: int = 16, n_pairs:
         t0 = time.time()
         list(pool.map(pair_one, pairs))
         t_pair = (time.time() - t0) / len(pairs)
-    n_img = scene.images.shape[0]
     P = n_img * (n_img - 1) // 2
     total = n_img * t_sift + P * t_pair
     return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port",
@@ -186,6 +145,10 @@ def c3_cpu_baseline(desc: torch.Tensor, threads: int = 16, n_pairs: int = 16) ->
 
 def main_c3(args, world, rank, dev):
     """configs[2] matcher: all pairs of 200 x 4096 x 256-D float descriptors, F16_RERANK + ratio 0.8."""
+    from gtsfm_amd import device as hip
+    from gtsfm_amd import native
+    from gtsfm_amd.frontend import sharding
+
     n_img, k, d = args.images or 200, args.kpts if args.kpts != 2048 else 4096, 256
     desc = c3_descriptors(n_img, k, d, dev)
     cnt = torch.full((n_img,), k, dtype=torch.int32, device=dev)
@@ -249,116 +212,144 @@ def main_c3(args, world, rank, dev):
         out["cpu_baseline"] = c3_cpu_baseline(desc)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--images", type=int, default=0)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--kpts", type=int, default=2048)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--config", default="c2", choices=["c2", "c3-match"])
-    args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
-    native.lib()
-    if args.config == "c3-match":
-        return main_c3(args, world, rank, dev)
-    n_img = args.images or images_for(world)
 
-    # every rank renders the same seeded scene but keeps only its own images resident
-    scene = synthetic.render_scene(n_img, args.height, args.width, device=str(dev))
-    local = scene.images[rank::world].contiguous()
-    fe = FrontEnd(local, scene.intrinsics, n_img, args.kpts, rank, world)
-    if rank != 0 or world > 1 or args.no_cpu_baseline:
-        keep_for_cpu = None
-    else:
-        keep_for_cpu = scene
-    del scene
-    torch.cuda.empty_cache()
-
-    for _ in range(args.warmup):
-        fe.step()
+def timed_steps(fe, steps: int, resident: bool, world: int, dev) -> float:
+    """Seconds for `steps` steps: barrier + synchronize on both sides, max over ranks."""
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    n_ok = None
-    for _ in range(args.steps):
-        n_ok, _ = fe.step()
+    for _ in range(steps):
+        fe.step(resident=resident)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    ok = n_ok.to(torch.float64).reshape(1)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
-        torch.distributed.all_reduce(ok, op=torch.distributed.ReduceOp.SUM)
-    elapsed = float(el.item())
+    return float(el.item())
+
+
+def sift_bytes_per_image(H: int, W: int, kpts: int) -> float:
+    """SURVEY.md §8(d) algorithmic bytes of SIFT extraction per image: 84 * sum_o P_o + H*W + K*(128*4 + 16), with
+    sum_o P_o = 4HW * 4/3 (21 fp32 image passes per pyramid pixel over the 2x-upsampled octave pyramid)."""
+    return 84.0 * (4.0 * H * W * 4.0 / 3.0) + H * W + kpts * (128 * 4 + 16)
+
+
+def main_frontend(args, info, config: str):
+    """configs[1] (C2, weak scaling) / configs[3] (C4, strong scaling): the SIFT all-pairs front-end."""
+    from gtsfm_amd import native, synthetic
+    from gtsfm_amd.frontend import sharding
+    from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig
+
+    rank, world, dev = info.rank, info.world, info.device
+    native.lib()
+    if config == "c4":
+        n_img, scaling = args.images or 1000, "strong"
+    else:
+        n_img, scaling = args.images or images_for(world), "weak"
+    H, W, kpts = args.height, args.width, args.kpts
+    mine = sharding.local_images(n_img, world, rank)
+    # every rank renders (seeded, identical cameras) only the images it extracts; rendering is data generation
+    scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine)
+    host_images = scene.images.cpu().pin_memory()
+    del scene.images
+    torch.cuda.empty_cache()
+    cfg = FrontEndConfig(kpts=kpts, ratio=RATIO, thresh_px=THRESH_PX, min_inliers=MIN_INLIERS,
+                         min_inlier_ratio=MIN_INLIER_RATIO)
+    if args.extract_chunk:
+        cfg.extract_chunk = args.extract_chunk
+    if args.pair_chunk:
+        cfg.pair_chunk = args.pair_chunk
+    fe = AllPairsFrontEnd(host_images, scene.intrinsics, n_img, rank, world, dev, cfg)
+
+    for _ in range(args.warmup):
+        res = fe.step()
+    elapsed = timed_steps(fe, args.steps, False, world, dev)
+    elapsed_res = timed_steps(fe, args.steps, True, world, dev)
     ms_per_step = elapsed / args.steps * 1e3
     value = fe.total_pairs / (elapsed / args.steps)
 
-    # stage split + roofline of the dominant kernel. HIP events on the stream the kernels run on (torch's current
-    # stream): stage events from Python, the distance-GEMM kernel's own pair through gtsfm_match_set_kernel_events.
-    names = ["t0", "t1", "t2", "t3", "t4"]
-    stage_ms = {"extract": [], "allgather": [], "match": [], "verify": []}
-    kernel_ms = []
+    # instrumented steps: per-phase HIP events on the compute / copy streams; the distance-GEMM kernel's own events
+    # through gtsfm_match_set_kernel_events (one pair chunk per launch at C2)
     lib = native.lib()
-    for _ in range(5):
-        evs = {k: torch.cuda.Event(enable_timing=True) for k in names}
+    stage_host, stage_res, kernel_ms = [], [], []
+    fe.instrument = True
+    for _ in range(3):
+        res = fe.step(resident=False)
+        torch.cuda.synchronize()
+        stage_host.append(fe.stage_ms())
         kev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         for e in kev:
-            e.record()  # creates the hipEvent_t handle
+            e.record()  # creates the hipEvent_t handles
         native.check(lib.gtsfm_match_set_kernel_events(kev[0].cuda_event, kev[1].cuda_event), "set_kernel_events")
-        _, (feats, idx, mcnt, res) = fe.step(evs)
+        fe.step(resident=True)
         torch.cuda.synchronize()
         native.check(lib.gtsfm_match_set_kernel_events(None, None), "set_kernel_events")
+        stage_res.append(fe.stage_ms())
         kernel_ms.append(kev[0].elapsed_time(kev[1]))
-        stage_ms["extract"].append(evs["t0"].elapsed_time(evs["t1"]))
-        stage_ms["allgather"].append(evs["t1"].elapsed_time(evs["t2"]))
-        stage_ms["match"].append(evs["t2"].elapsed_time(evs["t3"]))
-        stage_ms["verify"].append(evs["t3"].elapsed_time(evs["t4"]))
-    # medians over the instrumented steps (a single step can catch a clock or paging transient)
-    stage = {k: float(np.median(v)) for k, v in stage_ms.items()}
+    fe.instrument = False
+
+    def med(rows):
+        keys = sorted(set().union(*[r.keys() for r in rows]))
+        return {k: round(float(np.median([r.get(k, 0.0) for r in rows])), 3) for k in keys}
+
+    st_host, st_res = med(stage_host), med(stage_res)
+    n_ok = torch.tensor([float(res.isp_ok.sum())], dtype=torch.float64, device=dev)
+    n_inl_rows = torch.tensor([float(len(res.v_corr))], dtype=torch.float64, device=dev)
+    # per-stage algorithmic work of this rank
+    kc = np.zeros(n_img)
+    kc[mine] = res.kp_count
+    stats = {k: v.double() for k, v in fe.stats.items()}
+    if world > 1:
+        t = torch.from_numpy(kc).to(dev)
+        torch.distributed.all_reduce(t)
+        kc = t.cpu().numpy()
+    pr = fe.my_pairs
+    match_flop = float((2.0 * kc[pr[:, 0]] * kc[pr[:, 1]] * 128).sum())
+    H_p, M_p, S_p = stats["n_hyp"], stats["n_matches"], stats["n_models"]
+    verify_flop = float((1.2e4 * H_p + 36.0 * M_p * S_p).sum().item())
+    extract_bytes = fe.n_local * sift_bytes_per_image(H, W, kpts)
     mnn_ms = float(np.median(kernel_ms))
-    counts = feats.count
-    (counts_all,) = sharding.allgather_features((counts,), fe.n_per)
-    c = counts_all.to(torch.float64)
-    pairs = fe.pairs.long()
-    match_flops = float((2.0 * c[pairs[:, 0]] * c[pairs[:, 1]] * 128).sum().item())
-    match_tflops = match_flops / (mnn_ms * 1e-3) / 1e12
-    # algorithmic bytes of the launch: both fp16 operand forms of every image once + the per-keypoint top-2 records
-    kpad = -(-args.kpts // 256) * 256
+    if world > 1:
+        torch.distributed.all_reduce(n_ok)
+        torch.distributed.all_reduce(n_inl_rows)
+    match_tf = match_flop / (mnn_ms * 1e-3) / 1e12
+    ex_ms, ver_ms = st_res.get("extract", float("nan")), st_res.get("verify", float("nan"))
+    extract_gbs = extract_bytes / (ex_ms * 1e-3) / 1e9
+    verify_tf = verify_flop / (ver_ms * 1e-3) / 1e12
+    kpad = -(-kpts // 256) * 256
     n_rows = world * fe.n_per
-    algo_bytes = 2 * n_rows * kpad * 144 * 2 + 2 * len(pairs) * args.kpts * 8
+    algo_bytes = 2 * n_rows * kpad * 144 * 2 + 2 * fe.P * kpts * 8
     traffic = pmc_traffic()
-    roof = {"bound": "mfma", "achieved": round(match_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(match_tflops / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
+    roof = {"bound": "mfma", "achieved": round(match_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(match_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
             "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
-            "kernel": "mnn_mfma_kernel (one launch per step)", "kernel_ms": round(mnn_ms, 3),
-            "work": "2*K1*K2*128 flop per pair, summed over the launch's pairs (GFLOP: %.1f)" % (match_flops / 1e9)}
+            "kernel": "mnn_mfma_kernel (one launch per pair chunk)", "kernel_ms": round(mnn_ms, 3),
+            "work": "2*K1*K2*128 flop per pair, summed over the launch's pairs (GFLOP: %.1f)" % (match_flop / 1e9)}
+    roof["stages"] = {
+        "extract": {"bound": "hbm", "achieved": round(extract_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(extract_gbs / HBM_PEAK_GBS, 4), "ms": ex_ms,
+                    "work": "SURVEY 8(d): 84*sum_o P_o + H*W + K*528 B/image = %.3f GB x %d images"
+                            % (sift_bytes_per_image(H, W, kpts) / 1e9, fe.n_local)},
+        "match": {"bound": "mfma", "achieved": round(match_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                  "frac": round(match_tf / MFMA_F16_PEAK_TFLOPS, 4), "ms": round(mnn_ms, 3),
+                  "work": "2*K1*K2*128 flop per pair (distance GEMM counted once)"},
+        "verify": {"bound": "valu", "achieved": round(verify_tf, 2), "peak": VALU_F32_PEAK_TFLOPS,
+                   "unit": "TFLOP/s", "frac": round(verify_tf / VALU_F32_PEAK_TFLOPS, 4), "ms": ver_ms,
+                   "work": "SURVEY 8(d): sum_p H_p*1.2e4 + 36*M_p*(models scored)_p; H mean %.1f, models/H %.2f"
+                           % (float(H_p.mean()), float(S_p.sum() / max(float(H_p.sum()), 1.0)))},
+    }
     if traffic:
-        # FETCH_SIZE counts L2 -> fabric requests, Infinity Cache hits included (MI355X_MICROARCH.md, HBM section)
         roof["traffic_note"] = ("L2-miss bytes, Infinity-Cache hits included: the A operand (image i2) of each pair is "
                                 "re-read past the 4 MiB XCD L2, from a %.0f MB operand set that fits the 256 MiB "
-                                "Infinity Cache; %.2f TB/s at kernel_ms, not the bound"
-                                % (2 * n_rows * kpad * 144 * 2 / 1e6, traffic[0] / (mnn_ms * 1e-3) / 1e12))
-
+                                "Infinity Cache" % (2 * n_rows * kpad * 144 * 2 / 1e6))
+    wl = "C4" if config == "c4" else "C2"
     out = {
         "metric": "verified image-pairs/sec (all-pairs front-end), N images @ 2048 kpts/img",
         "value": round(value, 2),
@@ -368,24 +359,65 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8 image / fp32 pyramid / fp16-MFMA exact-int distances / fp64 RANSAC solver",
         "data": "synthetic (rendered textured room, seeds 0/1/2)",
-        "config": {"workload": f"C2: {n_img} synthetic {args.width}x{args.height} images, all "
-                               f"{fe.total_pairs} pairs, SIFT {args.kpts} kpts/img, ratio {RATIO}, "
-                               f"5-pt RANSAC {THRESH_PX}px", "images": n_img, "pairs": fe.total_pairs,
-                   "kpts": args.kpts, "parallelism": f"pair blocks x{world}"},
-        "pairs_passing_isp": int(ok.item()),
-        "stage_ms": {k: round(v, 3) for k, v in stage.items()},
+        "config": {"workload": f"{wl}: {n_img} synthetic {W}x{H} images, all {fe.total_pairs} pairs, SIFT {kpts} "
+                               f"kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px, host images -> host results",
+                   "images": n_img, "pairs": fe.total_pairs, "kpts": kpts, "parallelism": f"pair blocks x{world}",
+                   "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1},
+        "value_device_resident": round(fe.total_pairs / (elapsed_res / args.steps), 2),
+        "ms_per_step_device_resident": round(elapsed_res / args.steps * 1e3, 3),
+        "pairs_passing_isp": int(n_ok.item()),
+        "verified_rows": int(n_inl_rows.item()),
+        "stage_ms": st_host,
+        "stage_ms_device_resident": st_res,
         "roofline": roof,
     }
-    if keep_for_cpu is not None:
-        out["cpu_baseline"] = cpu_baseline(keep_for_cpu, args.kpts)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(host_images, scene.K, n_img, kpts)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--images", type=int, default=0)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--kpts", type=int, default=2048)
+    ap.add_argument("--extract-chunk", type=int, default=0)
+    ap.add_argument("--pair-chunk", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c3-match"])
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")
+    args = ap.parse_args()
+
+    if args.gpus > 1 and launch.launched_world() == 1:
+        # no launcher: start the ranks now, before this process touches a GPU, and exit with their status
+        sys.exit(launch.spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if args.launch_probe:
+        info = launch.init_rank("gloo")
+        print(json.dumps({"rank": info.rank, "world": info.world, "dist_world": torch.distributed.get_world_size()
+                          if torch.distributed.is_initialized() else 1}), flush=True)
+        launch.finish_rank(info)
+        return
+    if launch.launched_world() != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {launch.launched_world()} ranks; "
+              "using the launcher's world size", file=sys.stderr)
+    info = launch.init_rank("nccl")
+    try:
+        if args.config == "c3-match":
+            main_c3(args, info.world, info.rank, info.device)
+        else:
+            main_frontend(args, info, args.config)
+    finally:
+        launch.finish_rank(info)
 
 
 if __name__ == "__main__":

@@ -3,7 +3,8 @@
 
 extern "C" {
 
-int gtsfm_hip_abi_version(void) { return 101; }
+// 2.00: gtsfm_ransac_E_batched gained d_n_models; gtsfm_compact_verified added
+int gtsfm_hip_abi_version(void) { return 200; }
 
 const char* gtsfm_hip_target(void) { return "gfx950"; }
 

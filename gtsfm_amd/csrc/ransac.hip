@@ -987,11 +987,12 @@ struct RansacOutputs {
     int* status;     // [P]: 0 ok, 1 too few putatives (M < 6), 2 no model
     int* n_hyp;      // [P] (may be null)
     uint8_t* mask;   // [P][mcap]
+    int* n_models;   // [P] (may be null): candidate models scored (real 5-point solutions of the scored samples)
 };
 
 struct PairState {
     int best, best_h, best_s, done;
-    int niters, pad0, pad1, pad2;
+    int niters, n_models, pad1, pad2;
     double bestE[9];
     double pad3;
 };
@@ -1120,6 +1121,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
     if (M < 6) return;
     // thread 0 updates the pair state after each chunk; the others follow best / niters / done
     int best = st[p].best, best_h = st[p].best_h, best_s = st[p].best_s, done = st[p].done, niters = st[p].niters;
+    int n_models = st[p].n_models;
     if (done >= niters) return;
     const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
     const double fx = fmax(intr[3 * i1], intr[3 * i2]);  // opencv_verifier_base.py:86
@@ -1198,6 +1200,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
                 best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
             }
             if (best > 0) niters = min(niters, bound_tab[(size_t)p * (mcap + 1) + best]);
+            n_models += total;
             sh_bound[0] = best;
             sh_bound[1] = niters;
         }
@@ -1213,6 +1216,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
         o.best_s = best_s;
         o.done = done;
         o.niters = niters;
+        o.n_models = n_models;
         if (best_off >= 0)
             for (int e = 0; e < 9; ++e) o.bestE[e] = cand[best_off + e];
     }
@@ -1236,6 +1240,7 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
             out.n_inliers[p] = 0;
             out.status[p] = 1;
             if (out.n_hyp) out.n_hyp[p] = 0;
+            if (out.n_models) out.n_models[p] = 0;
         }
         for (int i = lane; i < M; i += 64) mask[i] = 0;
         return;
@@ -1246,6 +1251,7 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
             out.n_inliers[p] = 0;
             out.status[p] = 2;
             if (out.n_hyp) out.n_hyp[p] = ps.done;
+            if (out.n_models) out.n_models[p] = ps.n_models;
         }
         for (int i = lane; i < M; i += 64) mask[i] = 0;
         return;
@@ -1340,6 +1346,7 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
         out.n_inliers[p] = cur;
         out.status[p] = 0;
         if (out.n_hyp) out.n_hyp[p] = done;
+        if (out.n_models) out.n_models[p] = ps.n_models;
     }
 }
 
@@ -1378,7 +1385,8 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
                            double thr_px, double prob, int max_iters, uint64_t seed, int pair_id_base,
                            const int* d_pair_ids, void* d_workspace, size_t workspace_bytes, double* d_E, double* d_R, double* d_t,
-                           int* d_n_inliers, int* d_status, int* d_n_hyp, uint8_t* d_inlier_mask, void* stream_v) {
+                           int* d_n_inliers, int* d_status, int* d_n_hyp, int* d_n_models, uint8_t* d_inlier_mask,
+                           void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
     if (n_pairs == 0) return GTSFM_OK;
     if (!d_kp_xy || !d_intrinsics || !d_pairs || !d_match_idx || !d_match_count || !d_E || !d_R || !d_t ||
@@ -1434,7 +1442,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
-    const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask};
+    const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask, d_n_models};
     hipLaunchKernelGGL(ransac_refine_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics, d_match_count,
                        mcap, x1n, x2n, pts, thr_px, o, st);
     GTSFM_CHECK_HIP(hipGetLastError());

@@ -57,11 +57,13 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
 
 
 class RansacResult:
-    """Per-pair verifier outputs (device tensors): E, R (i2Ri1), t (i2ti1), n_inliers, status, n_hyp, mask."""
+    """Per-pair verifier outputs (device tensors): E, R (i2Ri1), t (i2ti1), n_inliers, status, n_hyp, mask, and
+    n_models (candidate models scored; E path only, else None)."""
 
-    def __init__(self, E, R, t, n_inliers, status, n_hyp, mask):
+    def __init__(self, E, R, t, n_inliers, status, n_hyp, mask, n_models=None):
         self.E, self.R, self.t = E, R, t
         self.n_inliers, self.status, self.n_hyp, self.mask = n_inliers, status, n_hyp, mask
+        self.n_models = n_models
 
 
 def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
@@ -90,6 +92,7 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
     n_inl = torch.zeros((max(P, 1),), dtype=torch.int32, device=dev)
     status = torch.zeros_like(n_inl)
     n_hyp = torch.zeros_like(n_inl)
+    n_models = torch.zeros_like(n_inl)
     mask = torch.zeros((max(P, 1), max(mcap, 1)), dtype=torch.uint8, device=dev)
     if P > 0:
         ws = _workspace(L.gtsfm_ransac_workspace_bytes(P, mcap), dev)
@@ -98,10 +101,36 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
         rc = L.gtsfm_ransac_E_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
                                       _ptr(match_count), mcap, float(thr_px), float(prob), int(max_iters), int(seed),
                                       int(pair_id_base), _ptr(pair_ids), _ptr(ws), ws.numel(), _ptr(E), _ptr(R), _ptr(t),
-                                      _ptr(n_inl), _ptr(status), _ptr(n_hyp), _ptr(mask),
+                                      _ptr(n_inl), _ptr(status), _ptr(n_hyp), _ptr(n_models), _ptr(mask),
                                       native.stream_handle(stream))
         native.check(rc, "gtsfm_ransac_E_batched")
-    return RansacResult(E[:P], R[:P], t[:P], n_inl[:P], status[:P], n_hyp[:P], mask[:P])
+    return RansacResult(E[:P], R[:P], t[:P], n_inl[:P], status[:P], n_hyp[:P], mask[:P], n_models[:P])
+
+
+def compact_verified(match_idx: torch.Tensor, match_count: torch.Tensor, res: "RansacResult", min_inliers: int,
+                     min_inlier_ratio: float, capacity: int, out_offsets: Optional[torch.Tensor] = None,
+                     out_v_corr: Optional[torch.Tensor] = None, out_isp_ok: Optional[torch.Tensor] = None,
+                     stream: Optional[torch.cuda.Stream] = None
+                     ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Inlier rows of every pair, concatenated in pair order, + the inlier-support verdict (gtsfm_compact_verified).
+
+    Returns offsets (P + 1,) int32, v_corr (capacity, 2) int32 holding uint32 indices (rows offsets[p] ..
+    offsets[p + 1] belong to pair p, matcher order), isp_ok (P,) uint8.
+    """
+    assert match_idx.dtype == torch.int32 and match_idx.is_contiguous() and match_idx.dim() == 3
+    P, mcap = match_idx.shape[0], match_idx.shape[1]
+    assert res.mask.shape[0] == P and (P == 0 or res.mask.shape[1] == mcap) and res.mask.is_contiguous()
+    dev = match_idx.device
+    offsets = out_offsets if out_offsets is not None else torch.empty(P + 1, dtype=torch.int32, device=dev)
+    v_corr = out_v_corr if out_v_corr is not None else torch.empty((max(capacity, 1), 2), dtype=torch.int32, device=dev)
+    isp_ok = out_isp_ok if out_isp_ok is not None else torch.empty(max(P, 1), dtype=torch.uint8, device=dev)
+    assert offsets.numel() >= P + 1 and v_corr.shape[0] >= capacity and isp_ok.numel() >= P
+    rc = native.lib().gtsfm_compact_verified(_ptr(match_idx), _ptr(match_count), mcap, _ptr(res.mask),
+                                             _ptr(res.status), _ptr(res.n_inliers), P, int(min_inliers),
+                                             float(min_inlier_ratio), _ptr(offsets), _ptr(v_corr), int(capacity),
+                                             _ptr(isp_ok), native.stream_handle(stream))
+    native.check(rc, "gtsfm_compact_verified")
+    return offsets, v_corr, isp_ok
 
 
 class FundamentalResult(RansacResult):

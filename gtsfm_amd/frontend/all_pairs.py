@@ -1,0 +1,292 @@
+"""All-pairs two-view front-end of one rank: images in host memory -> per-pair (R, t, v_corr, inlier count) in host
+memory, the unit SURVEY.md §8(d) times.
+
+This is the batched engine behind the drop-ins: it replaces the reference's Dask fan-out of
+`DetDescCorrespondenceGenerator.generate_correspondences` (det_desc_correspondence_generator.py:31-87: one
+detect_and_describe task per image, one match task per pair) followed by `run_two_view_estimator_as_futures`
+(two_view_estimator.py:531-587: one verify + inlier-support task per pair), with on-device batches:
+
+1. H2D + extraction, pipelined: the rank's images go up from pinned host memory in chunks on a copy stream while
+   SIFT runs on the previous chunk (`kernels.sift`, one batched launch sequence per chunk).
+2. The one exchange (N > 1): all-gather of the padded per-rank feature blocks (gtsfm_amd/frontend/sharding.py).
+3. Per block of pairs: mutual-NN + ratio matching (`kernels.match`), 5-point RANSAC + LO + recoverPose
+   (`kernels.verify`), then compaction of the verified rows + the inlier-support verdict (`kernels.compact`).
+4. D2H of the compact results into pinned host buffers: fixed-size per-pair records first, then exactly the verified
+   rows once their total is known.
+
+The kernels come from an object (default `HipKernels`: libgtsfm_hip.so). The control flow, the sharding and the
+buffers do not depend on it, so tests drive this same class under gloo on CPU with the oracle standing in for the
+device (tests/test_launcher.py). The product path has no CPU fallback: `HipKernels` fails when the library or the GPU
+is missing.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from gtsfm_amd.frontend import sharding
+
+
+@dataclass
+class FrontEndConfig:
+    kpts: int = 2048                 # SIFT max_keypoints (BASELINE configs C2 / C4)
+    ratio: float = 0.8               # TwoWayMatcher ratio_test_threshold (sift_front_end.yaml)
+    thresh_px: float = 4.0           # Ransac estimation_threshold_px (sift_front_end.yaml:48)
+    min_inliers: int = 15            # InlierSupportProcessor min_num_inliers_est_model
+    min_inlier_ratio: float = 0.1    # InlierSupportProcessor min_inlier_ratio_est_model
+    extract_chunk: int = 25          # images per SIFT launch sequence (the next chunk's H2D overlaps it)
+    pair_chunk: int = 32768          # pairs per match / verify / compact launch sequence
+
+
+class HipKernels:
+    """The product kernels: libgtsfm_hip.so through gtsfm_amd.device (no fallback)."""
+
+    def __init__(self):
+        from gtsfm_amd import device, native
+
+        native.require_gpu()
+        native.lib()
+        self._dev, self._native = device, native
+
+    def sift_workspace_bytes(self, n: int, H: int, W: int, kpts: int) -> int:
+        return int(self._native.lib().gtsfm_sift_workspace_bytes(n, H, W, kpts))
+
+    def sift(self, images, kpts, out, workspace):
+        self._dev.sift_extract(images, kpts, out=out, workspace=workspace)
+
+    def match(self, desc, counts, pairs, ratio):
+        return self._dev.match_pairs(desc, counts, pairs, ratio, self._native.GTSFM_MATCH_INT_F16)
+
+    def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_id_base):
+        return self._dev.ransac_essential(xy, intr, pairs, idx, cnt, thresh_px, pair_id_base=pair_id_base)
+
+    def compact(self, idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets, out_v_corr, out_isp_ok):
+        self._dev.compact_verified(idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets=out_offsets,
+                                   out_v_corr=out_v_corr, out_isp_ok=out_isp_ok)
+
+
+class Features:
+    """Per-image extraction outputs of one rank (device tensors): xy (n,k,2), attr (n,k,3), desc (n,k,128),
+    count (n,), n_detected (n,). Same fields as gtsfm_amd.device.SiftResult."""
+
+    def __init__(self, xy, attr, desc, count, n_detected):
+        self.xy, self.attr, self.desc, self.count, self.n_detected = xy, attr, desc, count, n_detected
+
+    def rows(self, a: int, b: int) -> "Features":
+        return Features(self.xy[a:b], self.attr[a:b], self.desc[a:b], self.count[a:b], self.n_detected[a:b])
+
+
+@dataclass
+class HostResults:
+    """Per-pair results of one rank in host memory (numpy views of pinned buffers, valid until the next step).
+
+    pairs[p] = (i1, i2) original image indices; R[p] = i2Ri1, t[p] = unit i2ti1; status[p] 0 ok / 1 too few
+    putatives / 2 no model; n_inliers[p]; n_matches[p] = putatives; isp_ok[p] = passes the inlier-support filter;
+    v_corr[offsets[p]:offsets[p+1]] = pair p's verified (i1 kp, i2 kp) rows in matcher order (uint32).
+    kp_xy / kp_count: this rank's keypoints (local image order, sharding.local_images).
+    """
+    pairs: np.ndarray
+    R: np.ndarray
+    t: np.ndarray
+    status: np.ndarray
+    n_inliers: np.ndarray
+    n_matches: np.ndarray
+    isp_ok: np.ndarray
+    offsets: np.ndarray
+    v_corr: np.ndarray
+    kp_xy: np.ndarray
+    kp_count: np.ndarray
+
+    def verified(self, p: int) -> np.ndarray:
+        return self.v_corr[self.offsets[p]: self.offsets[p + 1]]
+
+
+class AllPairsFrontEnd:
+    """One rank's share of the all-pairs front-end (images i with i % world == rank, one contiguous pair block)."""
+
+    def __init__(self, host_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, rank: int, world: int,
+                 device: torch.device, cfg: Optional[FrontEndConfig] = None, kernels=None):
+        self.cfg = cfg or FrontEndConfig()
+        self.kern = kernels if kernels is not None else HipKernels()
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.rank, self.world, self.n_img = rank, world, n_img
+        assert host_images.dtype == torch.uint8 and host_images.device.type == "cpu" and host_images.dim() in (3, 4)
+        n_local = host_images.shape[0]
+        if n_local != len(sharding.local_images(n_img, world, rank)):
+            raise ValueError(f"rank {rank} holds {n_local} images, expected {len(sharding.local_images(n_img, world, rank))}")
+        H, W = host_images.shape[1], host_images.shape[2]
+        k = self.cfg.kpts
+        self.n_local = n_local
+        self.host_images = host_images.contiguous()
+        if self.cuda and not self.host_images.is_pinned():
+            self.host_images = self.host_images.pin_memory()
+        self.dev_images = torch.empty_like(self.host_images, device=self.dev)
+        self.n_per = sharding.images_per_rank(n_img, world)
+        z = dict(device=self.dev)
+        self.feats = Features(torch.zeros((n_local, k, 2), dtype=torch.float32, **z),
+                              torch.zeros((n_local, k, 3), dtype=torch.float32, **z),
+                              torch.zeros((n_local, k, 128), dtype=torch.float32, **z),
+                              torch.zeros((n_local,), dtype=torch.int32, **z),
+                              torch.zeros((n_local,), dtype=torch.int32, **z))
+        ch = max(1, self.cfg.extract_chunk)
+        self.chunks = [(a, min(a + ch, n_local)) for a in range(0, n_local, ch)]
+        ws = self.kern.sift_workspace_bytes(min(ch, max(n_local, 1)), H, W, k) if n_local else 0
+        self.sift_ws = torch.empty(max(int(ws), 256), dtype=torch.uint8, **z)
+
+        slot = sharding.global_slots(n_img, world)
+        pairs = sharding.all_pairs(n_img)
+        self.total_pairs = len(pairs)
+        block = sharding.rank_pairs(pairs, world, rank)
+        self.pair_id_base = int(block[0]) if len(block) else 0  # global pair index keys the RANSAC sampler
+        self.my_pairs = pairs[block]
+        P = len(block)
+        self.P = P
+        self.pairs_dev = torch.from_numpy(slot[self.my_pairs].astype(np.int32)).to(self.dev)
+        intr = np.zeros((world * self.n_per, 3))
+        intr[slot] = intrinsics
+        self.intr = torch.from_numpy(intr).to(self.dev)
+        pc = max(1, self.cfg.pair_chunk)
+        self.pchunks = [(a, min(a + pc, P)) for a in range(0, P, pc)]
+
+        # compact results on the device: per chunk c, offsets rows [a + c, b + c] and verified rows from a * k
+        nc = len(self.pchunks)
+        self.d_offsets = torch.zeros(P + nc, dtype=torch.int32, **z)
+        self.d_v_corr = torch.zeros((max(P * k, 1), 2), dtype=torch.int32, **z)
+        self.d_isp_ok = torch.zeros(max(P, 1), dtype=torch.uint8, **z)
+        self.d_fixed = torch.zeros((max(P, 1), 12), dtype=torch.float64, **z)  # R (9) | t (3)
+        self.d_ints = torch.zeros((max(P, 1), 3), dtype=torch.int32, **z)      # status | n_inliers | n_matches
+        self.stats: Dict[str, torch.Tensor] = {}
+
+        pin = dict(pin_memory=self.cuda)
+        self.h_offsets = torch.zeros(P + nc, dtype=torch.int32, **pin)
+        self.h_v_corr = torch.zeros((max(P * k, 1), 2), dtype=torch.int32, **pin)
+        self.h_isp_ok = torch.zeros(max(P, 1), dtype=torch.uint8, **pin)
+        self.h_fixed = torch.zeros((max(P, 1), 12), dtype=torch.float64, **pin)
+        self.h_ints = torch.zeros((max(P, 1), 3), dtype=torch.int32, **pin)
+        self.h_xy = torch.zeros((n_local, k, 2), dtype=torch.float32, **pin)
+        self.h_count = torch.zeros((n_local,), dtype=torch.int32, **pin)
+
+        if self.cuda:
+            self.copy_stream = torch.cuda.Stream(device=self.dev)
+            self.copy_done = [torch.cuda.Event() for _ in self.chunks]
+        self.instrument = False
+        self.marks: List[Tuple[str, object]] = []
+        self.copy_marks: List[Tuple[str, object]] = []
+
+    # -- instrumentation: HIP events on the stream each phase runs on (no-ops unless self.instrument) --
+    def _mark(self, name: str, stream=None):
+        if not (self.instrument and self.cuda):
+            return
+        ev = torch.cuda.Event(enable_timing=True)
+        if stream is None:
+            ev.record()
+            self.marks.append((name, ev))
+        else:
+            ev.record(stream)
+            self.copy_marks.append((name, ev))
+
+    def stage_ms(self) -> Dict[str, float]:
+        """Per-phase milliseconds of the last instrumented step (call after synchronising)."""
+        out: Dict[str, float] = {}
+        for (_, e0), (name, e1) in zip(self.marks[:-1], self.marks[1:]):
+            out[name] = out.get(name, 0.0) + e0.elapsed_time(e1)
+        if len(self.copy_marks) >= 2:
+            out["h2d"] = self.copy_marks[0][1].elapsed_time(self.copy_marks[-1][1])
+        return out
+
+    def _extract(self, resident: bool):
+        k = self.cfg.kpts
+        cs = torch.cuda.current_stream(self.dev) if self.cuda else None
+        if self.cuda and not resident:
+            self.copy_stream.wait_stream(cs)  # the previous step's extraction has finished reading dev_images
+            self._mark("h2d_start", self.copy_stream)
+        for c, (a, b) in enumerate(self.chunks):
+            if not resident:
+                if self.cuda:
+                    with torch.cuda.stream(self.copy_stream):
+                        self.dev_images[a:b].copy_(self.host_images[a:b], non_blocking=True)
+                        self.copy_done[c].record(self.copy_stream)
+                    cs.wait_event(self.copy_done[c])
+                else:
+                    self.dev_images[a:b].copy_(self.host_images[a:b])
+            self.kern.sift(self.dev_images[a:b], k, self.feats.rows(a, b), self.sift_ws)
+        if self.cuda and not resident:
+            self._mark("h2d_end", self.copy_stream)
+
+    def step(self, resident: bool = False) -> Optional[HostResults]:
+        """One pass of the front-end over this rank's share.
+
+        resident=False (the contracted unit): H2D of the images from pinned host memory, ..., D2H of the results;
+        returns HostResults. resident=True: the images already sit in HBM from an earlier step and the results stay
+        there (returns None) -- the device-resident figure, reported beside the contracted one.
+        """
+        cfg, k = self.cfg, self.cfg.kpts
+        self.marks, self.copy_marks = [], []
+        self._mark("start")
+        self._extract(resident)
+        self._mark("extract")
+        xy_all, desc_all, cnt_all = sharding.allgather_features((self.feats.xy, self.feats.desc, self.feats.count),
+                                                                self.n_per)
+        self._mark("allgather")
+        n_hyp, n_models, n_match = [], [], []
+        for c, (a, b) in enumerate(self.pchunks):
+            pairs = self.pairs_dev[a:b]
+            idx, mcnt = self.kern.match(desc_all, cnt_all, pairs, cfg.ratio)
+            self._mark("match")
+            res = self.kern.verify(xy_all, self.intr, pairs, idx, mcnt, cfg.thresh_px, self.pair_id_base + a)
+            self._mark("verify")
+            self.kern.compact(idx, mcnt, res, cfg.min_inliers, cfg.min_inlier_ratio, (b - a) * k,
+                              self.d_offsets[a + c: b + c + 1], self.d_v_corr[a * k: b * k], self.d_isp_ok[a:b])
+            self.d_fixed[a:b, :9] = res.R.reshape(-1, 9)
+            self.d_fixed[a:b, 9:] = res.t
+            self.d_ints[a:b, 0] = res.status
+            self.d_ints[a:b, 1] = res.n_inliers
+            self.d_ints[a:b, 2] = mcnt
+            self._mark("compact")
+            n_hyp.append(res.n_hyp)
+            if res.n_models is not None:
+                n_models.append(res.n_models)
+            n_match.append(mcnt)
+        if self.P:
+            self.stats = {"n_hyp": torch.cat(n_hyp), "n_matches": torch.cat(n_match)}
+            if n_models:
+                self.stats["n_models"] = torch.cat(n_models)
+        if resident:
+            return None
+        return self._to_host()
+
+    def _to_host(self) -> HostResults:
+        k = self.cfg.kpts
+        P, nc = self.P, len(self.pchunks)
+        nb = dict(non_blocking=self.cuda)
+        self.h_fixed.copy_(self.d_fixed, **nb)
+        self.h_ints.copy_(self.d_ints, **nb)
+        self.h_isp_ok.copy_(self.d_isp_ok, **nb)
+        self.h_offsets.copy_(self.d_offsets, **nb)
+        self.h_xy.copy_(self.feats.xy, **nb)
+        self.h_count.copy_(self.feats.count, **nb)
+        self._mark("d2h")
+        if self.cuda:
+            torch.cuda.current_stream(self.dev).synchronize()
+        off = self.h_offsets.numpy()
+        glob = np.zeros(P + 1, dtype=np.int64)
+        pos = 0
+        for c, (a, b) in enumerate(self.pchunks):
+            n = int(off[b + c])
+            if n:
+                self.h_v_corr[pos: pos + n].copy_(self.d_v_corr[a * k: a * k + n], **nb)
+            glob[a: b + 1] = pos + off[a + c: b + c + 1]
+            pos += n
+        self._mark("d2h")
+        if self.cuda:
+            torch.cuda.current_stream(self.dev).synchronize()
+        fixed = self.h_fixed.numpy()[:P]
+        ints = self.h_ints.numpy()[:P]
+        return HostResults(pairs=self.my_pairs, R=fixed[:, :9].reshape(P, 3, 3), t=fixed[:, 9:], status=ints[:, 0],
+                           n_inliers=ints[:, 1], n_matches=ints[:, 2], isp_ok=self.h_isp_ok.numpy()[:P].astype(bool),
+                           offsets=glob, v_corr=self.h_v_corr.numpy()[:pos].view(np.uint32),
+                           kp_xy=self.h_xy.numpy(), kp_count=self.h_count.numpy())

@@ -56,7 +56,7 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_int,
          c_uint64, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-         c_void_p],
+         c_void_p, c_void_p],
     ),
     "gtsfm_ransac_F_workspace_bytes": (c_size_t, [c_int, c_int]),
     "gtsfm_ransac_F_batched": (
@@ -78,6 +78,11 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
          c_float, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p],
+    ),
+    "gtsfm_compact_verified": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_int,
+         c_void_p, c_void_p],
     ),
     "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gtsfm_sift_batched": (

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import List, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -24,8 +24,8 @@ class SyntheticScene:
 
     @property
     def intrinsics(self) -> np.ndarray:
-        """(N, 3) float64 rows (f, u0, v0) for the verifier."""
-        n = self.images.shape[0]
+        """(N, 3) float64 rows (f, u0, v0) for the verifier, one per camera of the scene."""
+        n = self.wRc.shape[0]
         return np.tile(np.array([self.K[0, 0], self.K[0, 2], self.K[1, 2]]), (n, 1))
 
     def relative_pose(self, i1: int, i2: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -89,8 +89,11 @@ def _room_planes() -> List[Tuple]:
 
 def render_scene(n_images: int = 100, height: int = 1080, width: int = 1920, seed_scene: int = 0,
                  seed_cameras: int = 1, seed_texture: int = 2, device: str = "cuda",
-                 tex_size: int = 2048) -> SyntheticScene:
+                 tex_size: int = 2048, indices: Optional[Sequence[int]] = None) -> SyntheticScene:
+    """Renders the scene's cameras `indices` (default: all n_images); `images` holds them in that order, while K,
+    wRc and wtc always describe all n_images cameras (a rank renders only the images it extracts)."""
     dev = torch.device(device)
+    indices = list(range(n_images)) if indices is None else [int(i) for i in indices]
     tex = make_texture(tex_size, seed_texture, "cpu").to(dev)[None, None]
     rng_s = np.random.default_rng(seed_scene)
     planes = _room_planes()
@@ -117,8 +120,8 @@ def render_scene(n_images: int = 100, height: int = 1080, width: int = 1920, see
     ys, xs = torch.meshgrid(torch.arange(height, device=dev, dtype=torch.float32) + 0.5,
                             torch.arange(width, device=dev, dtype=torch.float32) + 0.5, indexing="ij")
     rays_c = torch.stack([(xs - K[0, 2]) / f, (ys - K[1, 2]) / f, torch.ones_like(xs)], -1)  # (H, W, 3)
-    images = torch.empty((n_images, height, width, 3), dtype=torch.uint8, device=dev)
-    for i in range(n_images):
+    images = torch.empty((len(indices), height, width, 3), dtype=torch.uint8, device=dev)
+    for slot, i in enumerate(indices):
         R = torch.tensor(wRc[i], dtype=torch.float32, device=dev)
         o = torch.tensor(wtc[i], dtype=torch.float32, device=dev)
         d = rays_c @ R.T  # world directions
@@ -143,7 +146,7 @@ def render_scene(n_images: int = 100, height: int = 1080, width: int = 1920, see
             val = torch.where(ok, samp * shade, val)
             best_t = torch.where(ok, t, best_t)
         img = val.clamp(0, 255).round().to(torch.uint8)
-        images[i] = torch.stack([img, (img.float() * 0.95).round().to(torch.uint8), img], -1)
+        images[slot] = torch.stack([img, (img.float() * 0.95).round().to(torch.uint8), img], -1)
     return SyntheticScene(images=images, K=K, wRc=wRc, wtc=wtc)
 
 

@@ -57,7 +57,7 @@ const char* gtsfm_hip_target(void);
  *      extra K columns, fused row/column top-2. Exact integer arithmetic: bit-identical to EXACT_F32.
  *      kmax <= 8192, dim <= 139. (EXACT_F32: kmax <= 65535.)
  * mode GTSFM_MATCH_F16_RERANK: any float descriptors with dim <= 256 (e.g. SuperPoint's 256-D unit vectors).
- *      An fp16 MFMA distance GEMM shortlists 4 candidates per keypoint and side, an exact fp32 re-rank with
+ *      An fp16 MFMA distance GEMM shortlists 8 candidates per keypoint and side, an exact fp32 re-rank with
  *      EXACT_F32's arithmetic recomputes them, and a rounding-error certificate proves the shortlist holds the
  *      exact top 2; uncertified keypoints (and images with |value| > 60000 or non-finite values) are rescanned
  *      exactly. Bit-identical to EXACT_F32. dim > 256 runs the EXACT_F32 kernels. kmax <= 65535.
@@ -87,8 +87,10 @@ int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop);
  * (checked per batch of 64); `seed` and the pair id key the deterministic sampling of pair p: d_pair_ids[p]
  * when d_pair_ids is non-NULL (e.g. all 0 to reproduce one-pair calls), else pair_id_base + p.
  * Outputs per pair: E, R (i2Ri1) row-major 3x3, unit t (i2ti1), inlier count, status (0 ok, 1 fewer than
- * 6 putatives, 2 no model), number of hypotheses evaluated (d_n_hyp may be NULL) and the inlier mask
- * d_inlier_mask[n_pairs][mcap] over the putatives in matcher order.
+ * 6 putatives, 2 no model), number of hypotheses evaluated (d_n_hyp may be NULL), number of candidate models scored
+ * (the real 5-point solutions of those hypotheses; d_n_models may be NULL; a measurement output with no reference
+ * counterpart, it prices the RANSAC FLOP count of SURVEY.md §8(d)) and the inlier mask d_inlier_mask[n_pairs][mcap]
+ * over the putatives in matcher order.
  * ---------------------------------------------------------------------------------------------- */
 size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap);
 
@@ -97,7 +99,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            const int* d_match_count, int mcap, double thr_px, double prob, int max_iters,
                            uint64_t seed, int pair_id_base, const int* d_pair_ids, void* d_workspace,
                            size_t workspace_bytes, double* d_E, double* d_R, double* d_t, int* d_n_inliers, int* d_status,
-                           int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
+                           int* d_n_hyp, int* d_n_models, uint8_t* d_inlier_mask, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
  * Verifier, fundamental-matrix path (use_intrinsics_in_verification=False). Replaces Ransac.estimate_F
@@ -116,6 +118,22 @@ int gtsfm_ransac_F_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            uint64_t seed, int pair_id_base, const int* d_pair_ids, void* d_workspace,
                            size_t workspace_bytes, double* d_F, double* d_E, double* d_R, double* d_t,
                            int* d_n_inliers, int* d_status, int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
+
+/* ----------------------------------------------------------------------------------------------
+ * Verified-correspondence compaction + inlier-support filter (the device half of the hand-off to the host).
+ * Replaces, for every pair at once: v_corr_idxs = match_indices[mask == 1] and inlier_ratio = mean(mask)
+ * (gtsfm/frontend/verifier/opencv_verifier_base.py:98-101) and InlierSupportProcessor.run_inlier_support
+ * (gtsfm/frontend/inlier_support_processor.py:73-87: fail iff ratio < min_inlier_ratio or 0 < n < min_inliers).
+ * Inputs are the matcher's d_match_idx[n_pairs][mcap][2] / d_match_count and the verifier's mask, status and inlier
+ * counts. Outputs: d_offsets[n_pairs + 1] (exclusive scan of the rows each pair contributes: n_inliers when status is
+ * 0, else 0), d_v_corr[offsets[p] .. offsets[p+1])[2] uint32 = pair p's inlier putatives in matcher order (rows past
+ * `capacity` are not written; capacity = sum of match counts always suffices), d_isp_ok[n_pairs] = 1 iff the pair
+ * verified and passes the inlier-support filter.
+ * ---------------------------------------------------------------------------------------------- */
+int gtsfm_compact_verified(const uint32_t* d_match_idx, const int* d_match_count, int mcap,
+                           const uint8_t* d_inlier_mask, const int* d_status, const int* d_n_inliers, int n_pairs,
+                           int min_inliers, double min_inlier_ratio, int* d_offsets, uint32_t* d_v_corr, int capacity,
+                           uint8_t* d_isp_ok, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
  * Detector-descriptor: SIFT (OpenCV defaults) + top-k by response over a batch of same-sized images.
