@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "gtsfm_hip.h"
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -14,6 +18,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
         hipError_t _e = (expr);                        \
         if (_e != hipSuccess) return GTSFM_ERR_HIP;    \
     } while (0)
+
+// Raises a kernel's dynamic-LDS limit to `bytes` on the CURRENT device, once per (kernel, device) and size;
+// thread-safe (the attribute is per device, so a process-global "done" flag would skip the second GPU).
+static inline hipError_t gtsfm_set_dynamic_lds(const void* fn, int bytes) {
+    static std::mutex mu;
+    static std::map<std::pair<const void*, int>, int> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    int& have = done[{fn, dev}];
+    if (have >= bytes) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) have = bytes;
+    return e;
+}
 
 __host__ __device__ static inline size_t gtsfm_align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 

@@ -940,12 +940,7 @@ template <int NS>
 int launch_fl_shortlist(const _Float16* form, const float* norm2, const int* counts, const int* pairs, int n_pairs,
                         int kpad, int kmax, int* cand, float* tkey, hipStream_t stream) {
     const size_t lds = 2 * kFlRows * (NS * 16 + 8) * sizeof(_Float16) + 2 * kFlRows * sizeof(float);
-    static bool set = false;
-    if (!set) {
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)fl_shortlist_kernel<NS>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        set = true;
-    }
+    GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)fl_shortlist_kernel<NS>, (int)lds));
     hipLaunchKernelGGL(fl_shortlist_kernel<NS>, dim3(kpad / kFlQ, n_pairs, 2), dim3(256), lds, stream, form, norm2,
                        counts, pairs, n_pairs, kpad, kmax, cand, tkey);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;

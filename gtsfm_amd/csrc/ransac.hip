@@ -1103,6 +1103,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
 // done >= niters, exactly as the oracle's batch loop (oracle/ransac.c:679-706).
 constexpr int kScoreWaves = 4;
 
+template <bool kLds>
 __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,
                                                                         const double* __restrict__ intr,
                                                                         const int* __restrict__ match_count, int mcap,
@@ -1128,7 +1129,10 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
     const double thr = thr_px / fx;
     const float thr2 = (float)(thr * thr);
     const float4* pts = pts_all + (size_t)p * mcap;
-    for (int i = tid; i < M; i += 64 * kScoreWaves) spts[i] = pts[i];
+    // kLds: the putatives are staged in LDS once (M <= 9600); oversize pairs read them from L2/HBM instead
+    if (kLds)
+        for (int i = tid; i < M; i += 64 * kScoreWaves) spts[i] = pts[i];
+    const float4* sp = kLds ? (const float4*)spts : pts;
     long best_off = -1;  // cand offset of a winner found by this launch
 #pragma unroll 1
     for (int g = 0; g < n_chunks && done < niters; ++g) {
@@ -1172,7 +1176,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
                 // exact
                 const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
                 const int i = base + lane;
-                const bool in = i < M && sampson_inlier(E, spts[i], thr2);
+                const bool in = i < M && sampson_inlier(E, sp[i], thr2);
                 c += __popcll(__ballot(in));
                 const int remaining = M - (base + 64);
                 if (remaining > 0) {
@@ -1411,22 +1415,12 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                        d_intrinsics, kmax, d_pairs, d_match_idx, d_match_count, mcap, x1n, x2n, pts);
     hipLaunchKernelGGL(ransac_init_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, stream, st, n_pairs, max_iters);
     GTSFM_CHECK_HIP(hipGetLastError());
-    static bool lds_set = false;
-    if (!lds_set) {
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)ransac_solve1_kernel,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSolveLds));
-        lds_set = true;
-    }
-    const size_t score_lds = (size_t)mcap * sizeof(float4);  // the pair's putatives
-    if (score_lds > 150 * 1024) return GTSFM_ERR_ARG;
-    if (score_lds > 65536) {
-        static size_t score_lds_set = 0;
-        if (score_lds > score_lds_set) {
-            GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)ransac_score_kernel,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)score_lds));
-            score_lds_set = score_lds;
-        }
-    }
+    GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_solve1_kernel, (int)kSolveLds));
+    // the score kernel stages a pair's putatives in LDS when they fit (16 B each, up to 150 KiB)
+    const bool score_in_lds = (size_t)mcap * sizeof(float4) <= 150 * 1024;
+    const size_t score_lds = score_in_lds ? (size_t)mcap * sizeof(float4) : 0;
+    if (score_lds > 65536)
+        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true>, (int)score_lds));
     // Chunks of 64 hypotheses, as the oracle; launches cover 1, 1, 2, 4, 8, 8, ... chunks. Most pairs stop within the
     // first two chunks; the pairs that run on are few, so their later chunks are solved together (speculatively: a
     // chunk the score kernel does not reach is discarded) to give the solver kernels enough waves.
@@ -1438,8 +1432,13 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            d_match_count, mcap, x1n, x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs, g), dim3(64), kRootLds, stream, d_match_count, st,
                            stage, cand, nsol);
-        hipLaunchKernelGGL(ransac_score_kernel, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream, d_pairs,
-                           d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
+        if (score_in_lds)
+            hipLaunchKernelGGL(ransac_score_kernel<true>, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream,
+                               d_pairs, d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab,
+                               st);
+        else
+            hipLaunchKernelGGL(ransac_score_kernel<false>, dim3(n_pairs), dim3(64 * kScoreWaves), 0, stream, d_pairs,
+                               d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask, d_n_models};

@@ -38,6 +38,7 @@ class FrontEndConfig:
     min_inliers: int = 15            # InlierSupportProcessor min_num_inliers_est_model
     min_inlier_ratio: float = 0.1    # InlierSupportProcessor min_inlier_ratio_est_model
     extract_chunk: int = 25          # images per SIFT launch sequence (the next chunk's H2D overlaps it)
+    extract_first: int = 0           # size of a smaller first chunk (0: same as extract_chunk): less exposed H2D
     pair_chunk: int = 32768          # pairs per match / verify / compact launch sequence
 
 
@@ -133,8 +134,11 @@ class AllPairsFrontEnd:
                               torch.zeros((n_local,), dtype=torch.int32, **z),
                               torch.zeros((n_local,), dtype=torch.int32, **z))
         ch = max(1, self.cfg.extract_chunk)
-        self.chunks = [(a, min(a + ch, n_local)) for a in range(0, n_local, ch)]
-        ws = self.kern.sift_workspace_bytes(min(ch, max(n_local, 1)), H, W, k) if n_local else 0
+        first = self.cfg.extract_first if 0 < self.cfg.extract_first < ch else ch
+        edges = [0] + list(range(min(first, n_local), n_local, ch)) + [n_local]
+        self.chunks = [(a, b) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+        big = max([b - a for a, b in self.chunks] + [1])
+        ws = self.kern.sift_workspace_bytes(big, H, W, k) if n_local else 0
         self.sift_ws = torch.empty(max(int(ws), 256), dtype=torch.uint8, **z)
 
         slot = sharding.global_slots(n_img, world)

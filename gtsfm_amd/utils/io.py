@@ -10,7 +10,10 @@ reference writes it. Two things differ, both so that cache directories move betw
   either name); any other global is treated like a corrupted file. The reference's loader (io.py:613-623) unpickles
   anything; cache directories are shared between machines, so this one does not.
 
-Corrupted or refused files are removed and read as a miss, as in the reference (io.py:619-621).
+Corrupted files (bz2 or pickle decode errors) are removed and read as a miss, as in the reference (io.py:619-621).
+A file the allowlist refuses is read as a miss and KEPT: it may be a valid entry written by the reference into a
+shared cache directory (e.g. a two-view entry holding gtsam Rot3 / Unit3 objects read where gtsam is absent). When
+gtsam is importable, its Rot3 / Unit3 / Cal3Bundler classes are allowed, so such entries load.
 """
 import io
 import logging
@@ -42,6 +45,19 @@ _PACKAGE_GLOBALS = {
     ("gtsfm_amd.common.geometry", "Rot3"), ("gtsfm_amd.common.geometry", "Unit3"),
     ("gtsfm_amd.common.geometry", "Cal3Bundler"),
 }
+# gtsam's pybind11 classes (what the reference's two-view cache entries hold), only where gtsam itself is importable
+_GTSAM_GLOBALS = {(m, n) for m in ("gtsam", "gtsam.gtsam") for n in ("Rot3", "Unit3", "Cal3Bundler")} | {
+    ("copyreg", "__newobj__")}
+
+
+def _allowed_globals():
+    from gtsfm_amd.common import geometry
+
+    return _NUMPY_GLOBALS | _PACKAGE_GLOBALS | (_GTSAM_GLOBALS if geometry.HAVE_GTSAM else set())
+
+
+class RefusedGlobal(pickle.UnpicklingError):
+    """A cache file names a class outside the allowlist: a miss, not a corrupted file."""
 
 
 class _ReferenceNamePickler(pickle._Pickler):
@@ -67,9 +83,9 @@ class _ReferenceNamePickler(pickle._Pickler):
 class _CacheUnpickler(pickle.Unpickler):
     def find_class(self, module: str, name: str) -> Any:
         module, name = _OUR_NAMES.get((module, name), (module, name))
-        if (module, name) in _NUMPY_GLOBALS or (module, name) in _PACKAGE_GLOBALS:
+        if (module, name) in _allowed_globals():
             return super().find_class(module, name)
-        raise pickle.UnpicklingError(f"global {module}.{name} is not allowed in a front-end cache file")
+        raise RefusedGlobal(f"global {module}.{name} is not allowed in a front-end cache file")
 
 
 def dumps(data: Any) -> bytes:
@@ -83,13 +99,17 @@ def loads(blob: bytes) -> Any:
 
 
 def read_from_bz2_file(file_path: Path) -> Optional[Any]:
-    """Reads a cache entry if it exists (io.py:613-623); corrupted or refused files are removed and read as None."""
+    """Reads a cache entry if it exists (io.py:613-623). Corrupted files are removed and read as None; files naming a
+    class outside the allowlist are read as None and kept."""
     file_path = Path(file_path)
     if not file_path.exists():
         return None
     try:
         with BZ2File(file_path, "rb") as f:
             return loads(f.read())
+    except RefusedGlobal as e:
+        logger.warning("Cache file %s not loaded (%s); treated as a miss and kept", file_path, e)
+        return None
     except Exception:
         logger.exception("Cache file was corrupted, removing it...")
         os.remove(file_path)

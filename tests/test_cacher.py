@@ -107,14 +107,27 @@ class _Print:
         return (print, ("cache payload executed",))
 
 
-def test_disallowed_global_is_refused_and_removed(tmp_path, capsys):
+def test_disallowed_global_is_refused_and_kept(tmp_path, capsys):
     path = tmp_path / "bad.pbz2"
     path.write_bytes(bz2.compress(pickle.dumps(_Print())))
     assert io_utils.read_from_bz2_file(path) is None
-    assert not path.exists()
+    assert path.exists()  # a refusal is a miss, not corruption: a shared cache entry is never deleted for it
     assert "cache payload executed" not in capsys.readouterr().out
     with pytest.raises(pickle.UnpicklingError):
         io_utils.loads(pickle.dumps(_Print()))
+
+
+def test_reference_two_view_entry_with_gtsam_classes_is_kept(tmp_path):
+    """A reference-written two-view entry names gtsam.gtsam.Rot3 / Unit3; without gtsam it cannot load here, and the
+    file must survive for the processes that can read it."""
+    from gtsfm_amd.common import geometry
+
+    if geometry.HAVE_GTSAM:
+        pytest.skip("gtsam importable: such entries load")
+    blob = (b"\x80\x04\x95\x1a\x00\x00\x00\x00\x00\x00\x00\x8c\x0bgtsam.gtsam\x94\x8c\x04Rot3\x94\x93\x94)\x81\x94.")
+    path = tmp_path / "tv.pbz2"
+    path.write_bytes(bz2.compress(blob))
+    assert io_utils.read_from_bz2_file(path) is None and path.exists()
 
 
 def test_corrupted_file_reads_as_miss(tmp_path):
