@@ -37,8 +37,9 @@ class FrontEndConfig:
     thresh_px: float = 4.0           # Ransac estimation_threshold_px (sift_front_end.yaml:48)
     min_inliers: int = 15            # InlierSupportProcessor min_num_inliers_est_model
     min_inlier_ratio: float = 0.1    # InlierSupportProcessor min_inlier_ratio_est_model
-    extract_chunk: int = 25          # images per SIFT launch sequence (the next chunk's H2D overlaps it)
-    extract_first: int = 0           # size of a smaller first chunk (0: same as extract_chunk): less exposed H2D
+    extract_chunk: int = 40          # host steps: images per SIFT launch sequence (the next chunk's H2D overlaps it)
+    extract_first: int = 20          # host steps: size of a smaller first chunk (less exposed H2D); 0 = extract_chunk
+    resident_chunk: int = 100        # device-resident steps: images per SIFT launch sequence (bounded by workspace)
     pair_chunk: int = 32768          # pairs per match / verify / compact launch sequence
 
 
@@ -133,11 +134,15 @@ class AllPairsFrontEnd:
                               torch.zeros((n_local, k, 128), dtype=torch.float32, **z),
                               torch.zeros((n_local,), dtype=torch.int32, **z),
                               torch.zeros((n_local,), dtype=torch.int32, **z))
-        ch = max(1, self.cfg.extract_chunk)
-        first = self.cfg.extract_first if 0 < self.cfg.extract_first < ch else ch
-        edges = [0] + list(range(min(first, n_local), n_local, ch)) + [n_local]
-        self.chunks = [(a, b) for a, b in zip(edges[:-1], edges[1:]) if b > a]
-        big = max([b - a for a, b in self.chunks] + [1])
+        def schedule(ch: int, first: int):
+            ch = max(1, ch)
+            first = first if 0 < first < ch else ch
+            edges = [0] + list(range(min(first, n_local), n_local, ch)) + [n_local]
+            return [(a, b) for a, b in zip(edges[:-1], edges[1:]) if b > a]
+
+        self.chunks = schedule(self.cfg.extract_chunk, self.cfg.extract_first)
+        self.chunks_resident = schedule(self.cfg.resident_chunk, 0)
+        big = max([b - a for a, b in self.chunks + self.chunks_resident] + [1])
         ws = self.kern.sift_workspace_bytes(big, H, W, k) if n_local else 0
         self.sift_ws = torch.empty(max(int(ws), 256), dtype=torch.uint8, **z)
 
@@ -208,7 +213,7 @@ class AllPairsFrontEnd:
         if self.cuda and not resident:
             self.copy_stream.wait_stream(cs)  # the previous step's extraction has finished reading dev_images
             self._mark("h2d_start", self.copy_stream)
-        for c, (a, b) in enumerate(self.chunks):
+        for c, (a, b) in enumerate(self.chunks_resident if resident else self.chunks):
             if not resident:
                 if self.cuda:
                     with torch.cuda.stream(self.copy_stream):
