@@ -14,6 +14,8 @@ try:  # pragma: no cover - exercised only where gtsam is installed
     Cal3Bundler = gtsam.Cal3Bundler
     Rot3 = gtsam.Rot3
     Unit3 = gtsam.Unit3
+    Pose3 = gtsam.Pose3
+    PinholeCameraCal3Bundler = gtsam.PinholeCameraCal3Bundler
     HAVE_GTSAM = True
 except ImportError:
     HAVE_GTSAM = False
@@ -69,6 +71,43 @@ except ImportError:
         def __reduce__(self):
             return (Unit3, (self._v,))
 
+    class Pose3:  # type: ignore[no-redef]
+        """wTc: rotation (Rot3) and translation (3,) -- the accessors the front-end uses."""
+
+        def __init__(self, R=None, t=(0.0, 0.0, 0.0)):
+            self._R = R if isinstance(R, Rot3) else Rot3(R)
+            self._t = np.asarray(t, dtype=np.float64).reshape(3)
+
+        def rotation(self) -> "Rot3":
+            return self._R
+
+        def translation(self) -> np.ndarray:
+            return self._t.copy()
+
+        def matrix(self) -> np.ndarray:
+            T = np.eye(4)
+            T[:3, :3], T[:3, 3] = self._R.matrix(), self._t
+            return T
+
+        def __reduce__(self):
+            return (Pose3, (self._R.matrix(), self._t))
+
+    class PinholeCameraCal3Bundler:  # type: ignore[no-redef]
+        """Ground-truth camera: pose wTc (Pose3) and Cal3Bundler calibration."""
+
+        def __init__(self, pose=None, K=None):
+            self._pose = pose if pose is not None else Pose3()
+            self._K = K if K is not None else Cal3Bundler()
+
+        def pose(self) -> "Pose3":
+            return self._pose
+
+        def calibration(self) -> "Cal3Bundler":
+            return self._K
+
+        def __reduce__(self):
+            return (PinholeCameraCal3Bundler, (self._pose, self._K))
+
 
 def calibration_params(cal) -> np.ndarray:
     """(f, u0, v0) of a Cal3Bundler; the device path requires k1 == k2 == 0 (true for every reference loader)."""
@@ -83,3 +122,31 @@ def rotation_matrix(R) -> np.ndarray:
 
 def unit_vector(U) -> np.ndarray:
     return np.asarray(U.point3(), dtype=np.float64).reshape(3)
+
+
+def skew(v) -> np.ndarray:
+    x, y, z = np.asarray(v, dtype=np.float64).reshape(3)
+    return np.array([[0.0, -z, y], [z, 0.0, -x], [-y, x, 0.0]])
+
+
+def camera_pose(camera):
+    """(wRc, wtc) of a ground-truth camera: a camera with .pose() (gtsam or stand-in), a Pose3, or a 4x4 / 3x4 wTc."""
+    if camera is None:
+        return None
+    p = camera.pose() if hasattr(camera, "pose") else camera
+    if hasattr(p, "rotation"):
+        return (np.asarray(p.rotation().matrix(), np.float64),
+                np.asarray(p.translation(), np.float64).reshape(3))
+    T = np.asarray(p, np.float64)
+    return T[:3, :3], T[:3, 3]
+
+
+def is_pinhole_cal3bundler(camera) -> bool:
+    """The reference computes GT correspondence metrics only for PinholeCameraCal3Bundler cameras
+    (two_view_estimator.py:241-243)."""
+    return isinstance(camera, PinholeCameraCal3Bundler)
+
+
+def calibration_matrix(camera) -> np.ndarray:
+    K = camera.calibration()
+    return np.asarray(K.K(), dtype=np.float64)

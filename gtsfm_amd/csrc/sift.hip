@@ -692,6 +692,51 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
     }
 }
 
+// ------------------------------------------------------------------ image mask (cv::KeyPointsFilter::runByPixelsMask)
+// One 1024-thread block per image: keeps the records whose pixel mask[(int)(y + 0.5f)][(int)(x + 0.5f)] is non-zero,
+// compacting them in place in their original order (read a chunk, barrier, write), and updates the image's count.
+// x, y are already in input-image pixels, as OpenCV applies the mask after scaling keypoints back from the
+// upsampled octave (sift.dispatch.cpp detectAndCompute).
+constexpr int kMaskThreads = 1024;
+
+__global__ __launch_bounds__(kMaskThreads) void mask_filter_kernel(KeyRec* __restrict__ kps, int* __restrict__ kp_counts,
+                                                                   int kp_cap, const uint8_t* __restrict__ masks, int H0,
+                                                                   int W0) {
+    __shared__ int wave_tot[kMaskThreads / 64];
+    __shared__ int base_sh;
+    const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int N = min(kp_counts[img], kp_cap);
+    KeyRec* K = kps + (size_t)img * kp_cap;
+    const uint8_t* mk = masks + (size_t)img * H0 * W0;
+    if (tid == 0) base_sh = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < N; c0 += kMaskThreads) {
+        const int i = c0 + tid;
+        KeyRec r;
+        bool keep = false;
+        if (i < N) {
+            r = K[i];
+            const int yy = (int)(r.y + 0.5f), xx = (int)(r.x + 0.5f);
+            keep = yy >= 0 && yy < H0 && xx >= 0 && xx < W0 && mk[(size_t)yy * W0 + xx] != 0;
+        }
+        const unsigned long long bal = __ballot(keep);
+        const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0));
+        if (lane == 0) wave_tot[wave] = __popcll(bal);
+        __syncthreads();
+        int before = base_sh;
+        for (int w = 0; w < wave; ++w) before += wave_tot[w];
+        __syncthreads();  // every record of the chunk is in registers before any slot is overwritten
+        if (keep) K[before + rank] = r;
+        if (tid == kMaskThreads - 1) {
+            int tot = base_sh;
+            for (int w = 0; w < kMaskThreads / 64; ++w) tot += wave_tot[w];
+            base_sh = tot;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) kp_counts[img] = base_sh;
+}
+
 // ------------------------------------------------------------------ top-k per image
 constexpr int kTopkThreads = 1024;
 constexpr int kTopkTieCap = 512;  // tie slots after the np2 sort slots
@@ -1095,7 +1140,8 @@ size_t gtsfm_sift_workspace_bytes(int n_img, int H, int W, int max_kpts) {
     return make_layout(n_img, H, W, max_kpts).total;
 }
 
-int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int channels, int max_kpts, void* d_workspace,
+int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_img, int H, int W, int channels,
+                       int max_kpts, void* d_workspace,
                        size_t workspace_bytes, float* d_xy, float* d_attr, float* d_desc, int* d_counts,
                        int* d_n_detected, void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
@@ -1181,6 +1227,11 @@ int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int cha
         hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps), kp_counts,
                            kKpCapPerImg);
+        GTSFM_CHECK_HIP(hipGetLastError());
+    }
+    if (d_masks) {
+        hipLaunchKernelGGL(mask_filter_kernel, dim3(B), dim3(kMaskThreads), 0, stream, (KeyRec*)(ws + L.kps),
+                           kp_counts, kKpCapPerImg, d_masks, H, W);
         GTSFM_CHECK_HIP(hipGetLastError());
     }
     int np2 = 1;

@@ -133,6 +133,22 @@ def compact_verified(match_idx: torch.Tensor, match_count: torch.Tensor, res: "R
     return offsets, v_corr, isp_ok
 
 
+def sampson_sq(F: torch.Tensor, row_pair: torch.Tensor, x1: torch.Tensor, x2: torch.Tensor,
+               precision: int = native.GTSFM_SAMPSON_F64, stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """Squared Sampson distance of row r = (x1[r], x2[r]) under F[row_pair[r]] (gtsfm_sampson_sq_batched).
+
+    F: (n_mats, 3, 3) float64; row_pair: (N,) int32; x1, x2: (N, 2) float64. Returns (N,) float64.
+    """
+    assert F.dtype == torch.float64 and F.is_contiguous() and F.is_cuda
+    assert x1.dtype == torch.float64 and x2.dtype == torch.float64 and x1.is_contiguous() and x2.is_contiguous()
+    assert row_pair.dtype == torch.int32 and row_pair.numel() == x1.shape[0] == x2.shape[0]
+    out = torch.empty(max(x1.shape[0], 1), dtype=torch.float64, device=F.device)
+    rc = native.lib().gtsfm_sampson_sq_batched(_ptr(F), F.shape[0], _ptr(row_pair), _ptr(x1), _ptr(x2), x1.shape[0],
+                                               int(precision), _ptr(out), native.stream_handle(stream))
+    native.check(rc, "gtsfm_sampson_sq_batched")
+    return out[: x1.shape[0]]
+
+
 class FundamentalResult(RansacResult):
     """Per-pair F-path outputs: F plus everything RansacResult holds (E = K2^T F K1)."""
 
@@ -187,9 +203,13 @@ class SiftResult:
 
 
 def sift_extract(images: torch.Tensor, max_kpts: int, stream: Optional[torch.cuda.Stream] = None,
-                 out: Optional[SiftResult] = None, workspace: Optional[torch.Tensor] = None) -> SiftResult:
-    """SIFT + top-k on a batch of same-sized uint8 images (n, H, W) gray or (n, H, W, 3) RGB (gtsfm_sift_batched)."""
+                 out: Optional[SiftResult] = None, workspace: Optional[torch.Tensor] = None,
+                 masks: Optional[torch.Tensor] = None) -> SiftResult:
+    """SIFT + top-k on a batch of same-sized uint8 images (n, H, W) gray or (n, H, W, 3) RGB (gtsfm_sift_batched).
+    masks: optional (n, H, W) uint8; keypoints on zero pixels are dropped before the top-k."""
     assert images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous()
+    assert masks is None or (masks.is_cuda and masks.dtype == torch.uint8 and masks.is_contiguous()
+                             and tuple(masks.shape) == tuple(images.shape[:3]))
     n = images.shape[0]
     H, W = images.shape[1], images.shape[2]
     C = 1 if images.dim() == 3 else images.shape[3]
@@ -205,7 +225,8 @@ def sift_extract(images: torch.Tensor, max_kpts: int, stream: Optional[torch.cud
     ws = workspace if workspace is not None and workspace.numel() >= nbytes else _workspace(nbytes, dev)
     if stream is not None:
         ws.record_stream(stream)
-    rc = L.gtsfm_sift_batched(_ptr(images), n, H, W, C, max_kpts, _ptr(ws), ws.numel(), _ptr(out.xy), _ptr(out.attr),
+    rc = L.gtsfm_sift_batched(_ptr(images), _ptr(masks), n, H, W, C, max_kpts, _ptr(ws), ws.numel(), _ptr(out.xy),
+                              _ptr(out.attr),
                               _ptr(out.desc), _ptr(out.count), _ptr(out.n_detected), native.stream_handle(stream))
     native.check(rc, "gtsfm_sift_batched")
     return out

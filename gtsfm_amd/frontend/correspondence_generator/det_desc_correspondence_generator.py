@@ -23,7 +23,7 @@ from gtsfm_amd.common.image import Image
 from gtsfm_amd.common.keypoints import Keypoints
 from gtsfm_amd.frontend.correspondence_generator.correspondence_generator_base import CorrespondenceGeneratorBase
 from gtsfm_amd.frontend.detector_descriptor.detector_descriptor_base import DetectorDescriptorBase
-from gtsfm_amd.frontend.detector_descriptor.sift import SIFTDetectorDescriptor, _to_device_batch
+from gtsfm_amd.frontend.detector_descriptor.sift import SIFTDetectorDescriptor, extract_group, sift_groups
 from gtsfm_amd.frontend.matcher.matcher_base import MatcherBase
 from gtsfm_amd.frontend.matcher.twoway_matcher import MatchingDistanceType, TwoWayMatcher
 
@@ -43,7 +43,8 @@ class DeviceFeatures:
 
 
 def extract_sift_batched(detector: SIFTDetectorDescriptor, images: Sequence[Image]) -> DeviceFeatures:
-    """One gtsfm_sift_batched launch sequence per distinct image size; features gathered into one padded block."""
+    """gtsfm_sift_batched launch sequences per image size (workspace-bounded groups); features gathered into one
+    padded block."""
     native.require_gpu()
     n, k = len(images), detector.max_keypoints
     dev = torch.device("cuda")
@@ -51,13 +52,8 @@ def extract_sift_batched(detector: SIFTDetectorDescriptor, images: Sequence[Imag
     attr = torch.zeros((n, k, 3), dtype=torch.float32, device=dev)
     desc = torch.zeros((n, k, 128), dtype=torch.float32, device=dev)
     count = torch.zeros((n,), dtype=torch.int32, device=dev)
-    by_shape: Dict[tuple, List[int]] = {}
-    for i, im in enumerate(images):
-        if im.mask is not None:
-            raise NotImplementedError("SIFT masks are not supported on the MI355X path yet")
-        by_shape.setdefault(im.value_array.shape, []).append(i)
-    for _, idx in by_shape.items():
-        res = device.sift_extract(_to_device_batch([images[i].value_array for i in idx]), k)
+    for idx in sift_groups(list(images), k):  # same shape, workspace-bounded; masks as detectAndCompute's
+        res = extract_group(list(images), idx, k)
         sel = torch.tensor(idx, dtype=torch.long, device=dev)
         xy[sel], attr[sel], desc[sel], count[sel] = res.xy, res.attr, res.desc, res.count
     cnt = count.cpu().numpy()

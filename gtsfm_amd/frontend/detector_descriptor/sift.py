@@ -7,8 +7,12 @@ the one restated in oracle/sift.c, which reproduces the reference's OpenCV fixtu
 
 The reference's get_top_k order is np.argpartition's (implementation-defined); here keypoints come in descending
 response order with a deterministic tie-break.
+
+Image masks follow detectAndCompute(gray, image.mask) (sift.py:47): a keypoint whose rounded pixel is 0 in the mask
+is dropped before the top-k. Batches are split so that one launch's workspace stays under WORKSPACE_BUDGET bytes
+(the SIFT pyramid costs ~128 B per input pixel).
 """
-from typing import List, Tuple
+from typing import Dict, List, Tuple
 
 import numpy as np
 import torch
@@ -26,6 +30,40 @@ def _to_device_batch(arrays: List[np.ndarray]) -> torch.Tensor:
     return torch.from_numpy(x).to(torch.device("cuda"))
 
 
+WORKSPACE_BUDGET = 24 << 30  # bytes of SIFT workspace per launch sequence
+
+
+def _mask_array(image: Image):
+    if image.mask is None:
+        return None
+    m = np.asarray(image.mask)
+    if m.shape != image.value_array.shape[:2]:
+        raise ValueError(f"mask shape {m.shape} does not match the image {image.value_array.shape[:2]}")
+    return (m != 0).astype(np.uint8)
+
+
+def sift_groups(images: List[Image], max_kpts: int) -> List[List[int]]:
+    """Indices of the images that share one launch: same shape, all masked or none, workspace under budget."""
+    by_key: Dict[tuple, List[int]] = {}
+    for i, im in enumerate(images):
+        by_key.setdefault((im.value_array.shape, im.mask is not None), []).append(i)
+    groups: List[List[int]] = []
+    L = native.lib()
+    for (shape, _), idx in by_key.items():
+        per = max(1, int(L.gtsfm_sift_workspace_bytes(1, shape[0], shape[1], max_kpts)))
+        n = max(1, WORKSPACE_BUDGET // per)
+        groups.extend(idx[s: s + n] for s in range(0, len(idx), n))
+    return groups
+
+
+def extract_group(images: List[Image], idx: List[int], max_kpts: int) -> device.SiftResult:
+    """One gtsfm_sift_batched launch sequence over images[idx] (same shape; masks all present or all absent)."""
+    masks = None
+    if images[idx[0]].mask is not None:
+        masks = torch.from_numpy(np.ascontiguousarray(np.stack([_mask_array(images[i]) for i in idx]))).cuda()
+    return device.sift_extract(_to_device_batch([images[i].value_array for i in idx]), max_kpts, masks=masks)
+
+
 def keypoints_from_result(res: device.SiftResult, i: int) -> Tuple[Keypoints, np.ndarray]:
     n = int(res.count[i].item())
     xy = res.xy[i, :n].cpu().numpy().astype(np.float64)
@@ -39,20 +77,14 @@ class SIFTDetectorDescriptor(DetectorDescriptorBase):
 
     def detect_and_describe(self, image: Image) -> Tuple[Keypoints, np.ndarray]:
         native.require_gpu()
-        if image.mask is not None:
-            raise NotImplementedError("SIFT masks are not supported on the MI355X path yet")
-        res = device.sift_extract(_to_device_batch([image.value_array]), self.max_keypoints)
-        return keypoints_from_result(res, 0)
+        return keypoints_from_result(extract_group([image], [0], self.max_keypoints), 0)
 
     def detect_and_describe_batch(self, images: List[Image]) -> List[Tuple[Keypoints, np.ndarray]]:
-        """All images of one size in a single batched launch sequence."""
+        """Images of one size in batched launch sequences (sift_groups)."""
         native.require_gpu()
         out: List[Tuple[Keypoints, np.ndarray]] = [None] * len(images)  # type: ignore
-        by_shape = {}
-        for i, im in enumerate(images):
-            by_shape.setdefault(im.value_array.shape, []).append(i)
-        for _, idx in by_shape.items():
-            res = device.sift_extract(_to_device_batch([images[i].value_array for i in idx]), self.max_keypoints)
+        for idx in sift_groups(images, self.max_keypoints):
+            res = extract_group(images, idx, self.max_keypoints)
             for j, i in enumerate(idx):
                 out[i] = keypoints_from_result(res, j)
         return out

@@ -35,6 +35,8 @@ GTSFM_ERR_CAPACITY = -3
 GTSFM_MATCH_EXACT_F32 = 0
 GTSFM_MATCH_INT_F16 = 1
 GTSFM_MATCH_F16_RERANK = 2
+GTSFM_SAMPSON_F64 = 0
+GTSFM_SAMPSON_F32_VERIFIER = 1
 RANSAC_STATUS_OK = 0
 RANSAC_STATUS_TOO_FEW = 1
 RANSAC_STATUS_NO_MODEL = 2
@@ -84,11 +86,13 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_int,
          c_void_p, c_void_p],
     ),
+    "gtsfm_sampson_sq_batched": (
+        c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "gtsfm_sift_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gtsfm_sift_batched": (
         c_int,
-        [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
-         c_void_p, c_void_p],
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p],
     ),
 }
 

@@ -24,6 +24,7 @@ from gtsfm_amd.common.keypoints import Keypoints
 from gtsfm_amd.common.two_view_estimation_report import TwoViewEstimationReport
 from gtsfm_amd.frontend.inlier_support_processor import InlierSupportProcessor
 from gtsfm_amd.frontend.verifier.verifier_base import VerifierBase
+from gtsfm_amd.utils import metrics as metric_utils
 
 logger = logging.getLogger(__name__)
 
@@ -33,13 +34,7 @@ TWO_VIEW_OUTPUT = Tuple[Optional[Any], Optional[Any], np.ndarray, TwoViewEstimat
 
 def _pose(camera) -> Optional[Tuple[np.ndarray, np.ndarray]]:
     """(wRi, wti) of a GT camera: a gtsam camera (.pose()), or a 4x4 / 3x4 wTi matrix."""
-    if camera is None:
-        return None
-    if hasattr(camera, "pose"):
-        p = camera.pose()
-        return np.asarray(p.rotation().matrix(), np.float64), np.asarray(p.translation(), np.float64).reshape(3)
-    T = np.asarray(camera, np.float64)
-    return T[:3, :3], T[:3, 3]
+    return geometry.camera_pose(camera)
 
 
 def compute_relative_pose_metrics(i2Ri1, i2Ui1, gt_camera_i1, gt_camera_i2) -> Tuple[Optional[float], Optional[float]]:
@@ -97,13 +92,26 @@ class TwoViewEstimator:
     def get_corr_metric_dist_threshold(self) -> float:
         return self._corr_metric_dist_threshold
 
-    def _finish(self, verified, gt_camera_i1, gt_camera_i2) -> TWO_VIEW_OUTPUT:
-        """Report + (skipped) BA + inlier-support processor for one verifier result (:298-351)."""
-        i2Ri1, i2Ui1, v_corr, ratio = verified
-        R_err, U_err = (None, None)
+    def _report(self, i2Ri1, i2Ui1, keypoints_i1, keypoints_i2, v_corr, ratio, gt_camera_i1, gt_camera_i2,
+                gt_scene_mesh=None) -> TwoViewEstimationReport:
+        """__get_2view_report_from_results (:210-270): pose errors w.r.t. GT, and for pinhole GT cameras the
+        Sampson-distance classification of the verified correspondences (utils/metrics.py:38-96)."""
+        R_err = U_err = mask_gt = err_gt = None
         if gt_camera_i1 is not None and gt_camera_i2 is not None:
             R_err, U_err = compute_relative_pose_metrics(i2Ri1, i2Ui1, gt_camera_i1, gt_camera_i2)
-        pre_ba_report = generate_two_view_report(ratio, v_corr, R_error_deg=R_err, U_error_deg=U_err)
+            if geometry.is_pinhole_cal3bundler(gt_camera_i1) and geometry.is_pinhole_cal3bundler(gt_camera_i2):
+                mask_gt, err_gt = metric_utils.compute_correspondence_metrics(
+                    keypoints_i1, keypoints_i2, v_corr, self._corr_metric_dist_threshold, gt_camera_i1, gt_camera_i2,
+                    gt_scene_mesh)
+        return generate_two_view_report(ratio, v_corr, R_error_deg=R_err, U_error_deg=U_err,
+                                        v_corr_idxs_inlier_mask_gt=mask_gt, reproj_error_gt_model=err_gt)
+
+    def _finish(self, verified, keypoints_i1, keypoints_i2, gt_camera_i1, gt_camera_i2,
+                gt_scene_mesh=None) -> TWO_VIEW_OUTPUT:
+        """Report + (skipped) BA + inlier-support processor for one verifier result (:298-351)."""
+        i2Ri1, i2Ui1, v_corr, ratio = verified
+        pre_ba_report = self._report(i2Ri1, i2Ui1, keypoints_i1, keypoints_i2, v_corr, ratio, gt_camera_i1,
+                                     gt_camera_i2, gt_scene_mesh)
         post_ba_report = dataclasses.replace(pre_ba_report)
         post_isp = self.processor.run_inlier_support(i2Ri1, i2Ui1, v_corr, post_ba_report)
         return post_isp[0], post_isp[1], post_isp[2], pre_ba_report, post_ba_report, post_isp[3]
@@ -113,7 +121,7 @@ class TwoViewEstimator:
                   gt_camera_i2=None, gt_scene_mesh=None) -> TWO_VIEW_OUTPUT:
         verified = self._verifier.verify(keypoints_i1, keypoints_i2, putative_corr_idxs, camera_intrinsics_i1,
                                          camera_intrinsics_i2)
-        return self._finish(verified, gt_camera_i1, gt_camera_i2)
+        return self._finish(verified, keypoints_i1, keypoints_i2, gt_camera_i1, gt_camera_i2, gt_scene_mesh)
 
 
 def run_two_view_estimator_as_futures(
@@ -148,7 +156,8 @@ def run_two_view_estimator_as_futures(
                                               camera_intrinsics[i2])
                     for (i1, i2), m in todo.items()}
     for (i1, i2), m in todo.items():
-        results[(i1, i2)] = two_view_estimator._finish(verified[(i1, i2)], gt[i1], gt[i2])
+        results[(i1, i2)] = two_view_estimator._finish(verified[(i1, i2)], keypoints_list[i1], keypoints_list[i2],
+                                                       gt[i1], gt[i2], gt_scene_mesh)
         if cached is not None:
             two_view_estimator.cache_store(keypoints_list[i1], keypoints_list[i2], m, results[(i1, i2)])
     return {k: results[k] for k in putative_corr_idxs_dict}

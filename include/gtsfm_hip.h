@@ -136,20 +136,37 @@ int gtsfm_compact_verified(const uint32_t* d_match_idx, const int* d_match_count
                            uint8_t* d_isp_ok, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
+ * Squared Sampson distances. Replaces gtsfm/utils/verification.py:170-214 compute_epipolar_distances_sq_sampson (the
+ * two-view report's ground-truth correspondence metric, gtsfm/utils/metrics.py:99-128), batched over pairs:
+ * row r (of n_rows) pairs d_x1[r] (x, y) with d_x2[r] under matrix d_F[d_row_pair[r]] (row-major 3x3, n_mats of them):
+ *   d_out[r] = (x2^T F x1)^2 / ((F x1)_x^2 + (F x1)_y^2 + (F^T x2)_x^2 + (F^T x2)_y^2).
+ * precision GTSFM_SAMPSON_F64: float64 (the reference's numpy arithmetic). GTSFM_SAMPSON_F32_VERIFIER: the fp32 FMA
+ * expression the essential-matrix RANSAC thresholds (its inlier test is d_out <= thr^2), for pinning the verifier.
+ * ---------------------------------------------------------------------------------------------- */
+#define GTSFM_SAMPSON_F64 0
+#define GTSFM_SAMPSON_F32_VERIFIER 1
+
+int gtsfm_sampson_sq_batched(const double* d_F, int n_mats, const int* d_row_pair, const double* d_x1,
+                             const double* d_x2, int n_rows, int precision, double* d_out, void* stream);
+
+/* ----------------------------------------------------------------------------------------------
  * Detector-descriptor: SIFT (OpenCV defaults) + top-k by response over a batch of same-sized images.
  *
  * d_images[n_img][H][W][channels] uint8, channels 1 (gray) or 3 (RGB, converted like cv.COLOR_RGB2GRAY).
+ * d_masks[n_img][H][W] uint8 or NULL: as detectAndCompute(gray, image.mask) (reference sift.py:47), a keypoint is
+ * dropped when its pixel mask[(int)(y + 0.5)][(int)(x + 0.5)] is 0, before the top-k.
  * Outputs per image, rows 0..count-1 valid, ordered by descending response:
  *   d_xy[n_img][max_kpts][2]   keypoint (x, y) in pixels (x right, y down, origin top-left corner)
  *   d_attr[n_img][max_kpts][3] (size, angle in degrees, response) as cv.KeyPoint
  *   d_desc[n_img][max_kpts][128] float32 descriptors with integer values in [0, 255]
- *   d_counts[n_img] = min(#keypoints, max_kpts); d_n_detected[n_img] (may be NULL) = #keypoints before top-k.
+ *   d_counts[n_img] = min(#keypoints, max_kpts); d_n_detected[n_img] (may be NULL) = #keypoints before top-k
+ *   (after the mask).
  * Limits: 16 <= H, W < 4096, max_kpts <= 8192.
  * ---------------------------------------------------------------------------------------------- */
 size_t gtsfm_sift_workspace_bytes(int n_img, int H, int W, int max_kpts);
 
-int gtsfm_sift_batched(const uint8_t* d_images, int n_img, int H, int W, int channels, int max_kpts,
-                       void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_attr, float* d_desc,
+int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_img, int H, int W, int channels,
+                       int max_kpts, void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_attr, float* d_desc,
                        int* d_counts, int* d_n_detected, void* stream);
 
 /* ----------------------------------------------------------------------------------------------

@@ -58,6 +58,8 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_five_point.argtypes = [_f64p, _f64p, _f64p]
         l.oracle_sample5.restype = ctypes.c_int
         l.oracle_sample5.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, _i32p]
+        l.oracle_sampson_sq.restype = None
+        l.oracle_sampson_sq.argtypes = [_f64p, _f64p, _f64p, ctypes.c_int, ctypes.c_int, _f64p]
         l.oracle_recover_pose.restype = ctypes.c_int
         l.oracle_recover_pose.argtypes = [_f64p, _f64p, _f64p, ctypes.c_void_p, ctypes.c_int, _f64p, _f64p]
     if hasattr(l, "oracle_ransac_F"):
@@ -74,6 +76,9 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_sift_detect_describe.restype = ctypes.c_int
         l.oracle_sift_detect_describe.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p, _f32p,
                                                   ctypes.POINTER(ctypes.c_int)]
+        l.oracle_sift_detect_describe_masked.restype = ctypes.c_int
+        l.oracle_sift_detect_describe_masked.argtypes = [_u8p, _u8p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _f32p,
+                                                         _f32p, ctypes.POINTER(ctypes.c_int)]
         l.oracle_rgb_to_gray.restype = None
         l.oracle_rgb_to_gray.argtypes = [_u8p, ctypes.c_int, ctypes.c_int, _u8p]
         l.oracle_sift_pyramid_level.restype = ctypes.c_int
@@ -141,6 +146,16 @@ def ransac_E(x1n: np.ndarray, x2n: np.ndarray, thr: float, prob: float = 0.99999
     return E.reshape(3, 3), mask[:M].copy(), R.reshape(3, 3), t, n, nh.value
 
 
+def sampson_sq(F: np.ndarray, x1: np.ndarray, x2: np.ndarray, precision: int = 0) -> np.ndarray:
+    """Squared Sampson distances (n,) of x1[i] <-> x2[i] under F: 0 = double, 1 = the verifier's float32 expression."""
+    x1 = np.ascontiguousarray(x1, np.float64).reshape(-1, 2)
+    x2 = np.ascontiguousarray(x2, np.float64).reshape(-1, 2)
+    out = np.zeros(len(x1), np.float64)
+    lib().oracle_sampson_sq(np.ascontiguousarray(F, np.float64).ravel(), x1.ravel(), x2.ravel(), len(x1), precision,
+                            out)
+    return out
+
+
 def seven_point(x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
     """All fundamental matrices (k,3,3), k <= 3, through 7 pixel correspondences (x1, x2: (7,2))."""
     pts = np.ascontiguousarray(np.hstack([x1, x2]), np.float32)
@@ -205,13 +220,20 @@ def rgb_to_gray(rgb: np.ndarray) -> np.ndarray:
     return g
 
 
-def sift(gray: np.ndarray, max_kpts: int = 5000, with_desc: bool = True):
-    """SIFT restatement on a u8 gray image: (kp (N,5) [x, y, size, angle, response], desc (N,128), n_detected)."""
+def sift(gray: np.ndarray, max_kpts: int = 5000, with_desc: bool = True, mask: Optional[np.ndarray] = None):
+    """SIFT restatement on a u8 gray image: (kp (N,5) [x, y, size, angle, response], desc (N,128), n_detected).
+    mask: optional (H, W) u8; keypoints whose rounded pixel is 0 are dropped before the top-k (runByPixelsMask)."""
     gray = np.ascontiguousarray(gray, np.uint8)
     H, W = gray.shape
     kp = np.zeros((max_kpts, 5), np.float32)
     desc = np.zeros((max_kpts, 128), np.float32)
     nd = ctypes.c_int(0)
+    if mask is not None:
+        m = np.ascontiguousarray(mask, np.uint8)
+        assert m.shape == (H, W)
+        n = lib().oracle_sift_detect_describe_masked(gray.ravel(), m.ravel(), H, W, max_kpts, kp.ravel(), desc.ravel(),
+                                                     ctypes.byref(nd))
+        return kp[:n].copy(), desc[:n].copy(), nd.value
     n = lib().oracle_sift_detect_describe(gray.ravel(), H, W, max_kpts, kp.ravel(), desc.ravel(), ctypes.byref(nd))
     return kp[:n].copy(), desc[:n].copy(), nd.value
 

@@ -744,3 +744,33 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
     free(pts);
     return cur;
 }
+
+/* Squared Sampson distances of n correspondences under F (row-major 3x3) -- reference
+ * gtsfm/utils/verification.py:170-214. precision 0: double (the reference's numpy arithmetic); 1: the float32 FMA
+ * expression sampson_inlier() thresholds (num^2 / den evaluated from the same float terms). */
+void oracle_sampson_sq(const double* F, const double* x1, const double* x2, int n, int precision, double* out) {
+    for (int i = 0; i < n; ++i) {
+        if (precision == 0) {
+            double den;
+            const double d = sampson_sq(F, x1 + 2 * i, x2 + 2 * i, &den);
+            const double a0 = F[0] * x1[2 * i] + F[1] * x1[2 * i + 1] + F[2];
+            const double a1 = F[3] * x1[2 * i] + F[4] * x1[2 * i + 1] + F[5];
+            const double a2 = F[6] * x1[2 * i] + F[7] * x1[2 * i + 1] + F[8];
+            const double num = x2[2 * i] * a0 + x2[2 * i + 1] * a1 + a2;
+            out[i] = den > 0.0 ? d : num * num / den;
+        } else {
+            float E[9];
+            for (int k = 0; k < 9; ++k) E[k] = (float)F[k];
+            const float px = (float)x1[2 * i], py = (float)x1[2 * i + 1];
+            const float pz = (float)x2[2 * i], pw = (float)x2[2 * i + 1];
+            const float a0 = fmaf(E[1], py, fmaf(E[0], px, E[2]));
+            const float a1 = fmaf(E[4], py, fmaf(E[3], px, E[5]));
+            const float a2 = fmaf(E[7], py, fmaf(E[6], px, E[8]));
+            const float b0 = fmaf(E[3], pw, fmaf(E[0], pz, E[6]));
+            const float b1 = fmaf(E[4], pw, fmaf(E[1], pz, E[7]));
+            const float num = fmaf(pw, a1, fmaf(pz, a0, a2));
+            const float den = fmaf(b1, b1, fmaf(b0, b0, fmaf(a1, a1, a0 * a0)));
+            out[i] = (double)(num * num) / (double)den;
+        }
+    }
+}

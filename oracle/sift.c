@@ -442,8 +442,11 @@ int sift_num_octaves(int H, int W) {
  * original-image pixels, descending response) and their 128-D descriptors. Returns the count kept;
  * *n_detected receives the number of keypoints before the top-k cut.
  */
-int oracle_sift_detect_describe(const uint8_t* gray, int H0, int W0, int max_kpts, float* kp_out, float* desc_out,
-                                int* n_detected) {
+/* mask (H0 x W0 u8, may be NULL): cv::SIFT::detectAndCompute(gray, mask) keeps a keypoint iff
+ * mask[(int)(y + 0.5f)][(int)(x + 0.5f)] != 0 (KeyPointsFilter::runByPixelsMask), after detection and before the
+ * caller's top-k (reference frontend/detector_descriptor/sift.py:47-56). n_detected counts the keypoints kept. */
+int oracle_sift_detect_describe_masked(const uint8_t* gray, const uint8_t* mask, int H0, int W0, int max_kpts,
+                                       float* kp_out, float* desc_out, int* n_detected) {
     pyr_t P;
     memset(&P, 0, sizeof(P));
     P.n_oct = sift_num_octaves(H0, W0);
@@ -553,6 +556,15 @@ int oracle_sift_detect_describe(const uint8_t* gray, int H0, int W0, int max_kpt
         }
         free(seen);
     }
+    if (mask) {
+        size_t w = 0;
+        for (size_t k = 0; k < nk; ++k) {
+            const int yy = (int)(kps[k].y + 0.5f), xx = (int)(kps[k].x + 0.5f);
+            if (yy < 0 || yy >= H0 || xx < 0 || xx >= W0 || mask[(size_t)yy * W0 + xx] == 0) continue;
+            kps[w++] = kps[k];
+        }
+        nk = w;
+    }
     if (n_detected) *n_detected = (int)nk;
     qsort(kps, nk, sizeof(kp_t), kp_cmp_topk);
     const int nout = (int)(nk < (size_t)max_kpts ? nk : (size_t)max_kpts);
@@ -575,6 +587,11 @@ int oracle_sift_detect_describe(const uint8_t* gray, int H0, int W0, int max_kpt
         for (int i = 0; i < N_LAYERS + 2; ++i) free(P.d[o][i]);
     }
     return nout;
+}
+
+int oracle_sift_detect_describe(const uint8_t* gray, int H0, int W0, int max_kpts, float* kp_out, float* desc_out,
+                                int* n_detected) {
+    return oracle_sift_detect_describe_masked(gray, NULL, H0, W0, max_kpts, kp_out, desc_out, n_detected);
 }
 
 /* Debug / parity hook: the Gaussian level (o, i) of an image into out (size returned through H, W). */

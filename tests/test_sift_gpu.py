@@ -139,3 +139,32 @@ def test_topk_many_ties_periodic_texture(dev, oracle_mod):
         assert nd == rnd
         np.testing.assert_array_equal(kp, rkp)
         np.testing.assert_array_equal(desc, rdesc)
+
+
+def test_image_mask_bit_exact_vs_oracle(dev, oracle_mod):
+    """detectAndCompute(gray, image.mask) (reference sift.py:47): keypoints on zero mask pixels are dropped before the
+    top-k; through the drop-in and the batched generator, mixed masked / unmasked images of one size."""
+    from gtsfm_amd.common.image import Image
+    from gtsfm_amd.frontend.correspondence_generator.det_desc_correspondence_generator import extract_sift_batched
+    from gtsfm_amd.frontend.detector_descriptor.sift import SIFTDetectorDescriptor
+
+    rng = np.random.default_rng(11)
+    H, W, k = 300, 400, 300
+    grays = [_texture(rng, H, W) for _ in range(3)]
+    mask = np.ones((H, W), np.uint8)
+    mask[:, : W // 3] = 0
+    mask[100:180, 220:330] = 0
+    det = SIFTDetectorDescriptor(max_keypoints=k)
+    kp, desc = det.detect_and_describe(Image(grays[0], mask=mask))
+    rkp, rdesc, _ = oracle_mod.sift(grays[0], k, mask=mask)
+    unmasked = oracle_mod.sift(grays[0], k)[0]
+    assert len(rkp) < len(unmasked) or len(unmasked) == k
+    np.testing.assert_array_equal(kp.coordinates, rkp[:, :2].astype(np.float64))
+    np.testing.assert_array_equal(desc, rdesc)
+    xi, yi = (rkp[:, 0] + 0.5).astype(int), (rkp[:, 1] + 0.5).astype(int)
+    assert (mask[yi, xi] != 0).all()
+    imgs = [Image(grays[0], mask=mask), Image(grays[1]), Image(grays[2], mask=mask.astype(bool))]
+    feats = extract_sift_batched(det, imgs)
+    for i, im in enumerate(imgs):
+        ref = oracle_mod.sift(grays[i], k, mask=None if im.mask is None else mask)[0]
+        np.testing.assert_array_equal(feats.keypoints[i].coordinates, ref[:, :2].astype(np.float64))
