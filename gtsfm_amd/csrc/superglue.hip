@@ -498,6 +498,20 @@ __global__ __launch_bounds__(256) void sg_emit_kernel(const int* __restrict__ si
     if (threadIdx.x == 0) out_count[p] = base;
 }
 
+// final log-assignment of one pair ((Z + u) + v) - norm, rows 0..m, columns 0..n (ld = kmax + 1), NaN elsewhere
+__global__ __launch_bounds__(256) void sk_final_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                       int kmax, const float* __restrict__ u,
+                                                       const float* __restrict__ v, int p, float* __restrict__ out) {
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const long ld = kmax + 1;
+    const long e = (long)blockIdx.x * 256 + threadIdx.x;
+    if (e >= ld * ld) return;
+    const int i = (int)(e / ld), j = (int)(e % ld);
+    out[e] = (i <= m && j <= n) ? ((Z[(long)p * ld * ld + e] + u[(long)p * ld + i]) + v[(long)p * ld + j]) -
+                                      sk_norm(m, n)
+                                : __builtin_nanf("");
+}
+
 // ------------------------------------------------------------------ host-side orchestration
 struct SgLayout {
     size_t enc_in, X, T1, T2, qkv, att, msg, hid, Z, u, v, max0, idx0, idx1, cnt, total;
@@ -676,6 +690,22 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
                        idx1);
     hipLaunchKernelGGL(sg_emit_kernel, dim3(n_pairs), dim3(256), 0, stream, side_counts, kmax, max0, idx0, idx1,
                        match_threshold, d_out_idx, d_out_count, d_out_mscores);
+    GTSFM_CHECK_HIP(hipGetLastError());
+    return GTSFM_OK;
+}
+
+int gtsfm_superglue_log_assignment(const void* d_workspace, size_t workspace_bytes, int n_pairs, int kmax, int pair,
+                                   float* d_out, void* stream_v) {
+    hipStream_t stream = (hipStream_t)stream_v;
+    if (!d_workspace || !d_out || n_pairs <= 0 || pair < 0 || pair >= n_pairs || kmax <= 0 || kmax % 64 != 0)
+        return GTSFM_ERR_ARG;
+    const SgLayout L = sg_layout(n_pairs, kmax);
+    if (workspace_bytes < L.total) return GTSFM_ERR_CAPACITY;
+    const unsigned char* ws = (const unsigned char*)d_workspace;
+    const long ld = kmax + 1;
+    hipLaunchKernelGGL(sk_final_kernel, dim3((unsigned)((ld * ld + 255) / 256)), dim3(256), 0, stream,
+                       (const float*)(ws + L.Z), (const int*)(ws + L.cnt), kmax, (const float*)(ws + L.u),
+                       (const float*)(ws + L.v), pair, d_out);
     GTSFM_CHECK_HIP(hipGetLastError());
     return GTSFM_OK;
 }

@@ -275,7 +275,8 @@ def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: in
 def superglue_match(kp: torch.Tensor, scores: torch.Tensor, desc: torch.Tensor, counts: torch.Tensor,
                     image_hw: torch.Tensor, pairs: torch.Tensor, weights: torch.Tensor, n_layers: int = 18,
                     sinkhorn_iters: int = 20, match_threshold: float = 0.2,
-                    stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+                    stream: Optional[torch.cuda.Stream] = None, workspace: Optional[torch.Tensor] = None
+                    ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """SuperGlue over every pair (gtsfm_superglue_batched).
 
     Args: kp (n_img, kmax, 2) f32, scores (n_img, kmax) f32, desc (n_img, kmax, 256) f32, counts (n_img,) int32,
@@ -295,7 +296,8 @@ def superglue_match(kp: torch.Tensor, scores: torch.Tensor, desc: torch.Tensor, 
     cnt = torch.zeros((max(P, 1),), dtype=torch.int32, device=dev)
     ms = torch.zeros((max(P, 1), kmax), dtype=torch.float32, device=dev)
     if P > 0:
-        ws = _workspace(L.gtsfm_superglue_workspace_bytes(P, kmax), dev)
+        need = L.gtsfm_superglue_workspace_bytes(P, kmax)
+        ws = workspace if workspace is not None and workspace.numel() >= need else _workspace(need, dev)
         if stream is not None:
             ws.record_stream(stream)
         rc = L.gtsfm_superglue_batched(_ptr(kp), _ptr(scores), _ptr(desc), _ptr(counts), _ptr(image_hw), n_img, kmax,
@@ -304,3 +306,14 @@ def superglue_match(kp: torch.Tensor, scores: torch.Tensor, desc: torch.Tensor, 
                                        native.stream_handle(stream))
         native.check(rc, "gtsfm_superglue_batched")
     return idx[:P], cnt[:P], ms[:P]
+
+
+def superglue_log_assignment(workspace: torch.Tensor, n_pairs: int, kmax: int, pair: int,
+                             stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """Pair `pair`'s final log-assignment matrix (kmax + 1, kmax + 1) from the workspace of the superglue_match call
+    that used `workspace` (gtsfm_superglue_log_assignment; entries past (m + 1, n + 1) are NaN)."""
+    out = torch.empty((kmax + 1, kmax + 1), dtype=torch.float32, device=workspace.device)
+    rc = native.lib().gtsfm_superglue_log_assignment(_ptr(workspace), workspace.numel(), n_pairs, kmax, pair, _ptr(out),
+                                                     native.stream_handle(stream))
+    native.check(rc, "gtsfm_superglue_log_assignment")
+    return out

@@ -25,6 +25,25 @@ RANSAC_MAX_ITERS = 1000  # cv2.findEssentialMat default maxIters
 RANSAC_MAX_ITERS_F = 1000000  # ransac.py:23, passed to cv2.findFundamentalMat
 
 
+def _checked_indices(match_indices: np.ndarray, n1: int, n2: int) -> np.ndarray:
+    """(M, 2) int64 keypoint indices, as numpy's fancy indexing in the reference would take them
+    (opencv_verifier_base.py:73-74, uv_norm[match_indices[:, k]]): negative indices wrap once, anything outside
+    [-n, n) raises IndexError before a device kernel could read out of bounds."""
+    m = np.asarray(match_indices).reshape(-1, 2).astype(np.int64)
+    for col, n in ((0, n1), (1, n2)):
+        c = m[:, col]
+        if len(c) and (c.min() < -n or c.max() >= n):
+            raise IndexError(f"match index out of bounds for {n} keypoints (column {col})")
+        m[:, col] = np.where(c < 0, c + n, c)
+    return m
+
+
+def _calibration(cal) -> np.ndarray:
+    if cal is None:  # the reference fails on None intrinsics too (normalize_coordinates calls cal.calibrate)
+        raise ValueError("camera intrinsics are required by the verifier")
+    return geometry.calibration_params(cal)
+
+
 class Ransac(VerifierBase):
     """RANSAC verifier computed by HIP kernels: 5-point E path with intrinsics, 7-point F path without."""
 
@@ -43,6 +62,8 @@ class Ransac(VerifierBase):
     ) -> Tuple[Optional[object], Optional[object], np.ndarray, float]:
         if match_indices.shape[0] < self._min_matches or match_indices.shape[0] < 6:
             return self._failure_result
+        checked = _checked_indices(match_indices, len(keypoints_i1), len(keypoints_i2))
+        intr = np.stack([_calibration(camera_intrinsics_i1), _calibration(camera_intrinsics_i2)])
         native.require_gpu()
         M = match_indices.shape[0]
         if not self._use_intrinsics_in_verification:
@@ -55,9 +76,7 @@ class Ransac(VerifierBase):
         kp = np.zeros((2, kmax, 2), np.float32)
         kp[0, : len(c1)] = c1
         kp[1, : len(c2)] = c2
-        intr = np.stack([geometry.calibration_params(camera_intrinsics_i1),
-                         geometry.calibration_params(camera_intrinsics_i2)])
-        mi = np.ascontiguousarray(match_indices, dtype=np.int64).astype(np.int32).reshape(1, M, 2)
+        mi = checked.astype(np.int32).reshape(1, M, 2)
         res = device.ransac_essential(
             torch.from_numpy(kp).to(dev), torch.from_numpy(intr).to(dev),
             torch.tensor([[0, 1]], dtype=torch.int32, device=dev), torch.from_numpy(mi).to(dev),
@@ -93,7 +112,8 @@ class Ransac(VerifierBase):
         for i, k in enumerate(keypoints_list):
             kp[i, : len(k)] = k.coordinates
         kp_d = torch.from_numpy(kp).to(dev)
-        intr = np.stack([geometry.calibration_params(c) if c is not None else np.zeros(3) for c in camera_intrinsics])
+        used = {i for p in putative_corr_idxs_dict for i in p}
+        intr = np.stack([_calibration(c) if i in used else np.zeros(3) for i, c in enumerate(camera_intrinsics)])
         intr_d = torch.from_numpy(intr).to(dev)
         keys = list(putative_corr_idxs_dict.keys())
         out: Dict[Tuple[int, int], Tuple[Optional[object], Optional[object], np.ndarray, float]] = {}
@@ -108,8 +128,8 @@ class Ransac(VerifierBase):
             mi = np.zeros((len(run), mcap, 2), np.int32)
             cnt = np.zeros(len(run), np.int32)
             for j, p in enumerate(run):
-                m = np.asarray(putative_corr_idxs_dict[p]).reshape(-1, 2)
-                mi[j, : len(m)] = m.astype(np.int64).astype(np.int32)
+                m = _checked_indices(putative_corr_idxs_dict[p], len(keypoints_list[p[0]]), len(keypoints_list[p[1]]))
+                mi[j, : len(m)] = m.astype(np.int32)
                 cnt[j] = len(m)
             args = (kp_d, intr_d, torch.tensor(run, dtype=torch.int32, device=dev), torch.from_numpy(mi).to(dev),
                     torch.from_numpy(cnt).to(dev), self._estimation_threshold_px, RANSAC_SUCCESS_PROB)

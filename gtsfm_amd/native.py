@@ -81,6 +81,7 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int,
          c_float, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
+    "gtsfm_superglue_log_assignment": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p]),
     "gtsfm_compact_verified": (
         c_int,
         [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_int,

@@ -214,6 +214,13 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
                             void* d_workspace, size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count,
                             float* d_out_mscores, void* stream);
 
+/* Inspection hook (the reference keeps this matrix internal: superglue.py:261-263 `scores`): after a
+ * gtsfm_superglue_batched call, writes pair `pair`'s final log-assignment matrix (log_optimal_transport's output, the
+ * Sinkhorn result + the normalisation) from that call's workspace into d_out[(kmax + 1)][(kmax + 1)]: rows 0..m,
+ * columns 0..n (the last of each being the dustbin), NaN elsewhere. Same n_pairs / kmax as the call. */
+int gtsfm_superglue_log_assignment(const void* d_workspace, size_t workspace_bytes, int n_pairs, int kmax, int pair,
+                                   float* d_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,7 +6,7 @@ offline; torch.load is redirected while the module is constructed), sinkhorn_ite
 gtsfm/frontend/matcher/superglue_matcher.py:25-41 configures it. Inputs: seeded synthetic keypoint sets (x, y in the
 image, scores in (0, 1)) with unit 256-D descriptors; 40 % of the points of image 1 are noisy copies of points of
 image 0 so that matches exist. Recorded per case: inputs, matches0 / matching_scores0, and for the small case the
-full log-assignment matrix.
+full log-assignment matrix; for the 2048 x 2048 case (BASELINE config C5's keypoint count) every 32nd row of it.
 
     python tests/golden/make_superglue_golden.py
 """
@@ -87,15 +87,20 @@ def main():
     rng = np.random.default_rng(7)
     out = {}
     for name, (n0, n1, H, W, want_Z) in {"small_150x170": (150, 170, 480, 640, True),
-                                         "mid_700x650": (700, 650, 1080, 1920, False)}.items():
+                                         "mid_700x650": (700, 650, 1080, 1920, False),
+                                         "c5_2048x2048": (2048, 2048, 1080, 1920, True)}.items():
         kp0, kp1, d0, d1, s0, s1 = make_case(rng, n0, n1, H, W)
         m0, ms0, Z = run(model, kp0, kp1, d0, d1, s0, s1, H, W, want_Z)
         out.update({f"{name}__kp0": kp0, f"{name}__kp1": kp1, f"{name}__d0": d0, f"{name}__d1": d1,
                     f"{name}__s0": s0, f"{name}__s1": s1, f"{name}__hw": np.array([H, W]),
                     f"{name}__matches0": m0, f"{name}__mscores0": ms0})
-        if want_Z:
+        if want_Z and n0 <= 256:
             out[f"{name}__Z"] = Z["Z"]
             out[f"{name}__scores"] = Z["S"]
+        elif want_Z:  # BASELINE config C5 size: every 32nd row of the log-assignment + the dustbin row (16 MB in full)
+            rows = np.concatenate([np.arange(0, n0, 32), [n0]])
+            out[f"{name}__Z_rows"] = rows.astype(np.int32)
+            out[f"{name}__Z_sub"] = Z["Z"][rows].copy()
         print(name, "matches", int((m0 >= 0).sum()), "of", n0, "mscore range", float(ms0.max()))
     np.savez_compressed(os.path.join(HERE, "superglue_random_w0.npz"), **out)
 

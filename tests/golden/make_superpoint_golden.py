@@ -40,6 +40,10 @@ def reference_superpoint(seed=0):
     return model
 
 
+LUND_1080P_CROP = (slice(8, 1928), slice(108, 1188))
+TOPK_C3 = 4096  # BASELINE config C3: 4096 keypoints per image
+
+
 def cases():
     gray = np.asarray(PILImage.open(os.path.join(HERE, "lund_door_DSC_0001_gray.png")))
     out = {"lund_480x640": np.ascontiguousarray(gray[300:780, 200:840]),
@@ -52,6 +56,9 @@ def cases():
     from oracle import oracle
 
     out["synthetic_240x320"] = oracle.rgb_to_gray(rgb)
+    # BASELINE config C3 resolution: a 1920 x 1080 (portrait) crop of the full Lund image (not stored: the test
+    # re-crops the committed PNG with LUND_1080P_CROP)
+    out["lund_1920x1080"] = np.ascontiguousarray(gray[LUND_1080P_CROP])
     return out
 
 
@@ -65,8 +72,13 @@ def main():
         kp = r["keypoints"][0].numpy().astype(np.float32)
         sc = r["scores"][0].numpy().astype(np.float32)
         desc = r["descriptors"][0].numpy().astype(np.float32)  # (256, N)
-        sel = np.arange(0, kp.shape[0], 8)
-        res[f"{name}__image"] = g
+        if name == "lund_1920x1080":
+            # descriptors of every 8th keypoint of the top-4096 set (the drop-in's get_top_k(4096))
+            top = np.sort(np.argsort(-sc, kind="stable")[:TOPK_C3])
+            sel = top[::8]
+        else:
+            sel = np.arange(0, kp.shape[0], 8)
+            res[f"{name}__image"] = g
         res[f"{name}__keypoints"] = kp
         res[f"{name}__scores"] = sc
         res[f"{name}__desc_rows"] = sel.astype(np.int32)

@@ -61,3 +61,22 @@ def test_empty_inputs_need_no_gpu():
     m = TwoWayMatcher(ratio_test_threshold=0.8)
     out = m.match(None, None, np.zeros((0, 128), np.float32), np.zeros((5, 128), np.float32), (4, 4, 3), (4, 4, 3))
     assert out.size == 0
+
+
+def test_ransac_rejects_out_of_range_indices_and_missing_intrinsics():
+    """Index checks happen on the host before any device call (reference: numpy IndexError on fancy indexing)."""
+    import pytest
+
+    from gtsfm_amd.common import geometry
+    from gtsfm_amd.common.keypoints import Keypoints
+    from gtsfm_amd.frontend.verifier.ransac import Ransac, _checked_indices
+
+    kp = Keypoints(coordinates=np.random.default_rng(0).uniform(0, 100, (10, 2)))
+    v = Ransac(use_intrinsics_in_verification=True, estimation_threshold_px=4)
+    bad = np.stack([np.arange(8), np.arange(8)], 1)
+    bad[3, 1] = 10
+    with pytest.raises(IndexError):
+        v.verify(kp, kp, bad, geometry.Cal3Bundler(), geometry.Cal3Bundler())
+    with pytest.raises(ValueError):
+        v.verify(kp, kp, bad[:, ::-1] % 10, None, geometry.Cal3Bundler())
+    np.testing.assert_array_equal(_checked_indices(np.array([[-1, 2], [3, -10]]), 10, 10), [[9, 2], [3, 0]])

@@ -15,7 +15,7 @@ import torch
 from superpoint_weights import superglue_state_dict
 
 pytestmark = pytest.mark.gpu
-CASES = ["small_150x170", "mid_700x650"]
+CASES = ["small_150x170", "mid_700x650", "c5_2048x2048"]
 
 
 @pytest.fixture(scope="module")
@@ -89,3 +89,38 @@ def test_matching_scores_close(matcher, golden, name):
                                       matcher.weights())
     ref = golden[f"{name}__mscores0"]
     np.testing.assert_allclose(ms[0, :n0].cpu().numpy(), ref, atol=2e-3)
+
+
+@pytest.mark.parametrize("name", ["small_150x170", "c5_2048x2048"])
+def test_log_assignment_matrix(matcher, golden, name):
+    """The final log-assignment matrix (log_optimal_transport's output, dustbins included) against the reference
+    module's: the full (m+1) x (n+1) matrix for the small case, every 32nd row + the dustbin row at 2048 x 2048
+    (BASELINE config C5's keypoint count). atol 2e-3 on entries above -20 (exp(-20) ~ 2e-9 of probability mass)."""
+    from gtsfm_amd import device
+
+    kp0, kp1, d0, d1, shape, _ = _case(golden, name)
+    n0, n1 = len(kp0), len(kp1)
+    kmax = (max(n0, n1) + 63) // 64 * 64
+    kp = np.zeros((2, kmax, 2), np.float32)
+    sc = np.zeros((2, kmax), np.float32)
+    de = np.zeros((2, kmax, 256), np.float32)
+    kp[0, :n0], kp[1, :n1] = kp0.coordinates, kp1.coordinates
+    sc[0, :n0], sc[1, :n1] = kp0.responses, kp1.responses
+    de[0, :n0], de[1, :n1] = d0, d1
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    from gtsfm_amd import native
+
+    ws = torch.empty(native.lib().gtsfm_superglue_workspace_bytes(1, kmax), dtype=torch.uint8, device="cuda")
+    device.superglue_match(t(kp), t(sc), t(de), t(np.array([n0, n1], np.int32)),
+                           t(np.array([shape[:2], shape[:2]], np.int32)), t(np.array([[0, 1]], np.int32)),
+                           matcher.weights(), workspace=ws)
+    Z = device.superglue_log_assignment(ws, 1, kmax, 0).cpu().numpy()[: n0 + 1, : n1 + 1]
+    if f"{name}__Z" in golden.files:
+        rows, ref = np.arange(n0 + 1), golden[f"{name}__Z"]
+    else:
+        rows, ref = golden[f"{name}__Z_rows"], golden[f"{name}__Z_sub"]
+    got = Z[rows]
+    assert ref.shape == got.shape and np.isfinite(got).all()
+    live = ref > -20
+    np.testing.assert_allclose(got[live], ref[live], atol=2e-3)
+    assert (got[~live] < -15).all()

@@ -97,3 +97,31 @@ def test_plugin_api(det, golden):
     kp, desc = d.detect_and_describe(Image(rgb))
     assert len(kp) == 500 and desc.shape == (500, 256) and desc.dtype == np.float32
     assert kp.scales is None and kp.responses.shape == (500,) and kp.coordinates.dtype == np.float32
+
+
+def test_c3_1080p_top_4096(det, golden, golden_dir):
+    """BASELINE config C3's extraction: a 1920 x 1080 image, max_keypoints 4096 (the drop-in's get_top_k(4096) over
+    the reference module's detections). The kept set is the reference's 4096 highest scores (ties at the boundary
+    aside), emitted in raster order; scores rtol 1e-4 and descriptors 2e-4 as above."""
+    from PIL import Image as PILImage
+
+    gray = np.asarray(PILImage.open(os.path.join(golden_dir, "lund_door_DSC_0001_gray.png")))
+    img = np.ascontiguousarray(gray[8:1928, 108:1188])  # make_superpoint_golden.LUND_1080P_CROP
+    ref_kp, ref_sc = golden["lund_1920x1080__keypoints"], golden["lund_1920x1080__scores"]
+    res = det.extract_batch([img], max_kpts=4096)
+    n = int(res.count[0])
+    assert n == 4096 and abs(int(res.n_detected[0]) - len(ref_kp)) <= 0.005 * len(ref_kp)
+    xy = res.xy[0, :n].cpu().numpy()
+    sc = res.scores[0, :n].cpu().numpy()
+    desc = res.desc[0, :n].cpu().numpy()
+    assert np.array_equal(np.lexsort((xy[:, 0], xy[:, 1])), np.arange(n))
+    top = np.argsort(-ref_sc, kind="stable")[:4096]
+    a, b = _keyset(xy), _keyset(ref_kp[top])
+    assert len(a & b) >= 0.995 * 4096, len(a & b)
+    pos = {k: i for i, k in enumerate(map(tuple, np.round(xy).astype(int)))}
+    ref_pos = np.array([pos.get((int(x), int(y)), -1) for x, y in ref_kp])
+    m = ref_pos >= 0
+    np.testing.assert_allclose(sc[ref_pos[m]], ref_sc[m], rtol=1e-4)
+    for r, d in zip(golden["lund_1920x1080__desc_rows"], golden["lund_1920x1080__desc"]):
+        if ref_pos[r] >= 0:
+            np.testing.assert_allclose(desc[ref_pos[r]], d, atol=2e-4)
