@@ -134,3 +134,20 @@ def test_twoway_matcher_selects_rerank(dev):
     rng = np.random.default_rng(8)
     assert select_match_mode(_unit(rng, 5, 256), _unit(rng, 6, 256)) == native.GTSFM_MATCH_F16_RERANK
     assert select_match_mode(_unit(rng, 5, 300), _unit(rng, 6, 300)) == native.GTSFM_MATCH_EXACT_F32
+
+
+def test_c3_size_4096_by_4096_256d(dev, oracle_mod):
+    """BASELINE config C3's matcher shape: 4096 x 4096 x 256-D SuperPoint-like descriptors (planted matches, ratio
+    0.8), a batch of image pairs: identical to EXACT_F32 on every pair and to the oracle on two of them."""
+    rng = np.random.default_rng(4096)
+    base = _unit(rng, 4096, 256)
+    descs = []
+    for _ in range(4):
+        d = _unit(rng, 4096, 256)
+        k = int(0.3 * 4096)
+        y = base[rng.permutation(4096)[:k]] + 0.15 * rng.normal(size=(k, 256)) / 16
+        d[rng.permutation(4096)[:k]] = y / np.linalg.norm(y, axis=1, keepdims=True)
+        descs.append(d.astype(np.float32))
+    pairs = [(0, 1), (2, 3), (0, 3), (1, 2)]
+    fast = _check(dev, oracle_mod, descs, pairs, 0.8, n_oracle=2)
+    assert min(len(f) for f in fast) > 200  # ~0.3 x 0.3 x 4096 planted matches per pair
