@@ -29,7 +29,7 @@ def _checked_indices(match_indices: np.ndarray, n1: int, n2: int) -> np.ndarray:
     """(M, 2) int64 keypoint indices, as numpy's fancy indexing in the reference would take them
     (opencv_verifier_base.py:73-74, uv_norm[match_indices[:, k]]): negative indices wrap once, anything outside
     [-n, n) raises IndexError before a device kernel could read out of bounds."""
-    m = np.asarray(match_indices).reshape(-1, 2).astype(np.int64)
+    m = np.ascontiguousarray(np.asarray(match_indices).reshape(-1, 2), dtype=np.int64)
     for col, n in ((0, n1), (1, n2)):
         c = m[:, col]
         if len(c) and (c.min() < -n or c.max() >= n):
