@@ -273,6 +273,7 @@ def main_frontend(args, info, config: str):
         cfg.resident_chunk = args.resident_chunk
     if args.pair_chunk:
         cfg.pair_chunk = args.pair_chunk
+    cfg.bundle_adjust = args.ba
     fe = AllPairsFrontEnd(host_images, scene.intrinsics, n_img, rank, world, dev, cfg)
 
     for _ in range(args.warmup):
@@ -373,7 +374,8 @@ def main_frontend(args, info, config: str):
         "dtype": "u8 image / fp32 pyramid / fp16-MFMA exact-int distances / fp64 RANSAC solver",
         "data": "synthetic (rendered textured room, seeds 0/1/2)",
         "config": {"workload": f"{wl}: {n_img} synthetic {W}x{H} images, all {fe.total_pairs} pairs, SIFT {kpts} "
-                               f"kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px + inlier support",
+                               f"kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px"
+                               + (" + two-view BA" if args.ba else "") + " + inlier support",
                    "images": n_img, "pairs": fe.total_pairs, "kpts": kpts, "parallelism": f"pair blocks x{world}",
                    "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1},
         "value_host_to_host": round(fe.total_pairs / (elapsed / args.steps), 2),
@@ -404,6 +406,8 @@ def main():
     ap.add_argument("--resident-chunk", type=int, default=0)
     ap.add_argument("--pair-chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ba", action="store_true",
+                    help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
     ap.add_argument("--config", default="c2", choices=["c2", "c4", "c3-match"])
     ap.add_argument("--launch-probe", action="store_true",
                     help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")

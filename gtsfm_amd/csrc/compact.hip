@@ -51,7 +51,8 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(const uint2* __restri
                                                            const int* __restrict__ match_count, int mcap,
                                                            const uint8_t* __restrict__ mask,
                                                            const int* __restrict__ status,
-                                                           const int* __restrict__ n_inl, int n_pairs,
+                                                           const int* __restrict__ n_inl,
+                                                           const int* __restrict__ ratio_inl, int n_pairs,
                                                            int min_inliers, double min_ratio,
                                                            const int* __restrict__ offsets, int capacity,
                                                            uint2* __restrict__ v_corr, uint8_t* __restrict__ isp_ok) {
@@ -59,7 +60,8 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(const uint2* __restri
     if (p >= n_pairs) return;
     const int st = status[p], n = n_inl[p], M = match_count[p];
     if (lane == 0) {
-        const double ratio = (st == 0 && M > 0) ? (double)n / (double)M : 0.0;
+        const int nr = ratio_inl ? ratio_inl[p] : n;
+        const double ratio = (st == 0 && M > 0) ? (double)nr / (double)M : 0.0;
         const bool fail = ratio < min_ratio || (n > 0 && n < min_inliers);
         isp_ok[p] = (st == 0 && !fail) ? 1 : 0;
     }
@@ -84,9 +86,9 @@ __global__ __launch_bounds__(256) void compact_rows_kernel(const uint2* __restri
 extern "C" {
 
 int gtsfm_compact_verified(const uint32_t* d_match_idx, const int* d_match_count, int mcap,
-                           const uint8_t* d_inlier_mask, const int* d_status, const int* d_n_inliers, int n_pairs,
-                           int min_inliers, double min_inlier_ratio, int* d_offsets, uint32_t* d_v_corr, int capacity,
-                           uint8_t* d_isp_ok, void* stream_v) {
+                           const uint8_t* d_inlier_mask, const int* d_status, const int* d_n_inliers,
+                           const int* d_ratio_inliers, int n_pairs, int min_inliers, double min_inlier_ratio,
+                           int* d_offsets, uint32_t* d_v_corr, int capacity, uint8_t* d_isp_ok, void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
     if (n_pairs < 0 || mcap < 0 || capacity < 0) return GTSFM_ERR_ARG;
     if (!d_offsets) return GTSFM_ERR_ARG;
@@ -101,7 +103,7 @@ int gtsfm_compact_verified(const uint32_t* d_match_idx, const int* d_match_count
                        d_offsets);
     GTSFM_CHECK_HIP(hipGetLastError());
     hipLaunchKernelGGL(compact_rows_kernel, dim3((n_pairs + 3) / 4), dim3(256), 0, stream, (const uint2*)d_match_idx,
-                       d_match_count, mcap, d_inlier_mask, d_status, d_n_inliers, n_pairs, min_inliers,
+                       d_match_count, mcap, d_inlier_mask, d_status, d_n_inliers, d_ratio_inliers, n_pairs, min_inliers,
                        min_inlier_ratio, d_offsets, capacity, (uint2*)d_v_corr, d_isp_ok);
     GTSFM_CHECK_HIP(hipGetLastError());
     return GTSFM_OK;

@@ -110,9 +110,11 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
 def compact_verified(match_idx: torch.Tensor, match_count: torch.Tensor, res: "RansacResult", min_inliers: int,
                      min_inlier_ratio: float, capacity: int, out_offsets: Optional[torch.Tensor] = None,
                      out_v_corr: Optional[torch.Tensor] = None, out_isp_ok: Optional[torch.Tensor] = None,
-                     stream: Optional[torch.cuda.Stream] = None
+                     stream: Optional[torch.cuda.Stream] = None, ratio_inliers: Optional[torch.Tensor] = None
                      ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Inlier rows of every pair, concatenated in pair order, + the inlier-support verdict (gtsfm_compact_verified).
+    `res` supplies mask / status / n_inliers (a RansacResult, or a BA2Result for the post-BA rows); ratio_inliers
+    optionally gives the counts the inlier ratio is taken on (the pre-BA ones after BA).
 
     Returns offsets (P + 1,) int32, v_corr (capacity, 2) int32 holding uint32 indices (rows offsets[p] ..
     offsets[p + 1] belong to pair p, matcher order), isp_ok (P,) uint8.
@@ -126,11 +128,53 @@ def compact_verified(match_idx: torch.Tensor, match_count: torch.Tensor, res: "R
     isp_ok = out_isp_ok if out_isp_ok is not None else torch.empty(max(P, 1), dtype=torch.uint8, device=dev)
     assert offsets.numel() >= P + 1 and v_corr.shape[0] >= capacity and isp_ok.numel() >= P
     rc = native.lib().gtsfm_compact_verified(_ptr(match_idx), _ptr(match_count), mcap, _ptr(res.mask),
-                                             _ptr(res.status), _ptr(res.n_inliers), P, int(min_inliers),
+                                             _ptr(res.status), _ptr(res.n_inliers), _ptr(ratio_inliers), P,
+                                             int(min_inliers),
                                              float(min_inlier_ratio), _ptr(offsets), _ptr(v_corr), int(capacity),
                                              _ptr(isp_ok), native.stream_handle(stream))
     native.check(rc, "gtsfm_compact_verified")
     return offsets, v_corr, isp_ok
+
+
+class BA2Result:
+    """Post-BA per-pair outputs (device tensors): R (i2Ri1), t (unit i2ti1), mask (P, mcap) over the putatives,
+    n_inliers (its row count), ba_status (0 ok, 1 no track, 2 none valid, 3 not run), iters, and `status` = the
+    verifier's status (what the reference's R is None / not None follows)."""
+
+    def __init__(self, R, t, mask, n_inliers, ba_status, iters, status):
+        self.R, self.t, self.mask, self.n_inliers = R, t, mask, n_inliers
+        self.ba_status, self.iters, self.status = ba_status, iters, status
+
+
+def bundle_adjust_2view(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
+                        match_count: torch.Tensor, res: "RansacResult", min_inliers: int = 15, max_iters: int = 100,
+                        reproj_thresh: float = 0.5, tri_thresh: float = 100.0,
+                        stream: Optional[torch.cuda.Stream] = None) -> BA2Result:
+    """Two-view triangulation + bundle adjustment of every verified pair (gtsfm_ba2_batched) on the verifier's
+    outputs `res` (same tensors as ransac_essential took)."""
+    assert kp_xy.is_cuda and kp_xy.dtype == torch.float32 and kp_xy.is_contiguous()
+    assert intrinsics.dtype == torch.float64 and match_idx.dtype == torch.int32 and match_idx.is_contiguous()
+    n_img, kmax = kp_xy.shape[0], kp_xy.shape[1]
+    P, mcap = match_idx.shape[0], match_idx.shape[1]
+    dev = kp_xy.device
+    L = native.lib()
+    R = torch.zeros((max(P, 1), 3, 3), dtype=torch.float64, device=dev)
+    t = torch.zeros((max(P, 1), 3), dtype=torch.float64, device=dev)
+    mask = torch.zeros((max(P, 1), max(mcap, 1)), dtype=torch.uint8, device=dev)
+    n_out = torch.zeros(max(P, 1), dtype=torch.int32, device=dev)
+    st = torch.zeros_like(n_out)
+    iters = torch.zeros_like(n_out)
+    if P > 0:
+        ws = _workspace(L.gtsfm_ba2_workspace_bytes(P, mcap), dev)
+        if stream is not None:
+            ws.record_stream(stream)
+        rc = L.gtsfm_ba2_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
+                                 _ptr(match_count), mcap, _ptr(res.mask), _ptr(res.R.contiguous()),
+                                 _ptr(res.t.contiguous()), _ptr(res.status), int(min_inliers), int(max_iters),
+                                 float(reproj_thresh), float(tri_thresh), _ptr(ws), ws.numel(), _ptr(R), _ptr(t),
+                                 _ptr(mask), _ptr(n_out), _ptr(st), _ptr(iters), native.stream_handle(stream))
+        native.check(rc, "gtsfm_ba2_batched")
+    return BA2Result(R[:P], t[:P], mask[:P], n_out[:P], st[:P], iters[:P], res.status)
 
 
 def sampson_sq(F: torch.Tensor, row_pair: torch.Tensor, x1: torch.Tensor, x2: torch.Tensor,

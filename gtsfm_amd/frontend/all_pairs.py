@@ -10,7 +10,9 @@ detect_and_describe task per image, one match task per pair) followed by `run_tw
    SIFT runs on the previous chunk (`kernels.sift`, one batched launch sequence per chunk).
 2. The one exchange (N > 1): all-gather of the padded per-rank feature blocks (gtsfm_amd/frontend/sharding.py).
 3. Per block of pairs: mutual-NN + ratio matching (`kernels.match`), 5-point RANSAC + LO + recoverPose
-   (`kernels.verify`), then compaction of the verified rows + the inlier-support verdict (`kernels.compact`).
+   (`kernels.verify`), optionally the two-view triangulation + bundle adjustment (`kernels.bundle_adjust`,
+   TwoViewEstimator's bundle_adjust_2view), then compaction of the verified rows + the inlier-support verdict
+   (`kernels.compact`).
 4. D2H of the compact results into pinned host buffers: fixed-size per-pair records first, then exactly the verified
    rows once their total is known.
 
@@ -41,6 +43,10 @@ class FrontEndConfig:
     extract_first: int = 20          # host steps: size of a smaller first chunk (less exposed H2D); 0 = extract_chunk
     resident_chunk: int = 100        # device-resident steps: images per SIFT launch sequence (bounded by workspace)
     pair_chunk: int = 32768          # pairs per match / verify / compact launch sequence
+    bundle_adjust: bool = False      # TwoViewEstimator bundle_adjust_2view: two-view triangulation + BA after RANSAC
+    ba_max_iters: int = 100          # bundle_adjust_2view_maxiters
+    ba_reproj_thresh: float = 0.5    # ba_reproj_error_thresholds[-1]
+    tri_reproj_thresh: float = 100.0  # TriangulationOptions.reproj_error_threshold (sift_front_end.yaml)
 
 
 class HipKernels:
@@ -65,9 +71,14 @@ class HipKernels:
     def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_id_base):
         return self._dev.ransac_essential(xy, intr, pairs, idx, cnt, thresh_px, pair_id_base=pair_id_base)
 
-    def compact(self, idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets, out_v_corr, out_isp_ok):
+    def bundle_adjust(self, xy, intr, pairs, idx, cnt, res, min_inliers, max_iters, reproj_thresh, tri_thresh):
+        return self._dev.bundle_adjust_2view(xy, intr, pairs, idx, cnt, res, min_inliers, max_iters, reproj_thresh,
+                                             tri_thresh)
+
+    def compact(self, idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets, out_v_corr, out_isp_ok,
+                ratio_inliers=None):
         self._dev.compact_verified(idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets=out_offsets,
-                                   out_v_corr=out_v_corr, out_isp_ok=out_isp_ok)
+                                   out_v_corr=out_v_corr, out_isp_ok=out_isp_ok, ratio_inliers=ratio_inliers)
 
 
 class Features:
@@ -248,12 +259,19 @@ class AllPairsFrontEnd:
             self._mark("match")
             res = self.kern.verify(xy_all, self.intr, pairs, idx, mcnt, cfg.thresh_px, self.pair_id_base + a)
             self._mark("verify")
-            self.kern.compact(idx, mcnt, res, cfg.min_inliers, cfg.min_inlier_ratio, (b - a) * k,
-                              self.d_offsets[a + c: b + c + 1], self.d_v_corr[a * k: b * k], self.d_isp_ok[a:b])
-            self.d_fixed[a:b, :9] = res.R.reshape(-1, 9)
-            self.d_fixed[a:b, 9:] = res.t
+            out, ratio_inl = res, None
+            if cfg.bundle_adjust:
+                out = self.kern.bundle_adjust(xy_all, self.intr, pairs, idx, mcnt, res, cfg.min_inliers,
+                                              cfg.ba_max_iters, cfg.ba_reproj_thresh, cfg.tri_reproj_thresh)
+                ratio_inl = res.n_inliers  # the post-BA report keeps the pre-BA inlier ratio
+                self._mark("bundle_adjust")
+            self.kern.compact(idx, mcnt, out, cfg.min_inliers, cfg.min_inlier_ratio, (b - a) * k,
+                              self.d_offsets[a + c: b + c + 1], self.d_v_corr[a * k: b * k], self.d_isp_ok[a:b],
+                              ratio_inliers=ratio_inl)
+            self.d_fixed[a:b, :9] = out.R.reshape(-1, 9)
+            self.d_fixed[a:b, 9:] = out.t
             self.d_ints[a:b, 0] = res.status
-            self.d_ints[a:b, 1] = res.n_inliers
+            self.d_ints[a:b, 1] = out.n_inliers
             self.d_ints[a:b, 2] = mcnt
             self._mark("compact")
             n_hyp.append(res.n_hyp)

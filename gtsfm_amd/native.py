@@ -41,6 +41,10 @@ RANSAC_STATUS_OK = 0
 RANSAC_STATUS_TOO_FEW = 1
 RANSAC_STATUS_NO_MODEL = 2
 RANSAC_DEFAULT_SEED = 0x5EED5EED
+BA2_STATUS_OK = 0
+BA2_STATUS_NO_TRACKS = 1
+BA2_STATUS_NONE_VALID = 2
+BA2_STATUS_NOT_RUN = 3
 
 # (name, restype, argtypes) of every symbol declared in include/gtsfm_hip.h
 SIGNATURES = {
@@ -84,8 +88,15 @@ SIGNATURES = {
     "gtsfm_superglue_log_assignment": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p]),
     "gtsfm_compact_verified": (
         c_int,
-        [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p, c_int,
-         c_void_p, c_void_p],
+        [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p,
+         c_int, c_void_p, c_void_p],
+    ),
+    "gtsfm_ba2_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "gtsfm_ba2_batched": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_int, c_int, c_double, c_double, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p],
     ),
     "gtsfm_sampson_sq_batched": (
         c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

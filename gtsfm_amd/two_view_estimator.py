@@ -5,10 +5,11 @@ Drop-in for gtsfm/two_view_estimator.py: `TwoViewEstimator.run_2view` (:276-351)
 the same TWO_VIEW_OUTPUT 6-tuple (i2Ri1, i2Ui1, v_corr_idxs, pre-BA report, post-BA report, post-ISP report).
 
 `run_two_view_estimator_as_futures` is where the batching happens: instead of one Dask task per pair, every pair
-goes through ONE batched RANSAC launch sequence (Ransac.verify_batch) and only the cheap report / ISP logic runs per
-pair on the host. Two-view bundle adjustment (:311-337) is out of scope for this build: with
-`bundle_adjust_2view=True` the post-BA outputs equal the pre-BA ones, exactly as the reference's own else-branch
-(:338-342) produces them, and a warning says so once.
+goes through ONE batched RANSAC launch sequence (Ransac.verify_batch), then -- with bundle_adjust_2view=True, as in
+every shipped configuration -- ONE batched two-view triangulation + bundle adjustment launch
+(gtsfm_ba2_batched: `bundle_adjust`, :136-208, on the pairs with >= min_num_inliers verified rows, :311), and only
+the cheap report / ISP logic runs per pair on the host. After BA the report keeps the pre-BA inlier ratio, as the
+reference does (:325-327). Relative-pose priors on the BA path are not supported (the runner passes none).
 """
 from __future__ import annotations
 
@@ -18,6 +19,8 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 from scipy.spatial.transform import Rotation
+
+import math
 
 from gtsfm_amd.common import geometry
 from gtsfm_amd.common.keypoints import Keypoints
@@ -74,6 +77,9 @@ def generate_two_view_report(inlier_ratio_est_model: float, v_corr_idxs: np.ndar
         inlier_avg_reproj_error_gt_model=inl_err, outlier_avg_reproj_error_gt_model=out_err)
 
 
+BA_PAIR_CHUNK = 8192
+
+
 class TwoViewEstimator:
     def __init__(self, verifier: VerifierBase, inlier_support_processor: InlierSupportProcessor,
                  bundle_adjust_2view: bool, eval_threshold_px: float, triangulation_options: Any = None,
@@ -86,8 +92,105 @@ class TwoViewEstimator:
         self._triangulation_options = triangulation_options
         self._ba_reproj_error_thresholds = ba_reproj_error_thresholds
         self._bundle_adjust_2view_maxiters = bundle_adjust_2view_maxiters
-        if bundle_adjust_2view:
-            logger.warning("two-view BA is not part of the MI355X front-end (SURVEY.md §8 f2): post-BA = pre-BA")
+
+    # ---------------------------------------------------------------- two-view bundle adjustment (:101-208)
+    def _ba_params(self) -> Tuple[int, int, float, float]:
+        """(min verified rows, max LM iterations, post-BA reprojection threshold, triangulation threshold)."""
+        opts = self._triangulation_options
+        mode = getattr(opts, "mode", "NO_RANSAC")
+        if str(getattr(mode, "value", mode)) != "NO_RANSAC":
+            raise NotImplementedError("two-view triangulation supports TriangulationSamplingMode.NO_RANSAC only")
+        if getattr(opts, "min_triangulation_angle", 0.0):
+            raise NotImplementedError("min_triangulation_angle > 0 is not supported on the MI355X BA path")
+        tri = getattr(opts, "reproj_error_threshold", math.inf)
+        # run_ba repeats the stage from the same initial data for every threshold; the last stage's output is kept
+        # (bundle_adjustment.py:396-419)
+        thr = self._ba_reproj_error_thresholds[-1] if self._ba_reproj_error_thresholds else None
+        min_inl = self.processor._min_num_inliers_est_model if self.processor is not None else 0
+        return (min_inl, int(self._bundle_adjust_2view_maxiters or 0) or 1000000,
+                1e300 if thr is None else float(thr), 1e300 if tri is None or math.isinf(tri) else float(tri))
+
+    def bundle_adjust_batch(self, keypoints_list: Sequence[Keypoints],
+                            jobs: Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]], camera_intrinsics: Sequence
+                            ) -> Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]]:
+        """bundle_adjust (:136-208) of every (i1, i2) -> (i2Ri1, i2Ui1, verified_corr_idxs) job in batched
+        gtsfm_ba2_batched launches; returns (i2Ri1, i2Ui1, valid_corr_idxs) per job, as the reference returns them:
+        the initial pose and an empty (0, 2) int32 array when nothing triangulates, the initial pose and the (empty)
+        valid rows when BA leaves no valid track."""
+        import torch
+
+        from gtsfm_amd import device, native
+
+        native.require_gpu()
+        _, max_iters, thr, tri = self._ba_params()
+        out: Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]] = {}
+        keys = [k for k, (R, U, _) in jobs.items() if R is not None and U is not None]
+        for k in jobs:
+            if k not in keys:
+                out[k] = (None, None, jobs[k][2])
+        if not keys:
+            return out
+        dev = torch.device("cuda")
+        n = len(keypoints_list)
+        kmax = max([len(k) for k in keypoints_list] + [1])
+        kp = np.zeros((n, kmax, 2), np.float32)
+        for i, k in enumerate(keypoints_list):
+            kp[i, : len(k)] = k.coordinates
+        intr = np.zeros((n, 3))
+        used = {i for key in keys for i in key}
+        for i in used:
+            intr[i] = geometry.calibration_params(camera_intrinsics[i])
+        kp_d, intr_d = torch.from_numpy(kp).to(dev), torch.from_numpy(intr).to(dev)
+
+        class _Verified:
+            pass
+
+        for s in range(0, len(keys), BA_PAIR_CHUNK):
+            blk = keys[s: s + BA_PAIR_CHUNK]
+            rows = [np.asarray(jobs[k][2]).reshape(-1, 2) for k in blk]
+            mcap = max([len(r) for r in rows] + [1])
+            idx = np.zeros((len(blk), mcap, 2), np.int32)
+            cnt = np.zeros(len(blk), np.int32)
+            mask = np.zeros((len(blk), mcap), np.uint8)
+            R0 = np.zeros((len(blk), 3, 3))
+            t0 = np.zeros((len(blk), 3))
+            for j, (k, r) in enumerate(zip(blk, rows)):
+                idx[j, : len(r)] = r.astype(np.int64)
+                cnt[j] = len(r)
+                mask[j, : len(r)] = 1
+                R0[j] = geometry.rotation_matrix(jobs[k][0])
+                t0[j] = geometry.unit_vector(jobs[k][1])
+            v = _Verified()
+            v.mask, v.R, v.t = (torch.from_numpy(x).to(dev) for x in (mask, R0, t0))
+            v.status = torch.zeros(len(blk), dtype=torch.int32, device=dev)
+            res = device.bundle_adjust_2view(kp_d, intr_d, torch.tensor(blk, dtype=torch.int32, device=dev),
+                                             torch.from_numpy(idx).to(dev), torch.from_numpy(cnt).to(dev), v,
+                                             min_inliers=0, max_iters=max_iters, reproj_thresh=thr, tri_thresh=tri)
+            st = res.ba_status.cpu().numpy()
+            R, t, m = res.R.cpu().numpy(), res.t.cpu().numpy(), res.mask.cpu().numpy().astype(bool)
+            for j, (k, r) in enumerate(zip(blk, rows)):
+                if st[j] == native.BA2_STATUS_NO_TRACKS:
+                    out[k] = (jobs[k][0], jobs[k][1], np.zeros((0, 2), dtype=np.int32))
+                elif st[j] == native.BA2_STATUS_NONE_VALID:
+                    out[k] = (jobs[k][0], jobs[k][1], np.asarray(jobs[k][2]).reshape(-1, 2)[:0])
+                else:
+                    out[k] = (geometry.Rot3(R[j]), geometry.Unit3(t[j]),
+                              np.asarray(jobs[k][2]).reshape(-1, 2)[m[j, : len(r)]])
+        return out
+
+    def bundle_adjust(self, keypoints_i1: Keypoints, keypoints_i2: Keypoints, verified_corr_idxs: np.ndarray,
+                      camera_intrinsics_i1, camera_intrinsics_i2, i2Ri1_initial, i2Ui1_initial, i2Ti1_prior=None):
+        """Drop-in for TwoViewEstimator.bundle_adjust (:136-208): one pair through the batched kernel."""
+        if i2Ti1_prior is not None:
+            raise NotImplementedError("relative pose priors are not supported on the MI355X two-view BA path")
+        if i2Ri1_initial is None or i2Ui1_initial is None:
+            return None, None, verified_corr_idxs
+        return self.bundle_adjust_batch([keypoints_i1, keypoints_i2],
+                                        {(0, 1): (i2Ri1_initial, i2Ui1_initial, verified_corr_idxs)},
+                                        [camera_intrinsics_i1, camera_intrinsics_i2])[(0, 1)]
+
+    def _wants_ba(self, v_corr) -> bool:
+        return self._bundle_adjust_2view and len(v_corr) >= self.processor._min_num_inliers_est_model
 
     def get_corr_metric_dist_threshold(self) -> float:
         return self._corr_metric_dist_threshold
@@ -106,14 +209,21 @@ class TwoViewEstimator:
         return generate_two_view_report(ratio, v_corr, R_error_deg=R_err, U_error_deg=U_err,
                                         v_corr_idxs_inlier_mask_gt=mask_gt, reproj_error_gt_model=err_gt)
 
-    def _finish(self, verified, keypoints_i1, keypoints_i2, gt_camera_i1, gt_camera_i2,
-                gt_scene_mesh=None) -> TWO_VIEW_OUTPUT:
-        """Report + (skipped) BA + inlier-support processor for one verifier result (:298-351)."""
+    def _finish(self, verified, keypoints_i1, keypoints_i2, gt_camera_i1, gt_camera_i2, gt_scene_mesh=None,
+                post_ba=None) -> TWO_VIEW_OUTPUT:
+        """Reports + inlier-support processor for one verifier result and its BA result, if BA ran (:298-351)."""
         i2Ri1, i2Ui1, v_corr, ratio = verified
         pre_ba_report = self._report(i2Ri1, i2Ui1, keypoints_i1, keypoints_i2, v_corr, ratio, gt_camera_i1,
                                      gt_camera_i2, gt_scene_mesh)
-        post_ba_report = dataclasses.replace(pre_ba_report)
-        post_isp = self.processor.run_inlier_support(i2Ri1, i2Ui1, v_corr, post_ba_report)
+        if post_ba is not None:
+            R_b, U_b, v_b = post_ba
+            # the reference keeps the pre-BA inlier ratio after BA (:325-327)
+            post_ba_report = self._report(R_b, U_b, keypoints_i1, keypoints_i2, v_b, ratio, gt_camera_i1,
+                                          gt_camera_i2, gt_scene_mesh)
+        else:
+            R_b, U_b, v_b = i2Ri1, i2Ui1, v_corr
+            post_ba_report = dataclasses.replace(pre_ba_report)
+        post_isp = self.processor.run_inlier_support(R_b, U_b, v_b, post_ba_report)
         return post_isp[0], post_isp[1], post_isp[2], pre_ba_report, post_ba_report, post_isp[3]
 
     def run_2view(self, keypoints_i1: Keypoints, keypoints_i2: Keypoints, putative_corr_idxs: np.ndarray,
@@ -121,7 +231,11 @@ class TwoViewEstimator:
                   gt_camera_i2=None, gt_scene_mesh=None) -> TWO_VIEW_OUTPUT:
         verified = self._verifier.verify(keypoints_i1, keypoints_i2, putative_corr_idxs, camera_intrinsics_i1,
                                          camera_intrinsics_i2)
-        return self._finish(verified, keypoints_i1, keypoints_i2, gt_camera_i1, gt_camera_i2, gt_scene_mesh)
+        post_ba = None
+        if self._wants_ba(verified[2]):
+            post_ba = self.bundle_adjust(keypoints_i1, keypoints_i2, verified[2], camera_intrinsics_i1,
+                                         camera_intrinsics_i2, verified[0], verified[1], i2Ti1_prior)
+        return self._finish(verified, keypoints_i1, keypoints_i2, gt_camera_i1, gt_camera_i2, gt_scene_mesh, post_ba)
 
 
 def run_two_view_estimator_as_futures(
@@ -155,9 +269,15 @@ def run_two_view_estimator_as_futures(
         verified = {(i1, i2): verifier.verify(keypoints_list[i1], keypoints_list[i2], m, camera_intrinsics[i1],
                                               camera_intrinsics[i2])
                     for (i1, i2), m in todo.items()}
+    post_ba: Dict[Tuple[int, int], Any] = {}
+    ba_jobs = {k: verified[k][:3] for k in todo if two_view_estimator._wants_ba(verified[k][2])}
+    if ba_jobs:
+        if any((relative_pose_priors or {}).get(k) is not None for k in ba_jobs):
+            raise NotImplementedError("relative pose priors are not supported on the MI355X two-view BA path")
+        post_ba = two_view_estimator.bundle_adjust_batch(keypoints_list, ba_jobs, camera_intrinsics)
     for (i1, i2), m in todo.items():
         results[(i1, i2)] = two_view_estimator._finish(verified[(i1, i2)], keypoints_list[i1], keypoints_list[i2],
-                                                       gt[i1], gt[i2], gt_scene_mesh)
+                                                       gt[i1], gt[i2], gt_scene_mesh, post_ba.get((i1, i2)))
         if cached is not None:
             two_view_estimator.cache_store(keypoints_list[i1], keypoints_list[i2], m, results[(i1, i2)])
     return {k: results[k] for k in putative_corr_idxs_dict}

@@ -120,7 +120,35 @@ int gtsfm_ransac_F_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            int* d_n_inliers, int* d_status, int* d_n_hyp, uint8_t* d_inlier_mask, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
+ * Two-view triangulation + bundle adjustment. Replaces TwoViewEstimator.bundle_adjust and the run_2view branch
+ * that calls it (gtsfm/two_view_estimator.py:101-208, 311-337; gtsam.triangulatePoint3 + the 2-view
+ * BundleAdjustmentOptimizer, bundle/bundle_adjustment.py:269-275, 359-419), batched over pairs; the restatement is
+ * oracle/ba2.c (calibrations held fixed; the reference's sigma 1e-5 prior pins them).
+ * Inputs: the verifier's keypoints / intrinsics / pairs / putatives exactly as gtsfm_ransac_E_batched takes them,
+ * its inlier mask d_in_mask[n_pairs][mcap] (the pre-BA verified rows), i2Ri1 d_R_in[n_pairs][9], unit i2ti1
+ * d_t_in[n_pairs][3] and status d_status_in (0 = verified). Per pair with status 0 and >= min_inliers verified rows:
+ * every verified row is triangulated (DLT + LM point refinement, cheirality, reprojection < tri_thresh px), the
+ * 2-view BA runs (Huber 1.345 on 1 px, X0 prior 0.1, first-point prior 0.1, Levenberg-Marquardt <= max_iters
+ * iterations), and rows whose two reprojections stay < reproj_thresh px survive (filter_landmarks).
+ * Outputs: d_R_out / d_t_out (post-BA i2Ri1, unit i2ti1; the inputs when BA did not produce a pose),
+ * d_out_mask[n_pairs][mcap] (post-BA verified rows; the input mask when BA did not run), d_n_out (its count),
+ * d_status_out (0 BA ok, 1 no track triangulated, 2 no track valid after BA, 3 not run), d_iters (LM iterations,
+ * may be NULL).
+ * ---------------------------------------------------------------------------------------------- */
+size_t gtsfm_ba2_workspace_bytes(int n_pairs, int mcap);
+
+int gtsfm_ba2_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
+                      int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
+                      const uint8_t* d_in_mask, const double* d_R_in, const double* d_t_in, const int* d_status_in,
+                      int min_inliers, int max_iters, double reproj_thresh, double tri_thresh, void* d_workspace,
+                      size_t workspace_bytes, double* d_R_out, double* d_t_out, uint8_t* d_out_mask, int* d_n_out,
+                      int* d_status_out, int* d_iters, void* stream);
+
+/* ----------------------------------------------------------------------------------------------
  * Verified-correspondence compaction + inlier-support filter (the device half of the hand-off to the host).
+ * d_n_inliers are the rows of d_inlier_mask each pair keeps (the verifier's counts, or gtsfm_ba2_batched's post-BA
+ * counts with its mask); inlier_ratio = d_n_inliers / d_match_count unless d_ratio_inliers (may be NULL) gives the
+ * count the ratio is taken on (the reference keeps the pre-BA ratio after BA: two_view_estimator.py:326-327).
  * Replaces, for every pair at once: v_corr_idxs = match_indices[mask == 1] and inlier_ratio = mean(mask)
  * (gtsfm/frontend/verifier/opencv_verifier_base.py:98-101) and InlierSupportProcessor.run_inlier_support
  * (gtsfm/frontend/inlier_support_processor.py:73-87: fail iff ratio < min_inlier_ratio or 0 < n < min_inliers).
@@ -131,9 +159,9 @@ int gtsfm_ransac_F_batched(const float* d_kp_xy, const double* d_intrinsics, int
  * verified and passes the inlier-support filter.
  * ---------------------------------------------------------------------------------------------- */
 int gtsfm_compact_verified(const uint32_t* d_match_idx, const int* d_match_count, int mcap,
-                           const uint8_t* d_inlier_mask, const int* d_status, const int* d_n_inliers, int n_pairs,
-                           int min_inliers, double min_inlier_ratio, int* d_offsets, uint32_t* d_v_corr, int capacity,
-                           uint8_t* d_isp_ok, void* stream);
+                           const uint8_t* d_inlier_mask, const int* d_status, const int* d_n_inliers,
+                           const int* d_ratio_inliers, int n_pairs, int min_inliers, double min_inlier_ratio,
+                           int* d_offsets, uint32_t* d_v_corr, int capacity, uint8_t* d_isp_ok, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
  * Squared Sampson distances. Replaces gtsfm/utils/verification.py:170-214 compute_epipolar_distances_sq_sampson (the

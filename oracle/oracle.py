@@ -62,6 +62,11 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_sampson_sq.argtypes = [_f64p, _f64p, _f64p, ctypes.c_int, ctypes.c_int, _f64p]
         l.oracle_recover_pose.restype = ctypes.c_int
         l.oracle_recover_pose.argtypes = [_f64p, _f64p, _f64p, ctypes.c_void_p, ctypes.c_int, _f64p, _f64p]
+    if hasattr(l, "oracle_ba2"):
+        l.oracle_ba2.restype = ctypes.c_int
+        l.oracle_ba2.argtypes = [_f64p, _f64p, ctypes.c_int, _f64p, _f64p, _f64p, _f64p, ctypes.c_int, ctypes.c_double,
+                                 ctypes.c_double, _f64p, _f64p, _u8p, ctypes.POINTER(ctypes.c_int),
+                                 ctypes.POINTER(ctypes.c_double)]
     if hasattr(l, "oracle_ransac_F"):
         l.oracle_ransac_F.restype = ctypes.c_int
         l.oracle_ransac_F.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
@@ -210,6 +215,22 @@ def recover_pose(E: np.ndarray, x1n: np.ndarray, x2n: np.ndarray):
     good = lib().oracle_recover_pose(np.ascontiguousarray(E, np.float64).ravel(), x1n.ravel(), x2n.ravel(), None,
                                      x1n.shape[0], R, t)
     return R.reshape(3, 3), t, good
+
+
+def ba2(uv1: np.ndarray, uv2: np.ndarray, K1, K2, R: np.ndarray, t: np.ndarray, max_iters: int = 100,
+        reproj_thresh: float = 0.5, tri_thresh: float = 100.0):
+    """Two-view triangulation + bundle adjustment (oracle/ba2.c). K = (f, u0, v0). Returns
+    (status, R_out, t_out, valid (n,) bool, LM iterations, final error); status 0 ok / 1 no track / 2 none valid."""
+    uv1 = np.ascontiguousarray(uv1, np.float64).reshape(-1, 2)
+    uv2 = np.ascontiguousarray(uv2, np.float64).reshape(-1, 2)
+    n = len(uv1)
+    Ro, to = np.zeros(9), np.zeros(3)
+    valid = np.zeros(max(n, 1), np.uint8)
+    it, err = ctypes.c_int(0), ctypes.c_double(0)
+    st = lib().oracle_ba2(uv1.ravel(), uv2.ravel(), n, np.asarray(K1, np.float64), np.asarray(K2, np.float64),
+                          np.ascontiguousarray(R, np.float64).ravel(), np.ascontiguousarray(t, np.float64).ravel(),
+                          max_iters, reproj_thresh, tri_thresh, Ro, to, valid, ctypes.byref(it), ctypes.byref(err))
+    return st, Ro.reshape(3, 3), to, valid[:n].astype(bool), it.value, err.value
 
 
 def rgb_to_gray(rgb: np.ndarray) -> np.ndarray:

@@ -78,14 +78,40 @@ class OracleKernels:
             res.mask[p, :M] = torch.from_numpy(mask)
         return res
 
-    def compact(self, idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets, out_v_corr, out_isp_ok):
+    def bundle_adjust(self, xy, intr, pairs, idx, cnt, res, min_inliers, max_iters, reproj_thresh, tri_thresh):
+        """oracle/ba2.c on every verified pair with >= min_inliers rows (two_view_estimator.py:311-337)."""
+        P, mcap = idx.shape[0], idx.shape[1]
+        out = OracleRansacResult(P, mcap)
+        out.status = res.status.clone()
+        for p in range(P):
+            M = int(cnt[p])
+            rows = np.flatnonzero(res.mask[p, :M].numpy())
+            out.R[p], out.t[p] = res.R[p], res.t[p]
+            if int(res.status[p]) != 0 or len(rows) < min_inliers:
+                out.mask[p] = res.mask[p]
+                out.n_inliers[p] = len(rows)
+                continue
+            i1, i2 = int(pairs[p, 0]), int(pairs[p, 1])
+            m = idx[p, rows].numpy().astype(np.int64)
+            uv1 = xy[i1, m[:, 0]].numpy().astype(np.float64)
+            uv2 = xy[i2, m[:, 1]].numpy().astype(np.float64)
+            st, R, t, valid, _, _ = oracle.ba2(uv1, uv2, intr[i1].numpy(), intr[i2].numpy(), res.R[p].numpy(),
+                                               res.t[p].numpy(), max_iters, reproj_thresh, tri_thresh)
+            out.R[p], out.t[p] = torch.from_numpy(R), torch.from_numpy(t)
+            out.mask[p, rows[valid]] = 1
+            out.n_inliers[p] = int(valid.sum())
+        return out
+
+    def compact(self, idx, cnt, res, min_inliers, min_ratio, capacity, out_offsets, out_v_corr, out_isp_ok,
+                ratio_inliers=None):
         """numpy restatement of gtsfm_compact_verified (opencv_verifier_base.py:98-101 +
         inlier_support_processor.py:73-87)."""
         pos = 0
         for p in range(idx.shape[0]):
             out_offsets[p] = pos
             st, n, M = int(res.status[p]), int(res.n_inliers[p]), int(cnt[p])
-            ratio = n / M if (st == 0 and M > 0) else 0.0
+            nr = n if ratio_inliers is None else int(ratio_inliers[p])
+            ratio = nr / M if (st == 0 and M > 0) else 0.0
             out_isp_ok[p] = int(st == 0 and not (ratio < min_ratio or (0 < n < min_inliers)))
             if st != 0:
                 continue

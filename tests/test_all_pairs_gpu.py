@@ -123,3 +123,33 @@ def test_engine_host_to_host_matches_oracle_engine(dev):
     gpu.step(resident=True)
     torch.cuda.synchronize()
     assert torch.equal(gpu.d_v_corr, before)
+
+
+def test_engine_with_two_view_bundle_adjustment(dev):
+    """bundle_adjust_2view=True (every shipped config): RANSAC -> two-view triangulation + BA -> compaction + ISP on
+    the post-BA rows with the pre-BA inlier ratio, against the same engine on the oracle kernels (RANSAC masks differ
+    within 1 %, so BA sees slightly different rows: counts within 2 % + 2, poses within 0.1 deg)."""
+    from gtsfm_amd import synthetic
+    from gtsfm_amd.frontend import sharding
+    from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig
+    from oracle_kernels import OracleKernels
+
+    n_img = 5
+    scene = synthetic.render_scene(24, 360, 480, device="cuda", indices=range(n_img))
+    cfg = FrontEndConfig(kpts=600, extract_chunk=3, pair_chunk=4, bundle_adjust=True)
+    mine = sharding.local_images(n_img, 1, 0)
+    host = scene.images[mine].cpu()
+    gpu = AllPairsFrontEnd(host, scene.intrinsics[:n_img], n_img, 0, 1, dev, cfg).step()
+    ref = AllPairsFrontEnd(host, scene.intrinsics[:n_img], n_img, 0, 1, torch.device("cpu"), cfg,
+                           kernels=OracleKernels()).step()
+    np.testing.assert_array_equal(gpu.status, ref.status)
+    ran = 0
+    for p in range(len(gpu.pairs)):
+        if gpu.status[p] != 0:
+            continue
+        n, rn = int(gpu.n_inliers[p]), int(ref.n_inliers[p])
+        assert abs(n - rn) <= 0.02 * rn + 2, (p, n, rn)
+        assert len(gpu.verified(p)) == n
+        assert scenes.rotation_angle_deg(gpu.R[p], ref.R[p]) < 0.1
+        ran += int(n > 0)
+    assert ran >= 4

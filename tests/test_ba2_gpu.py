@@ -1,0 +1,92 @@
+"""GPU two-view triangulation + bundle adjustment (gtsfm_ba2_batched) against the oracle (oracle/ba2.c).
+
+One batched launch over pairs that exercise every branch of the reference's bundle_adjust / run_2view guard
+(two_view_estimator.py:136-208, 311-337): noisy pairs with outliers (BA runs, the 0.5 px filter drops rows), an
+exact five-point pair (the reference test's shape: <= 1 degree, all rows kept), a pair below min_inliers and a failed
+verification (not run: the pre-BA mask and pose pass through), and a pair whose points all triangulate behind a
+camera. Same fp64 algorithm on both sides, the sums over tracks reduced in a different order: statuses and LM
+iteration counts equal, poses within 1e-6 degrees, post-BA masks equal up to one row per pair (a row whose
+reprojection error sits within rounding of 0.5 px).
+"""
+import numpy as np
+import pytest
+import torch
+
+from tests import ba2_scenes
+
+pytestmark = pytest.mark.gpu
+
+
+class _Verified:
+    """The verifier outputs gtsfm_ba2_batched consumes."""
+
+    def __init__(self, mask, R, t, status):
+        self.mask, self.R, self.t, self.status = mask, R, t, status
+
+
+def test_ba2_batch_vs_oracle(oracle_mod):
+    from gtsfm_amd import device, native
+
+    native.require_gpu()
+    rng = np.random.default_rng(21)
+    scenes = [ba2_scenes.make_pair(rng, 600, noise_px=0.3, n_out=40),
+              ba2_scenes.make_pair(rng, 1500, noise_px=0.15, n_out=100, init_err_deg=0.8),
+              ba2_scenes.make_pair(rng, 5, noise_px=0.0, init_err_deg=0.0),
+              ba2_scenes.make_pair(rng, 12, noise_px=0.2),            # 12 < 15 verified rows: not run
+              ba2_scenes.make_pair(rng, 200, noise_px=0.2),           # verification failed: not run
+              ba2_scenes.make_pair(rng, 80, noise_px=0.1)]            # pose flipped: nothing in front
+    scenes[-1]["t0"] = -scenes[-1]["t0"]
+    P = len(scenes)
+    kmax = max(len(s["x1"]) for s in scenes)
+    n_img = 2 * P
+    kp = np.zeros((n_img, kmax, 2), np.float32)
+    intr = np.zeros((n_img, 3))
+    idx = np.zeros((P, kmax, 2), np.int32)
+    cnt = np.zeros(P, np.int32)
+    mask = np.zeros((P, kmax), np.uint8)
+    R0 = np.zeros((P, 3, 3))
+    t0 = np.zeros((P, 3))
+    status = np.zeros(P, np.int32)
+    for p, s in enumerate(scenes):
+        n = len(s["x1"])
+        perm = rng.permutation(n)  # keypoint order differs from the putative order
+        kp[2 * p, perm] = s["x1"]
+        kp[2 * p + 1, :n] = s["x2"]
+        idx[p, :n, 0] = perm
+        idx[p, :n, 1] = np.arange(n)
+        cnt[p] = n
+        mask[p, :n] = (rng.random(n) < 0.95) if p < 2 else 1  # pre-BA verified rows (a few putatives not)
+        intr[2 * p] = intr[2 * p + 1] = s["K"]
+        R0[p], t0[p] = s["R0"], s["t0"]
+    status[4] = native.RANSAC_STATUS_NO_MODEL
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    pairs = np.arange(n_img, dtype=np.int32).reshape(P, 2)
+    res = device.bundle_adjust_2view(t(kp), t(intr), t(pairs), t(idx), t(cnt),
+                                     _Verified(t(mask), t(R0), t(t0), t(status)))
+    g_st, g_R, g_t = res.ba_status.cpu().numpy(), res.R.cpu().numpy(), res.t.cpu().numpy()
+    g_mask, g_n, g_it = res.mask.cpu().numpy(), res.n_inliers.cpu().numpy(), res.iters.cpu().numpy()
+    expect_status = [0, 0, 0, 3, 3, None]
+    for p, s in enumerate(scenes):
+        n = cnt[p]
+        rows = np.flatnonzero(mask[p, :n])
+        if expect_status[p] == 3:
+            assert g_st[p] == 3 and g_n[p] == len(rows)
+            np.testing.assert_array_equal(g_mask[p, :n], mask[p, :n])
+            np.testing.assert_array_equal(g_R[p], R0[p])
+            continue
+        uv1 = s["x1"][rows]
+        uv2 = s["x2"][rows]
+        o_st, o_R, o_t, o_valid, o_it, _ = oracle_mod.ba2(uv1, uv2, s["K"], s["K"], R0[p], t0[p])
+        assert g_st[p] == o_st, (p, g_st[p], o_st)
+        o_mask = np.zeros(n, np.uint8)
+        o_mask[rows[o_valid]] = 1
+        assert np.count_nonzero(g_mask[p, :n] != o_mask) <= 1, p
+        assert g_n[p] == g_mask[p, :n].sum()
+        if o_st == 0:
+            assert g_it[p] == o_it, (p, g_it[p], o_it)
+            assert ba2_scenes.angle_deg(g_R[p], o_R) < 1e-6
+            assert ba2_scenes.dir_deg(g_t[p], o_t) < 1e-6
+            assert ba2_scenes.angle_deg(g_R[p], s["R"]) <= 1.0 and ba2_scenes.dir_deg(g_t[p], s["t"]) <= 1.0
+        if p == 2:
+            assert o_st == 0 and o_valid.all()
