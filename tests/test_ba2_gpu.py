@@ -5,7 +5,7 @@ One batched launch over pairs that exercise every branch of the reference's bund
 exact five-point pair (the reference test's shape: <= 1 degree, all rows kept), a pair below min_inliers and a failed
 verification (not run: the pre-BA mask and pose pass through), and a pair whose points all triangulate behind a
 camera. Same fp64 algorithm on both sides, the sums over tracks reduced in a different order: statuses and LM
-iteration counts equal, poses within 1e-6 degrees, post-BA masks equal up to one row per pair (a row whose
+iteration counts equal, poses within 1e-4 degrees (arccos resolves ~1e-6), post-BA masks equal up to one row per pair (a row whose
 reprojection error sits within rounding of 0.5 px).
 """
 import numpy as np
@@ -66,7 +66,7 @@ def test_ba2_batch_vs_oracle(oracle_mod):
                                      _Verified(t(mask), t(R0), t(t0), t(status)))
     g_st, g_R, g_t = res.ba_status.cpu().numpy(), res.R.cpu().numpy(), res.t.cpu().numpy()
     g_mask, g_n, g_it = res.mask.cpu().numpy(), res.n_inliers.cpu().numpy(), res.iters.cpu().numpy()
-    expect_status = [0, 0, 0, 3, 3, None]
+    expect_status = [0, 0, 3, 3, 3, None]  # the five-point pair is below min_inliers here (run on its own below)
     for p, s in enumerate(scenes):
         n = cnt[p]
         rows = np.flatnonzero(mask[p, :n])
@@ -85,8 +85,16 @@ def test_ba2_batch_vs_oracle(oracle_mod):
         assert g_n[p] == g_mask[p, :n].sum()
         if o_st == 0:
             assert g_it[p] == o_it, (p, g_it[p], o_it)
-            assert ba2_scenes.angle_deg(g_R[p], o_R) < 1e-6
-            assert ba2_scenes.dir_deg(g_t[p], o_t) < 1e-6
+            assert ba2_scenes.angle_deg(g_R[p], o_R) < 1e-4
+            assert ba2_scenes.dir_deg(g_t[p], o_t) < 1e-4
             assert ba2_scenes.angle_deg(g_R[p], s["R"]) <= 1.0 and ba2_scenes.dir_deg(g_t[p], s["t"]) <= 1.0
-        if p == 2:
-            assert o_st == 0 and o_valid.all()
+    # the reference's unit test calls bundle_adjust directly (no min-inlier guard) on five exact correspondences
+    res5 = device.bundle_adjust_2view(t(kp[4:6]), t(intr[4:6]), t(np.array([[0, 1]], np.int32)), t(idx[2:3]),
+                                      t(cnt[2:3]), _Verified(t(mask[2:3]), t(R0[2:3]), t(t0[2:3]),
+                                                             t(np.zeros(1, np.int32))), min_inliers=0)
+    s = scenes[2]
+    assert int(res5.ba_status[0]) == 0 and int(res5.n_inliers[0]) == 5
+    R5, t5 = res5.R[0].cpu().numpy(), res5.t[0].cpu().numpy()
+    assert ba2_scenes.angle_deg(R5, s["R"]) <= 1.0 and ba2_scenes.dir_deg(t5, s["t"]) <= 1.0
+    o_st, o_R, o_t, o_valid, o_it, _ = oracle_mod.ba2(s["x1"], s["x2"], s["K"], s["K"], R0[2], t0[2])
+    assert o_st == 0 and o_valid.all() and ba2_scenes.angle_deg(R5, o_R) < 1e-4
