@@ -5,20 +5,18 @@
 // (:137), the stable sort by distance (:141), the query->train dict (:142) and the mutual filter in
 // 1->2 order (:117-120).
 //
-// Fast path (GTSFM_MATCH_INT_F16): one K1 x K2 distance GEMM per pair on fp16 MFMA
-// (v_mfma_f32_32x32x16_f16). The squared norms are folded into 4 extra K columns, so the accumulator
-// IS the squared L2 distance:   A'_r = [a, |a|^2 mod 2048, |a|^2 div 2048, 1, 2048, 2048]
-//                               B'_c = [-2b, 1, 2048, |b|^2 mod 2048, |b|^2 div 2048, 4096]
-// (the last column adds 2^23, see the epilogue)
-// Every factor is an integer exactly representable in fp16 and every partial sum is an integer < 2^24,
-// so the fp32 accumulation is exact in any order: d2 = |a|^2 + |b|^2 - 2 a.b exactly.
-// The epilogue keeps a running top-2 per row in registers and per column through LDS; the K1 x K2 matrix is never
-// written to HBM. Columns (image i1) track packed keys d2 << ib | row (ib = max(11, ceil log2 kmax)); rows (image i2)
-// track distance VALUES only, with no key build. Both insert two values at a time (v_min3 + v_med3 + v_min per pair):
-// 3.8 VALU per distance. In finalize, i1's keypoint i with nearest j is mutual iff j's best distance equals d(i, j) and
-// j has no tie at its minimum; tied j are recomputed exactly (rare). Lexicographic (d2, index) order == OpenCV's
-// strict-'<' scan order, and for d2 < 2^22 ordering by d2 equals ordering by sqrtf(d2), so results are bit-identical
-// to the oracle.
+// Fast path (GTSFM_MATCH_INT_F16): one K1 x K2 distance GEMM per pair on fp16 MFMA (v_mfma_f32_32x32x16_f16), rows =
+// image i1's keypoints (A operand, held in registers), columns = image i2's (B operand, streamed through LDS). The
+// squared norms and a 4-bit row code are folded into 5 extra K columns, so every accumulator IS
+//      d2(i, j) + (i mod 16) / 16
+// exactly (pack_code_kernel). The epilogue never converts: rows keep a value-only top-2 of the raw accumulator bits
+// (their code is constant per row, so the order is d2's), columns keep a value-only top-2 over each lane's 16 rows of
+// a tile (the code breaks ties in row order) and turn it into packed keys d2 << ib | row only once per tile. Three
+// VALU per distance in total (two v_min3/v_med3/v_min inserts per two values, one per direction).
+// The K1 x K2 matrix is never written to HBM. In finalize, i2's keypoint j with nearest i (from its key) is mutual iff
+// i's best distance equals d(i, j) and i has no tie at its minimum; tied i are recomputed exactly (rare).
+// Lexicographic (d2, index) order == OpenCV's strict-'<' scan order, and for d2 < 2^22 ordering by d2 equals ordering
+// by sqrtf(d2), so results are bit-identical to the oracle.
 //
 // Exact path (GTSFM_MATCH_EXACT_F32): float descriptors, per-row sequential fp32 sums (no FMA
 // contraction), top-2 on sqrtf distances — the oracle's arithmetic, for tests and non-SIFT data.
@@ -32,7 +30,6 @@
 namespace {
 
 // Packed key = (d2 << ib) | index with ib = ceil(log2(kmax)) (>= 11) index bits and 32-ib distance bits.
-// d2 saturates at 2^(32-ib)-1; finalize recomputes any row/column whose top-2 touched the saturated value.
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 constexpr int kMaxKmaxPacked = 8192;   // fast path
 // Correctly rounded fp32 square root, as the oracle's sqrtf (HIP's __fsqrt_rn is the ~1-ulp native sqrt).
@@ -46,74 +43,109 @@ inline int index_bits(int kmax) {
     return b;
 }
 
+// Poison distance of padding keypoints (the saturated key field when ib <= 12; 2^20 > every real d2 otherwise).
+// A real value never reaches it: |a|^2, |b|^2 < 2^19 bound d2 <= 2^20 - 2.
+inline uint32_t code_poison(int ib) { return ib <= 12 ? (1u << (32 - ib)) - 1u : (1u << 20); }
+constexpr uint32_t kRowPoisonD2 = (1u << 20) - 1u;  // trunc(row value) >= this: poison (no such neighbour)
+
 // ---------------------------------------------------------------------------------------------
-// Pack float descriptors into the two fp16 MFMA operand forms (norm digits folded into K).
-// A form: row-major [img][kpad][da]. B form: fragment-major per 32-row chunk, [img][chunk][s][h][r][8] with
-// k = 16 s + 8 h + e: the 64 16-B granules one MFMA k-step reads (rows r = 0..31 x halves h) are one contiguous
-// KiB, so a linear LDS-DMA copy of the chunk gives conflict-free ds_read_b128 at lane * 16.
+// Pack float descriptors into the two fp16 MFMA operand forms of the INT_F16 distance GEMM. K columns
+// (da = dim + 5 rounded up to 16 NK):
+//   A'_i = [a_i, |a_i|^2 mod 2048, |a_i|^2 div 2048, 1, 2048, (i mod 16) / 16, 0 ...]      (image in registers)
+//   B'_j = [-2 b_j, 1, 2048, |b_j|^2 mod 2048, |b_j|^2 div 2048, 1, 0 ...]                  (image streamed)
+// Exactness: descriptors are integers in [0, 1023] with |a|^2 < 2^19, so every product is an exact integer (or the
+// code) and EVERY partial sum of any subset of a row-column's K products lies in [-2 a.b, |a|^2 + |b|^2 + 1), inside
+// +-2^20 where fp32 still holds 4 fraction bits: no accumulation order (inside an MFMA or across k-steps) rounds.
+// Padding keypoints (>= count) are poison rows: exactly P = code_poison(ib) against every real keypoint of the other
+// image (their norm columns carry P, their dims are zero), so they never enter a real keypoint's top-2 unless it has
+// fewer than two real neighbours, where they read as "no neighbour".
+// A form: row-major [img][kpad][da] with rows permuted inside each 32-row tile: MFMA tile row r' = (g & 3) + 8 (g >> 2)
+//   + 4 h holds keypoint 16 h + g, so output lane-half h holds the tile's keypoints 16 h .. 16 h + 15 in register
+//   order g, and the 4-bit code i mod 16 is the keypoint's offset inside its lane's 16 rows.
+// B form: fragment-major per 32-row chunk, [img][chunk][s][h][r][8] with k = 16 s + 8 h + e: the 64 16-B granules one
+//   MFMA k-step reads (rows r = 0..31 x halves h) are one contiguous KiB, so a linear LDS-DMA copy of the chunk gives
+//   conflict-free ds_read_b128 at lane * 16.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ size_t b_form_index(int img, int row, int k, int kpad, int da) {
     const size_t chunk = (size_t)img * kpad + (row & ~31);
     return chunk * da + (size_t)(k >> 4) * 512 + ((k >> 3) & 1) * 256 + (row & 31) * 8 + (k & 7);
 }
 
-__global__ void pack_desc_kernel(const float* __restrict__ desc, const int* __restrict__ counts, int kmax, int dim,
-                                 int kpad, int da, _Float16* __restrict__ a_form, _Float16* __restrict__ b_form) {
+__global__ void pack_code_kernel(const float* __restrict__ desc, const int* __restrict__ counts, int kmax, int dim,
+                                 int kpad, int da, uint32_t poison, _Float16* __restrict__ a_form,
+                                 _Float16* __restrict__ b_form) {
     const int img = blockIdx.y;
-    const int row = blockIdx.x * blockDim.y + threadIdx.y;  // one 64-lane wave per descriptor row
+    const int row = blockIdx.x * blockDim.y + threadIdx.y;  // keypoint; one 64-lane wave per descriptor row
     if (row >= kpad) return;
     const int lane = threadIdx.x;
-    const int n = counts[img];
-    _Float16* ar = a_form + ((size_t)img * kpad + row) * da;
-    if (row >= n) {  // padding rows: all-zero operands (masked in the epilogue)
-        for (int k = lane; k < da; k += 64) {
-            ar[k] = (_Float16)0.f;
-            b_form[b_form_index(img, row, k, kpad, da)] = (_Float16)0.f;
-        }
-        return;
-    }
-    const float* src = desc + ((size_t)img * kmax + row) * dim;
+    const bool real = row < counts[img];
+    const int j = row & 31, g = j & 15;
+    const int apos = (row & ~31) + (g & 3) + 8 * (g >> 2) + 4 * (j >> 4);
+    _Float16* ar = a_form + ((size_t)img * kpad + apos) * da;
     float sq = 0.f;
+    const float* src = desc + ((size_t)img * kmax + row) * dim;
     for (int k = lane; k < dim; k += 64) {
-        float v = src[k];
+        const float v = real ? src[k] : 0.f;
         sq += v * v;  // integer-valued: exact
         ar[k] = (_Float16)v;
         b_form[b_form_index(img, row, k, kpad, da)] = (_Float16)(-2.f * v);
     }
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) sq += __shfl_xor(sq, m);
-    const uint32_t nsq = (uint32_t)sq;
-    const float lo = (float)(nsq & 2047u), hi = (float)(nsq >> 11);
+    const uint32_t nrm = real ? (uint32_t)sq : poison;
+    const float lo = (float)(nrm & 2047u), hi = (float)(nrm >> 11);
     for (int k = dim + lane; k < da; k += 64) {
         const int e = k - dim;
         float av = 0.f, bv = 0.f;
-        if (e == 0) { av = lo; bv = 1.f; }
-        else if (e == 1) { av = hi; bv = 2048.f; }
-        else if (e == 2) { av = 1.f; bv = lo; }
-        else if (e == 3) { av = 2048.f; bv = hi; }
-        else if (e == 4) { av = 2048.f; bv = 4096.f; }  // + 2^23: accumulator bits = 0x4B000000 | d2
+        if (e == 0) { av = lo; bv = real ? 1.f : 0.f; }
+        else if (e == 1) { av = hi; bv = real ? 2048.f : 0.f; }
+        else if (e == 2) { av = real ? 1.f : 0.f; bv = lo; }
+        else if (e == 3) { av = real ? 2048.f : 0.f; bv = hi; }
+        else if (e == 4 && real) { av = (float)(row & 15) * 0.0625f; bv = 1.f; }
         ar[k] = (_Float16)av;
         b_form[b_form_index(img, row, k, kpad, da)] = (_Float16)bv;
     }
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fused distance GEMM + row/column top-2. One workgroup (4 waves) per pair.
-// Each wave owns 64 rows (two 32-row MFMA tiles) of a 256-row pass; B streams through LDS in
-// 32-column chunks (double buffered, 304-B padded rows: conflict-free ds_read_b128).
+// Fused distance GEMM + row/column top-2, ping-pong over two wave groups.
+//
+// A workgroup = 8 waves, two groups of 4; waves w and w + 4 share a SIMD. Each wave holds 64 rows (two 32-row MFMA
+// tiles) of A in registers, so a pass covers 512 rows. B streams through a 2-deep LDS ring in units of 64 columns
+// (18 KiB at K = 144, one LDS-DMA burst issued a phase ahead). Every unit is one MFMA segment M (36 MFMAs per wave)
+// and one epilogue segment E (~230 VALU per wave); group 1 runs one phase behind group 0, so in every phase each
+// SIMD has one wave in M beside one wave in E: the matrix pipe and the VALU issue of a SIMD are both busy.
+//   phase 2k:     group 0 M(unit k)        group 1 E(unit k-1)      (LDS-DMA of unit k+1 issued)
+//   phase 2k+1:   group 0 E(unit k)        group 1 M(unit k)
+// A workgroup takes a GROUP of up to kMaxGroup pairs that share image i1 (the register operand): per pass it loads
+// its A rows once and streams each pair's B image in turn (unit order: pass, slot, column unit). Groups are laid out
+// by the caller (gtsfm_match_batched_grouped) so that the ~32 workgroups resident on one XCD stream the same few B
+// images out of that XCD's L2 while each reads its own A image once.
+// Columns: each wave merges its per-lane top-2 into the pair's LDS column state with two LDS atomics per tile
+// (k1 -> ds_min_rtn on C1; min(max(old, k1), k2) -> ds_min on C2 keeps the exact top-2 under any interleaving).
+// Rows: value-only top-2 in registers across a pass; at the pass's last unit one 5-step halving exchange leaves lane
+// l of each half-wave with row l's top-2, stored to rowres.
 // ---------------------------------------------------------------------------------------------
-constexpr int kWaves = 4;
-constexpr int kThreads = kWaves * 64;
-constexpr int kRowsPerPass = kWaves * 64;
-constexpr int kChunk = 32;
+constexpr int kPpGroupWaves = 4;
+constexpr int kPpWaves = 2 * kPpGroupWaves;
+constexpr int kPpThreads = kPpWaves * 64;
+constexpr int kPpRowsPerPass = kPpWaves * 64;  // 512
+constexpr int kUnitCols = 64;
+constexpr int kMaxGroup = 4;
+constexpr int kPpLdsBudget = 160 * 1024;
+#ifndef GTSFM_PP_DMA_MODE
+#define GTSFM_PP_DMA_MODE 0  // 0: every wave issues its share at the end of even phases; 1: group 1 at the start of E
+#endif
+constexpr int kRowAlign = 256;                 // kpad granularity of the packed forms
 
-template <int NK>  // NK = da / 16 k-steps
-struct MnnCfg {
+template <int NK>
+struct PpCfg {
     static constexpr int kDa = NK * 16;
-    static constexpr int kRowBytes = kDa * 2;                      // 288 B at dim 128 (B-form row)
-    static constexpr int kBufBytes = kChunk * kRowBytes;           // one B chunk, contiguous in HBM
-    static constexpr int kGlds = kBufBytes / 1024;                 // 1-KiB LDS-DMA wave-instructions
-    static_assert(kBufBytes % 1024 == 0, "chunk must be whole 1-KiB LDS-DMA pieces");
+    static constexpr int kChunkBytes = 32 * kDa * 2;    // one 32-column MFMA tile of B (9 KiB at NK = 9)
+    static constexpr int kUnitBytes = 2 * kChunkBytes;  // 64 columns
+    static constexpr int kPieces = kUnitBytes / 1024;   // 1-KiB LDS-DMA wave-instructions per unit
+    static constexpr int kPiecesPerWave = GTSFM_PP_DMA_MODE == 1 ? (kPieces + 3) / 4 : (kPieces + 7) / 8;
+    static_assert(kUnitBytes % 1024 == 0, "unit must be whole 1-KiB LDS-DMA pieces");
 };
 
 // Async HBM -> LDS copy of one 1-KiB piece by one wave (lane l moves bytes [16l, 16l+16)).
@@ -122,199 +154,333 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
                                      (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
 }
 
-// A fifth folded K column (A' = 2048, B' = 4096) adds 2^23 to every accumulator, so each holds 2^23 + d2 exactly
-// (d2 < 2^20 for non-negative integer descriptors with |a|^2 < 2^19) and its bit pattern is 0x4B000000 | d2.
-// kFast (ib <= 12, i.e. kmax <= 4096): the packed key is one v_lshl_or_b32 of the raw accumulator bits (the shift
-// drops exponent and sign), no conversion and no saturation. ib = 13 converts, subtracts 2^23 and saturates.
-// B streams through LDS in super-chunks of kSub x 32 columns per barrier; the column partials of a super-chunk are
-// merged by one wave with all 64 lanes busy.
-constexpr int kSub = 2;
-constexpr int kSuper = kSub * kChunk;
+__device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// Orientation: the GEMM's rows (A operand, held in registers) are image i2's keypoints and its columns (B operand,
-// streamed through LDS) are image i1's. Pairs arrive in lexicographic (i1, i2) order, so consecutive pairs share the
-// streamed image; the XCD-aware block remap below hands every XCD a contiguous run of pairs, so the workgroups
-// resident on one XCD stream the same B image out of that XCD's L2 instead of re-reading it from HBM.
-//   rowres[p][j2] = top-2 of image i2's keypoint j2 (distance values in kFast, packed keys otherwise)
-//   colres[p][j1] = top-2 packed keys of image i1's keypoint j1 (index = keypoint of i2)
-template <int NK, bool kFast>
-__global__ __launch_bounds__(kThreads, 2) void mnn_mfma_kernel(const _Float16* __restrict__ a_form,
+// x from lane (l ^ d) within each 32-lane half (ds_swizzle bit mode: and 0x1F, xor d; no address VGPR)
+__device__ __forceinline__ uint32_t xor_swizzle(uint32_t x, int d) {
+    switch (d) {
+        case 16: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (16 << 10));
+        case 8: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (8 << 10));
+        case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (4 << 10));
+        case 2: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (2 << 10));
+        default: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (1 << 10));
+    }
+}
+
+// one v_med3_u32 / v_min3_u32 / v_and_or_b32, free to schedule
+__device__ __forceinline__ uint32_t med3u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ uint32_t min3u(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// running top-2 insert of two values, updated IN PLACE (tied asm operands): the loop-carried row state keeps its
+// registers instead of rotating through copies
+__device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
+    uint32_t m;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(b1), "v"(a), "v"(b));
+    asm("v_min3_u32 %0, %0, %1, %2" : "+v"(b1) : "v"(a), "v"(b));
+    asm("v_min_u32 %0, %0, %1" : "+v"(b2) : "v"(m));
+}
+
+// Per-slot (pair) description, wave-uniform.
+struct PpSlot {
+    int pair, img_a, img_b, na, nb, nsup;
+};
+
+// Unit iterator over (pass, slot, column unit), skipping slots with no rows left in the pass; `cur` caches the
+// slot's description so that stepping within a slot touches no memory. Wave-uniform.
+struct PpIter {
+    int pass, slot, sc, seq;  // seq: running unit number (LDS ring parity)
+    bool valid;
+    PpSlot cur;
+};
+
+#ifdef GTSFM_PP_STAMPS  // diagnostic builds only: per-wave cycle sums of M, barrier after M, E, barrier after E
+__device__ unsigned long long g_pp_stamps[kPpWaves * 4];
+#define PP_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define PP_STAMP(v)
+#endif
+
+template <int NK, bool kClamp>
+__global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* __restrict__ a_form,
                                                                const _Float16* __restrict__ b_form,
                                                                const int* __restrict__ counts,
                                                                const int* __restrict__ pairs, int n_pairs,
-                                                               int kpad, int kmax, int ib,
+                                                               const int* __restrict__ groups, int n_groups,
+                                                               int group_size, int kpad, int kmax, int kmax64, int ib,
                                                                uint2* __restrict__ rowres,
                                                                uint2* __restrict__ colres) {
-    using Cfg = MnnCfg<NK>;
-    constexpr int kSupBytes = kSub * Cfg::kBufBytes;
-    const uint32_t dsat = (1u << (32 - ib)) - 1u;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    unsigned char* bbuf = smem;                                      // [2][kSuper][kRowBytes]
-    uint32_t* partial = (uint32_t*)(smem + 2 * kSupBytes);           // [2][kWaves][kSuper][2]
-    uint2* colstate = (uint2*)(partial + 2 * kWaves * kSuper * 2);   // [kmax]
+    using Cfg = PpCfg<NK>;
+    // the B ring is its own LDS object, so the LDS-DMA into it provably never aliases the column state's atomics
+    __shared__ __attribute__((aligned(1024))) unsigned char ring[2 * Cfg::kUnitBytes];
+    __shared__ int sinfo[kMaxGroup * 8];
+    extern __shared__ __attribute__((aligned(16))) uint32_t colstate[];  // [G][2][kmax64]
 
-    // bijective XCD remap (blocks b, b + 8, ... share an XCD and take consecutive pairs)
-    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_pairs >> 3, r8 = n_pairs & 7;
-    const int p = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
-    const int img_a = pairs[2 * p + 1], img_b = pairs[2 * p];
-    const int n1 = counts[img_a], n2 = counts[img_b];  // n1 rows (A), n2 columns (B)
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int lrow = lane & 31, half = lane >> 5;
-    if (n1 <= 0 || n2 <= 0) return;  // nothing to match; finalize reads zero rows
+    const int tid = threadIdx.x, wave = uniform(tid >> 6), lane = tid & 63;
+    const int lrow = lane & 31, half = lane >> 5, grp = wave >> 2;
+    // bijective XCD remap (blocks b, b + 8, ... share an XCD and take consecutive groups)
+    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_groups >> 3, r8 = n_groups & 7;
+    const int grp_idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
+    const int G = groups ? group_size : 1;
 
-    const _Float16* A = a_form + (size_t)img_a * kpad * Cfg::kDa;
-    const unsigned char* Bbytes = (const unsigned char*)(b_form + (size_t)img_b * kpad * Cfg::kDa);
-    uint2* rres = rowres + (size_t)p * kmax;
-    uint2* cres = colres + (size_t)p * kmax;
+    if (tid < kMaxGroup) {
+        int p = -1;
+        if (tid < G) p = groups ? groups[(size_t)grp_idx * group_size + tid] : grp_idx;
+        if (p >= n_pairs) p = -1;
+        int ia = 0, ibm = 0, na = 0, nb = 0;
+        if (p >= 0) {
+            ia = pairs[2 * p];
+            ibm = pairs[2 * p + 1];
+            na = counts[ia];
+            nb = counts[ibm];
+            if (na <= 0 || nb <= 0) na = nb = 0;
+        }
+        int* si = sinfo + tid * 8;
+        si[0] = p; si[1] = ia; si[2] = ibm; si[3] = na; si[4] = nb; si[5] = (nb + kUnitCols - 1) / kUnitCols;
+    }
+    for (int c = tid; c < G * 2 * kmax64; c += kPpThreads) colstate[c] = kNoKey;
+    __syncthreads();
 
-    for (int c = tid; c < n2; c += kThreads) colstate[c] = make_uint2(kNoKey, kNoKey);
-    const int nsup = (n2 + kSuper - 1) / kSuper;
-
-    // Super-chunk `sc` of B (kSuper consecutive B-form rows, contiguous in HBM; B-form rows are padded to kpad,
-    // a multiple of 256, so a whole super-chunk is always in bounds) -> LDS buffer `buf`.
-    auto issue_super = [&](int sc, int buf) {
-        const unsigned char* src = Bbytes + (size_t)sc * kSupBytes + lane * 16;
-        unsigned char* dst = bbuf + buf * kSupBytes;
-        for (int q = wave; q < kSub * Cfg::kGlds; q += kWaves) glds16(src + q * 1024, dst + q * 1024);
+    auto slot_info = [&](int s) {  // LDS broadcast read (slot changes only)
+        const int* si = sinfo + s * 8;
+        PpSlot r;
+        r.pair = uniform(si[0]); r.img_a = uniform(si[1]); r.img_b = uniform(si[2]);
+        r.na = uniform(si[3]); r.nb = uniform(si[4]); r.nsup = uniform(si[5]);
+        return r;
     };
-    // Merge the 4 waves' column partials of super-chunk `sc` (buffer pb) into colstate (one wave, lane = column).
-    auto merge_partials = [&](int sc, int pb) {
-        if (wave == (sc & (kWaves - 1))) {
-            const int col = sc * kSuper + lane;
-            if (col < n2) {
-                uint2 s = colstate[col];
-                uint32_t s1 = s.x, s2 = s.y;
+    int npass = 0;
+    for (int s = 0; s < G; ++s) npass = max(npass, (slot_info(s).na + kPpRowsPerPass - 1) / kPpRowsPerPass);
+    auto seek = [&](PpIter& it) {  // from (pass, slot) onwards to the first active (pass, slot)
+        while (it.pass < npass) {
+            it.cur = slot_info(it.slot);
+            if (it.cur.pair >= 0 && it.cur.nsup > 0 && it.pass * kPpRowsPerPass < it.cur.na) break;
+            if (++it.slot == G) { it.slot = 0; ++it.pass; }
+        }
+        it.valid = it.pass < npass;
+    };
+    auto advance = [&](PpIter& it) {
+        ++it.seq;
+        if (++it.sc < it.cur.nsup) return;
+        it.sc = 0;
+        if (++it.slot == G) { it.slot = 0; ++it.pass; }
+        seek(it);
+    };
+    PpIter first;
+    first.pass = first.slot = first.sc = first.seq = 0;
+    seek(first);
+    int n_units = 0;
+    for (PpIter it = first; it.valid; ) {  // whole slots at a time
+        n_units += it.cur.nsup;
+        it.seq += it.cur.nsup - 1;
+        it.sc = it.cur.nsup - 1;
+        advance(it);
+    }
+
+    // LDS-DMA of one unit's 64 B columns (contiguous kUnitBytes in the B form) into ring buffer `buf`
+    auto issue_unit = [&](const PpIter& it) {
+        const unsigned char* src = (const unsigned char*)(b_form + ((size_t)it.cur.img_b * kpad + it.sc * kUnitCols) *
+                                                                       Cfg::kDa) + lane * 16;
+        unsigned char* dst = ring + (it.seq & 1) * Cfg::kUnitBytes;
+        // a fixed count per wave (surplus pieces rewrite a piece with the same bytes), so the compiler's vmcnt for a
+        // later A-fragment use can count past them instead of draining the DMA
 #pragma unroll
-                for (int w = 0; w < kWaves; ++w) {
-                    const uint32_t* pp = partial + ((pb * kWaves + w) * kSuper + lane) * 2;
-                    top2_merge(s1, s2, pp[0], pp[1]);
-                }
-                colstate[col] = make_uint2(s1, s2);
-            }
+        for (int i = 0; i < Cfg::kPiecesPerWave; ++i) {
+            const int q = GTSFM_PP_DMA_MODE == 1 ? ((wave & 3) + 4 * i) % Cfg::kPieces : (wave + kPpWaves * i) % Cfg::kPieces;
+            glds16(src + q * 1024, dst + q * 1024);
         }
     };
 
-    for (int rp = 0; rp < n1; rp += kRowsPerPass) {
-        const int r0w = rp + wave * 64;
-        // A fragments for this wave's two row tiles: lane holds A[row = lrow][k = 16s + 8*half .. +8].
-        half8 afrag[2][NK];
+    half8 afrag[2][NK];
+    int a_loaded_img = -1, a_loaded_pass = -1;
+    // A fragments of this wave's 64 rows of pass `pass` (lane holds A[row = lrow][k = 16 s + 8 half .. +8])
+    auto load_a = [&](int img, int pass) {
+        if (img == a_loaded_img && pass == a_loaded_pass) return;
+        a_loaded_img = img;
+        a_loaded_pass = pass;
+        const int r0w = pass * kPpRowsPerPass + wave * 64;
+        if (r0w >= kpad) return;
+        const _Float16* A = a_form + (size_t)img * kpad * Cfg::kDa;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const _Float16* arow = A + (size_t)(r0w + 32 * t + lrow) * Cfg::kDa + 8 * half;
 #pragma unroll
             for (int s = 0; s < NK; ++s) afrag[t][s] = *(const half8*)(arow + 16 * s);
         }
-        uint32_t rb1[2][16], rb2[2][16];
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
-        const bool rows_partial1 = (r0w + 64 > n1);  // either row tile of this wave is partial
+        __builtin_amdgcn_s_waitcnt(0x0070);  // here, so the MFMA stream never waits on the in-flight LDS-DMA
+    };
 
-        issue_super(0, 0);
-        __syncthreads();  // vmcnt(0) + barrier: super-chunk 0 landed, colstate initialised
-
-        for (int sc = 0; sc < nsup; ++sc) {
-            const int buf = sc & 1;
-            if (sc + 1 < nsup) issue_super(sc + 1, buf ^ 1);  // lands during this super-chunk's MFMAs
-            // Both 32-column chunks of the super-chunk against both row tiles (acc[sub][t]), so every row sees two
-            // new distances per epilogue and takes them with one paired top-2 insert (3 VALU per 2 distances).
-            // B fragments: lane holds B[k = 16s + 8*half .. +8][col = lrow]; 2-way bank conflict on 288-B rows.
-            const unsigned char* bb = bbuf + buf * kSupBytes + lane * 16;
-            f32x16 acc[kSub][2];
+    const uint32_t dsat = (1u << (32 - ib)) - 1u;
+    uint32_t rb1[2][16], rb2[2][16];
 #pragma unroll
-            for (int sub = 0; sub < kSub; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
+    f32x16 acc[2][2];  // [sub (32-column tile)][t (32-row tile)]
+
+    PpIter work = first, dma = first;
+    if (first.valid) {
+        issue_unit(dma);
+        advance(dma);
+    }
+    __syncthreads();  // unit 0 landed (vmcnt(0) + barrier)
+
+    // Phase barriers order LDS only. The LDS-DMA of unit k+1 is issued at the end of phase 2k (by every wave: group
+    // 0 right after its M(k), group 1 right after its E(k-1)) and waited for at the end of phase 2k+1, so it has a
+    // whole phase to land and nothing drains it earlier.
+    auto phase_barrier = [&](bool drain_dma) {
+        if (drain_dma) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) expcnt(7) lgkmcnt(0)
+        else __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0), vmcnt/expcnt untouched
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    };
+    auto dma_next = [&]() {
+        if (dma.valid) {
+            issue_unit(dma);
+            advance(dma);
+        }
+    };
+    if (grp == 1 && n_units > 0) {  // group 1's leading phase 0: idle
+        if (GTSFM_PP_DMA_MODE == 0 || true) dma_next();
+        phase_barrier(false);
+    }
+    // One unit per iteration, straight-line M then E for both groups (group 1 one phase behind):
+    //   group 0: M(k) = phase 2k, E(k) = phase 2k+1;   group 1: M(k) = phase 2k+1, E(k) = phase 2k+2.
+#ifdef GTSFM_PP_STAMPS
+    unsigned long long st[4] = {0, 0, 0, 0};
+#endif
+    for (int k = 0; k < n_units; ++k) {
+        PP_STAMP(t0);
+        const PpSlot si = work.cur;
+        const int r0w = work.pass * kPpRowsPerPass + wave * 64;
+        const bool rows_here = r0w < si.na;
+        // ---- M: 2 x 2 tiles of 32 x 32, K = 16 NK. A new (pass, A image) reloads the A fragments first (once per
+        // pass: a short stall the partner wave's E covers).
+        load_a(si.img_a, work.pass);
+        __builtin_amdgcn_s_setprio(2);  // the MFMA stream outranks the partner wave's VALU epilogue for issue
+#ifdef GTSFM_PP_SKIP_M
+        if (false) {
+#else
+        if (rows_here) {
+#endif
+            const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
 #pragma unroll
             for (int s = 0; s < NK; ++s) {
 #pragma unroll
-                for (int sub = 0; sub < kSub; ++sub) {
-                    const half8 bf = *(const half8*)(bb + sub * Cfg::kBufBytes + 1024 * s);
+                for (int sub = 0; sub < 2; ++sub) {
+                    const half8 bf = *(const half8*)(bb + sub * Cfg::kChunkBytes + 1024 * s);
                     acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc[sub][0], 0, 0, 0);
                     acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc[sub][1], 0, 0, 0);
                 }
             }
-
-            const int c0 = sc * kSuper;
-            const bool cols_partial = (c0 + kSuper > n2);
-            uint32_t cb1[kSub], cb2[kSub];
-            // Epilogue. kFast: rows keep value-only top-2s of the raw accumulator bits (0x4B000000 | d2, monotone in
-            // d2), columns keep packed keys with the row index (one v_lshl_or), both inserted two at a time. Partial
-            // tiles (last row tile / column chunk) take a separate masked copy so the full-tile path has no selects.
-            auto epilogue = [&](auto masked) {
-                constexpr bool kMasked = decltype(masked)::value;
+        }
+        PP_STAMP(t1);
+        if (GTSFM_PP_DMA_MODE == 0 && grp == 0) dma_next();
+        phase_barrier(grp == 1);
+        PP_STAMP(t2);
+        // ---- E
+        __builtin_amdgcn_s_setprio(0);
+        if (GTSFM_PP_DMA_MODE == 1 && grp == 1) dma_next();
+#ifdef GTSFM_PP_SKIP_E
+        if (false) {
+#else
+        if (rows_here) {
+#endif
+            // rows: both column tiles' values of row (t, g) in one paired insert
 #pragma unroll
-                for (int sub = 0; sub < kSub; ++sub) cb1[sub] = cb2[sub] = kNoKey;
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int g = 0; g < 16; ++g)
+                    ins2(rb1[t][g], rb2[t][g], __float_as_uint(acc[0][t][g]), __float_as_uint(acc[1][t][g]));
+            // columns: value-only top-2 over the lane's 16 rows of each (column tile, row tile), then keys
+            // (d2 << ib) | row with row = rowbase | code; all four returning atomics issued before any wait
+            uint32_t* c1s = colstate + work.slot * 2 * kmax64;
+            uint32_t* c2s = c1s + kmax64;
+            uint32_t k1[2][2], k2[2][2], old[2][2];
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
-                    const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 4 * half);
+                    const f32x16& a = acc[sub][t];
+                    uint32_t v1 = umin(__float_as_uint(a[0]), __float_as_uint(a[1]));
+                    uint32_t v2 = umax(__float_as_uint(a[0]), __float_as_uint(a[1]));
 #pragma unroll
-                    for (int g0 = 0; g0 < 16; g0 += 2) {  // two rows at a time: column keys go in as a pair
-                        uint32_t ck[kSub][2];
+                    for (int g = 2; g < 16; g += 2) ins2(v1, v2, __float_as_uint(a[g]), __float_as_uint(a[g + 1]));
+                    const uint32_t u = (uint32_t)(__uint_as_float(v1) * 16.f);
+                    uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
+                    if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
+                    const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 16 * half);
+                    k1[sub][t] = (d1 << ib) | rowbase | (u & 15u);
+                    k2[sub][t] = d2 << ib;  // the second's index never matters
+                }
+            }
+            const int col0 = work.sc * kUnitCols + lrow;
 #pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const int g = g0 + h;
-                            const uint32_t grow = rowbase + (uint32_t)((g & 3) + 8 * (g >> 2));
-                            uint32_t rv[kSub];
+            for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-                            for (int sub = 0; sub < kSub; ++sub) {
-                                const uint32_t gcol = (uint32_t)(c0 + sub * kChunk + lrow);
-                                const uint32_t bits = __float_as_uint(acc[sub][t][g]);
-                                if constexpr (kFast) {
-                                    rv[sub] = bits;
-                                    ck[sub][h] = lshl_or(bits, (uint32_t)ib, grow);
-                                } else {
-                                    const uint32_t d2 = umin((uint32_t)acc[sub][t][g] - (1u << 23), dsat);
-                                    rv[sub] = (d2 << ib) | gcol;
-                                    ck[sub][h] = (d2 << ib) | grow;
-                                }
-                                if constexpr (kMasked) {
-                                    if ((int)gcol >= n2) rv[sub] = kNoKey;
-                                    if ((int)grow >= n1) ck[sub][h] = kNoKey;
-                                }
-                            }
-                            top2_insert2(rb1[t][g], rb2[t][g], rv[0], rv[1]);
-                        }
+                for (int t = 0; t < 2; ++t)
+                    old[sub][t] = __hip_atomic_fetch_min(&c1s[col0 + 32 * sub], k1[sub][t], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-                        for (int sub = 0; sub < kSub; ++sub) top2_insert2(cb1[sub], cb2[sub], ck[sub][0], ck[sub][1]);
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+                    __hip_atomic_fetch_min(&c2s[col0 + 32 * sub], umin(umax(old[sub][t], k1[sub][t]), k2[sub][t]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (work.sc == si.nsup - 1) {
+                // the pass is over for this pair: halving exchange across each half-wave's 32 lanes, then lane
+                // (lrow, half) holds register j = lrow = 16 t + g, i.e. keypoint r0w + 32 t + 16 half + g
+                uint32_t* x1 = &rb1[0][0];  // in place: the row state restarts after the store
+                uint32_t* x2 = &rb2[0][0];
+#pragma unroll
+                for (int d = 16; d >= 1; d >>= 1) {
+                    const bool up = (lrow & d) != 0;
+#pragma unroll
+                    for (int j = 0; j < d; ++j) {
+                        const uint32_t s1 = up ? x1[j] : x1[j + d], s2 = up ? x2[j] : x2[j + d];
+                        const uint32_t q1 = up ? x1[j + d] : x1[j], q2 = up ? x2[j + d] : x2[j];
+                        const uint32_t o1 = xor_swizzle(s1, d), o2 = xor_swizzle(s2, d);
+                        x1[j] = umin(q1, o1);
+                        x2[j] = med3u(q1, o1, umin(q2, o2));
+                        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the temporaries
                     }
                 }
-            };
-            static_assert(kSub == 2, "paired row insert takes exactly two chunks");
-            if (cols_partial || rows_partial1)
-                epilogue(std::true_type{});
-            else
-                epilogue(std::false_type{});
-            // combine the two half-waves (same column, rows +0/+4) and publish the wave's column partials
+                const int key = r0w + 32 * (lrow >> 4) + 16 * half + (lrow & 15);
+                if (key < si.na) rowres[(size_t)si.pair * kmax + key] = make_uint2(x1[0], x2[0]);
 #pragma unroll
-            for (int sub = 0; sub < kSub; ++sub) {
-                uint32_t a1 = cb1[sub], a2 = cb2[sub];
-                const uint32_t o1 = __shfl_xor(a1, 32), o2 = __shfl_xor(a2, 32);
-                top2_merge(a1, a2, o1, o2);
-                partial[((buf * kWaves + wave) * kSuper + sub * kChunk + lrow) * 2 + half] = half ? a2 : a1;
-            }
-            if (sc > 0) merge_partials(sc - 1, buf ^ 1);
-            __syncthreads();  // next super-chunk landed (vmcnt(0)); partials of this one visible
-        }
-        merge_partials(nsup - 1, (nsup - 1) & 1);
-
-        // reduce each row's top-2 across the 32 lanes of its half-wave and store it
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                uint32_t b1 = rb1[t][g], b2 = rb2[t][g];
-#pragma unroll
-                for (int m = 1; m < 32; m <<= 1) {
-                    const uint32_t o1 = __shfl_xor(b1, m), o2 = __shfl_xor(b2, m);
-                    top2_merge(b1, b2, o1, o2);
-                }
-                const int grow = r0w + 32 * t + (g & 3) + 8 * (g >> 2) + 4 * half;
-                if (lrow == g && grow < n1) rres[grow] = make_uint2(b1, b2);
+                for (int j = 0; j < 32; ++j) x1[j] = x2[j] = kNoKey;
             }
         }
-        __syncthreads();
+        advance(work);
+        PP_STAMP(t3);
+        if (GTSFM_PP_DMA_MODE == 0 && grp == 1) dma_next();
+        phase_barrier(grp == 0);
+        PP_STAMP(t4);
+#ifdef GTSFM_PP_STAMPS
+        st[0] += t1 - t0; st[1] += t2 - t1; st[2] += t3 - t2; st[3] += t4 - t3;
+#endif
     }
-    for (int c = tid; c < n2; c += kThreads) cres[c] = colstate[c];
+#ifdef GTSFM_PP_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_pp_stamps[wave * 4 + i], st[i]);
+#endif
+    if (grp == 0 && n_units > 0) phase_barrier(false);  // group 0's trailing phase 2U: idle
+    __syncthreads();
+    for (int s = 0; s < G; ++s) {
+        const PpSlot si = slot_info(s);
+        if (si.pair < 0 || si.na == 0) continue;
+        const uint32_t* c1s = colstate + s * 2 * kmax64;
+        const uint32_t* c2s = c1s + kmax64;
+        for (int c = tid; c < si.nb; c += kPpThreads) colres[(size_t)si.pair * kmax + c] = make_uint2(c1s[c], c2s[c]);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -424,11 +590,12 @@ __device__ void block_exact_top2(const float* __restrict__ q, const float* __res
     __syncthreads();
 }
 
-// Per-keypoint top-2 encodings consumed by finalize. side1 = image i1's keypoints (best in i2), side2 = image i2's.
-//   kResExact:  ExactTop2 on both sides (exact fp32 path)
-//   kResKeys:   packed (d2 << ib | index) keys on both sides (ib = 13)
-//   kResValues: side1 packed keys, side2 raw accumulator bits 0x4B000000 | d2 without an index (ib <= 12)
-constexpr int kResExact = 0, kResKeys = 1, kResValues = 2;
+// Per-keypoint top-2 encodings consumed by finalize.
+//   kResExact: ExactTop2 on both sides (exact fp32 path); rowres = image i1's keypoints, colres = image i2's.
+//   kResCodes: mnn_pp_kernel. rowres = image i1's keypoints: raw accumulator bits (d2 + code/16, value-only);
+//              colres = image i2's keypoints: packed keys (d2 << ib) | i1 index (second: distance only).
+constexpr int kResExact = 0, kResCodes = 1;
+template <int kRes> constexpr int kRedoIntsOf = kRes == kResCodes ? 2 : 1;  // redo list length / kmax
 
 template <int kRes>
 __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void* __restrict__ rowres_v,
@@ -439,102 +606,67 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
                                                                      int dim, int ib, double ratio,
                                                                      uint32_t* __restrict__ out_idx,
                                                                      int* __restrict__ out_count) {
+    constexpr int kRedoInts = kRedoIntsOf<kRes>;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int* hdr = (int*)smem;                                           // [0] matches, [1] redo rows
+    int* hdr = (int*)smem;                                           // [0] matches, [1] redo rows, [2] redo keys
     float* red_d = (float*)(smem + 16);                               // [2*kFinThreads]
     int* red_j = (int*)(smem + 16 + 8 * kFinThreads);                 // [kFinThreads]
-    int* redo = (int*)(smem + 16 + 12 * kFinThreads);                 // [kmax]
+    int* redo = (int*)(smem + 16 + 12 * kFinThreads);                 // [2 kmax]: rows from the front, keys from the back
     unsigned long long* keys =
-        (unsigned long long*)(smem + 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * 4, 16));
+        (unsigned long long*)(smem + 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * kRedoInts * 4, 16));
     const int p = blockIdx.x;
     const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
     const int n1 = counts[i1], n2 = counts[i2];
     const int tid = threadIdx.x;
-    if (tid == 0) { hdr[0] = 0; hdr[1] = 0; }
+    if (tid == 0) { hdr[0] = 0; hdr[1] = 0; hdr[2] = 0; }
     __syncthreads();
-    const uint32_t imask = (1u << ib) - 1u, dsat = (1u << (32 - ib)) - 1u;
     auto push = [&](int i, int j, float d1r) {
         const int slot = atomicAdd(&hdr[0], 1);
         keys[slot] = ((unsigned long long)__float_as_uint(d1r) << 32) | ((unsigned long long)i << 16) | (uint32_t)j;
     };
-
-    constexpr bool kPacked = kRes == kResKeys;
     const float* D1 = desc + (size_t)i1 * kmax * dim;
     const float* D2 = desc + (size_t)i2 * kmax * dim;
-    if constexpr (kRes == kResValues) {
-        // side2 carries distances only. Keypoint i's nearest j (from its key) is mutual iff j's best distance equals
-        // d(i, j) and j has no tie at its minimum (then i, reaching that minimum, is j's unique nearest). A tied j
-        // whose own ratio test can pass is recomputed exactly below; one that cannot is in no match.
-        constexpr uint32_t kMant = 0x7FFFFFu;
-        const uint2* s1 = (const uint2*)rowres_v + (size_t)p * kmax;
-        const uint2* s2 = (const uint2*)colres_v + (size_t)p * kmax;
-        for (int j = tid; j < n2 && n1 > 0; j += kFinThreads) {
-            const uint2 v = s2[j];
-            if (v.x == kNoKey || v.x != v.y) continue;
-            const float d = sqrt_cr((float)(v.x & kMant));
-            if (ratio_ok(d, d, ratio)) redo[atomicAdd(&hdr[1], 1)] = j;
-        }
-        for (int i = tid; i < n1 && n2 > 0; i += kFinThreads) {
-            const uint2 k = s1[i];
-            if (k.x == kNoKey) continue;
-            const int j = (int)(k.x & imask);
-            const uint32_t d = k.x >> ib;
-            const uint2 v = s2[j];
-            if (v.x == v.y || (v.x & kMant) != d) continue;  // j tied (redo) or j's nearest is not i
-            const float d1r = sqrt_cr((float)d);
-            const float d2r = (k.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(k.y >> ib));
-            const float d2c = (v.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(v.y & kMant));
-            if (ratio_ok(d1r, d2r, ratio) && ratio_ok(d1r, d2c, ratio)) push(i, j, d1r);
+
+    if constexpr (kRes == kResCodes) {
+        // Image i2's keypoint j with key nearest i is mutual iff i's best distance equals d(i, j) and i has no tie at
+        // its minimum (then j, reaching that minimum, is i's unique nearest). A tied i whose own ratio test can pass
+        // is recomputed exactly ("row redo"); one that cannot is in no match. Key fields equal to dsat are padding
+        // ("no neighbour") when ib <= 12 and possibly clamped distances when ib = 13: those keypoints are recomputed
+        // exactly too ("key redo"), unless their nearest i is a row redo (which finds the same match).
+        const uint32_t imask = (1u << ib) - 1u, dsat = (1u << (32 - ib)) - 1u;
+        const bool clamped = ib > 12;
+        const uint2* rv = (const uint2*)rowres_v + (size_t)p * kmax;
+        const uint2* ck = (const uint2*)colres_v + (size_t)p * kmax;
+        auto rdec = [](uint32_t bits) { return (uint32_t)__uint_as_float(bits); };  // trunc: d2
+        auto row_redo = [&](uint2 v) {
+            const uint32_t a = rdec(v.x);
+            return a == rdec(v.y) && ratio_ok(sqrt_cr((float)a), sqrt_cr((float)a), ratio);
+        };
+        auto row_d2 = [&](uint32_t bits) {
+            const uint32_t d = rdec(bits);
+            return d >= kRowPoisonD2 ? __builtin_inff() : sqrt_cr((float)d);
+        };
+        if (n1 > 0 && n2 > 0) {
+            for (int i = tid; i < n1; i += kFinThreads)
+                if (row_redo(rv[i])) redo[atomicAdd(&hdr[1], 1)] = i;
+            for (int j = tid; j < n2; j += kFinThreads) {
+                const uint2 k = ck[j];
+                const uint32_t kd1 = k.x >> ib, kd2 = k.y >> ib;
+                if (kd1 == dsat || (clamped && kd2 == dsat)) {
+                    if (clamped) redo[2 * kmax - 1 - atomicAdd(&hdr[2], 1)] = j;
+                    continue;
+                }
+                const int i = (int)(k.x & imask);
+                const uint2 v = rv[i];
+                if (row_redo(v) || rdec(v.x) != kd1 || rdec(v.y) == kd1) continue;
+                const float d1r = sqrt_cr((float)kd1);
+                const float d2c = kd2 == dsat ? __builtin_inff() : sqrt_cr((float)kd2);
+                if (ratio_ok(d1r, row_d2(v.y), ratio) && ratio_ok(d1r, d2c, ratio)) push(i, j, d1r);
+            }
         }
         __syncthreads();
-        const int nredo = hdr[1];
-        for (int r = 0; r < nredo; ++r) {
-            const int j = redo[r];
-            float d1r, d2r, d1c, d2c;
-            int i, jj;
-            block_exact_top2(D2 + (size_t)j * dim, D1, n1, dim, red_d, red_j, d1c, d2c, i);
-            if (i < 0) continue;
-            block_exact_top2(D1 + (size_t)i * dim, D2, n2, dim, red_d, red_j, d1r, d2r, jj);
-            if (tid == 0 && jj == j && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
-            __syncthreads();
-        }
-    }
-    for (int i = tid; i < n1 && n2 > 0 && kRes != kResValues; i += kFinThreads) {
-        float d1r, d2r, d1c, d2c;
-        int j, ic;
-        if (kPacked) {
-            const uint2 r = ((const uint2*)rowres_v)[(size_t)p * kmax + i];
-            if (r.x == kNoKey) continue;
-            j = (int)(r.x & imask);
-            const uint2 c = ((const uint2*)colres_v)[(size_t)p * kmax + j];
-            const bool sat = (r.x >> ib) == dsat || (r.y != kNoKey && (r.y >> ib) == dsat) || (c.x >> ib) == dsat ||
-                             (c.y != kNoKey && (c.y >> ib) == dsat);
-            if (sat) {
-                redo[atomicAdd(&hdr[1], 1)] = i;
-                continue;
-            }
-            d1r = sqrt_cr((float)(r.x >> ib));
-            d2r = (r.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(r.y >> ib));
-            ic = (int)(c.x & imask);
-            d1c = sqrt_cr((float)(c.x >> ib));
-            d2c = (c.y == kNoKey) ? __builtin_inff() : sqrt_cr((float)(c.y >> ib));
-        } else {
-            const ExactTop2 r = ((const ExactTop2*)rowres_v)[(size_t)p * kmax + i];
-            if (r.j1 < 0) continue;
-            j = r.j1;
-            d1r = r.d1;
-            d2r = r.d2;
-            const ExactTop2 c = ((const ExactTop2*)colres_v)[(size_t)p * kmax + j];
-            ic = c.j1;
-            d1c = c.d1;
-            d2c = c.d2;
-        }
-        if (ic == i && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
-    }
-    __syncthreads();
-    if (kPacked) {  // rare: saturated keys -> exact block-wide recomputation of that row and its column
-        const int nredo = hdr[1];
-        for (int r = 0; r < nredo; ++r) {
+        const int nrow = hdr[1], nkey = hdr[2];
+        for (int r = 0; r < nrow; ++r) {
             const int i = redo[r];
             float d1r, d2r, d1c, d2c;
             int j, ic;
@@ -543,6 +675,24 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(const void*
             block_exact_top2(D2 + (size_t)j * dim, D1, n1, dim, red_d, red_j, d1c, d2c, ic);
             if (tid == 0 && ic == i && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
             __syncthreads();
+        }
+        for (int r = 0; r < nkey; ++r) {
+            const int j = redo[2 * kmax - 1 - r];
+            float d1r, d2r, d1c, d2c;
+            int i, jj;
+            block_exact_top2(D2 + (size_t)j * dim, D1, n1, dim, red_d, red_j, d1c, d2c, i);
+            if (i < 0 || row_redo(rv[i])) continue;  // uniform: every thread reads the same i
+            block_exact_top2(D1 + (size_t)i * dim, D2, n2, dim, red_d, red_j, d1r, d2r, jj);
+            if (tid == 0 && jj == j && ratio_ok(d1r, d2r, ratio) && ratio_ok(d1c, d2c, ratio)) push(i, j, d1r);
+            __syncthreads();
+        }
+    } else {
+        for (int i = tid; i < n1 && n2 > 0; i += kFinThreads) {
+            const ExactTop2 r = ((const ExactTop2*)rowres_v)[(size_t)p * kmax + i];
+            if (r.j1 < 0) continue;
+            const int j = r.j1;
+            const ExactTop2 c = ((const ExactTop2*)colres_v)[(size_t)p * kmax + j];
+            if (c.j1 == i && ratio_ok(r.d1, r.d2, ratio) && ratio_ok(c.d1, c.d2, ratio)) push(i, j, r.d1);
         }
     }
     __syncthreads();
@@ -588,29 +738,51 @@ inline int pack_da(int dim) {
     const int nk = (dim + 5 + 15) / 16;
     return 16 * (nk <= 2 ? 2 : nk <= 5 ? 5 : nk <= 9 ? 9 : nk);
 }
-inline int pack_kpad(int kmax) { return (int)gtsfm_align_up((size_t)kmax, kRowsPerPass); }
+inline int pack_kpad(int kmax) { return (int)gtsfm_align_up((size_t)kmax, kRowAlign); }
+inline int pp_kmax64(int kmax) { return (int)gtsfm_align_up((size_t)kmax, kUnitCols); }
 
-template <int NK, bool kFast>
-int launch_mnn_t(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
-                 int kpad, int kmax, int ib, uint2* rowres, uint2* colres, hipStream_t stream) {
-    using Cfg = MnnCfg<NK>;
-    const size_t lds = 2 * kSub * Cfg::kBufBytes + 2 * kWaves * kSuper * 2 * sizeof(uint32_t) +
-                       (size_t)kmax * sizeof(uint2);
-    if (lds > 160 * 1024) return GTSFM_ERR_ARG;
-    if (lds > 65536)
-        GTSFM_CHECK_HIP(hipFuncSetAttribute((const void*)mnn_mfma_kernel<NK, kFast>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL((mnn_mfma_kernel<NK, kFast>), dim3(n_pairs), dim3(kThreads), lds, stream, a_form, b_form,
-                       counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres);
+// dynamic LDS (column state) and total LDS (+ the static B ring and slot table) of mnn_pp_kernel<NK>
+inline size_t pp_dyn_lds_bytes(int kmax, int group_size) {
+    return (size_t)group_size * 2 * pp_kmax64(kmax) * sizeof(uint32_t);
+}
+template <int NK>
+size_t pp_lds_bytes(int kmax, int group_size) {
+    return 2 * (size_t)PpCfg<NK>::kUnitBytes + kMaxGroup * 8 * sizeof(int) + pp_dyn_lds_bytes(kmax, group_size);
+}
+
+// Largest group size (pairs per workgroup) whose column state fits the LDS next to the B ring.
+int pp_max_group(int kmax, int dim) {
+    const int nk = pack_da(dim) / 16;
+    for (int g = kMaxGroup; g >= 1; --g) {
+        const size_t lds = nk == 2 ? pp_lds_bytes<2>(kmax, g) : nk == 5 ? pp_lds_bytes<5>(kmax, g) : pp_lds_bytes<9>(kmax, g);
+        if (lds <= (size_t)kPpLdsBudget) return g;
+    }
+    return 0;
+}
+
+template <int NK, bool kClamp>
+int launch_pp_t(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
+                const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, uint2* rowres,
+                uint2* colres, hipStream_t stream) {
+    const int gs = groups ? group_size : 1;
+    if (pp_lds_bytes<NK>(kmax, gs) > (size_t)kPpLdsBudget) return GTSFM_ERR_ARG;
+    const size_t lds = pp_dyn_lds_bytes(kmax, gs);
+    GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)mnn_pp_kernel<NK, kClamp>, (int)lds));
+    hipLaunchKernelGGL((mnn_pp_kernel<NK, kClamp>), dim3(n_groups), dim3(kPpThreads), lds, stream, a_form, b_form,
+                       counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax, pp_kmax64(kmax), ib, rowres,
+                       colres);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
 
 template <int NK>
-int launch_mnn(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
-               int kpad, int kmax, int ib, uint2* rowres, uint2* colres, hipStream_t stream) {
+int launch_pp(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
+              const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, uint2* rowres,
+              uint2* colres, hipStream_t stream) {
     if (ib <= 12)
-        return launch_mnn_t<NK, true>(a_form, b_form, counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream);
-    return launch_mnn_t<NK, false>(a_form, b_form, counts, pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream);
+        return launch_pp_t<NK, false>(a_form, b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad,
+                                      kmax, ib, rowres, colres, stream);
+    return launch_pp_t<NK, true>(a_form, b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax,
+                                 ib, rowres, colres, stream);
 }
 
 // side1 / side2: per-keypoint top-2 of image i1 / image i2 of each pair (encoding kRes)
@@ -618,7 +790,7 @@ template <int kRes>
 int launch_finalize(const void* side1, const void* side2, const float* desc, const int* counts, const int* pairs,
                     int n_pairs, int kmax, int dim, int ib, double ratio, uint32_t* out_idx, int* out_count,
                     hipStream_t stream) {
-    const size_t lds = 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * 4, 16) +
+    const size_t lds = 16 + 12 * kFinThreads + gtsfm_align_up((size_t)kmax * kRedoIntsOf<kRes> * 4, 16) +
                        (size_t)next_pow2(kmax) * sizeof(unsigned long long);
     if (lds > 160 * 1024) return GTSFM_ERR_ARG;
     if (lds > 65536)
@@ -1013,45 +1185,63 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
     return 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
 }
 
-int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim, const int* d_pairs,
-                        int n_pairs, double ratio, int mode, void* d_workspace, size_t workspace_bytes,
-                        uint32_t* d_out_idx, int* d_out_count, void* stream_v) {
+#ifdef GTSFM_PP_STAMPS
+int gtsfm_pp_stamps(unsigned long long* out) {  // diagnostic builds: read and clear the per-wave cycle sums
+    GTSFM_CHECK_HIP(hipDeviceSynchronize());
+    GTSFM_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pp_stamps), sizeof(g_pp_stamps)));
+    static const unsigned long long zero[kPpWaves * 4] = {};
+    GTSFM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), zero, sizeof(zero)));
+    return GTSFM_OK;
+}
+#endif
+
+int gtsfm_match_max_group(int kmax, int dim) {
+    if (kmax <= 0 || kmax > kMaxKmaxPacked || dim <= 0 || dim > 139) return 0;
+    return pp_max_group(kmax, dim);
+}
+
+int gtsfm_match_batched_grouped(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim,
+                                const int* d_pairs, int n_pairs, const int* d_groups, int n_groups, int group_size,
+                                double ratio, int mode, void* d_workspace, size_t workspace_bytes, uint32_t* d_out_idx,
+                                int* d_out_count, void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
     if (n_pairs == 0) return GTSFM_OK;
     if (!d_desc || !d_counts || !d_pairs || !d_out_idx || !d_out_count || n_img <= 0 || kmax <= 0 || dim <= 0 ||
         n_pairs < 0 || kmax > kMaxKmax)
         return GTSFM_ERR_ARG;
+    if (d_groups && (n_groups <= 0 || group_size <= 0 || group_size > kMaxGroup)) return GTSFM_ERR_ARG;
     if (workspace_bytes < gtsfm_match_workspace_bytes(n_img, kmax, dim, n_pairs, mode)) return GTSFM_ERR_CAPACITY;
     unsigned char* ws = (unsigned char*)d_workspace;
 
     if (mode == GTSFM_MATCH_INT_F16) {
         const int da = pack_da(dim), kpad = pack_kpad(kmax), nk = da / 16, ib = index_bits(kmax);
         if (dim > 139 || kmax > kMaxKmaxPacked) return GTSFM_ERR_ARG;
+        if (d_groups && group_size > pp_max_group(kmax, dim)) return GTSFM_ERR_ARG;
         const size_t form_bytes = gtsfm_align_up((size_t)n_img * kpad * da * sizeof(_Float16), 256);
         _Float16* a_form = (_Float16*)ws;
         _Float16* b_form = (_Float16*)(ws + form_bytes);
         const size_t res_bytes = gtsfm_align_up((size_t)n_pairs * kmax * sizeof(uint2), 256);
         uint2* rowres = (uint2*)(ws + 2 * form_bytes);
         uint2* colres = (uint2*)(ws + 2 * form_bytes + res_bytes);
-        hipLaunchKernelGGL(pack_desc_kernel, dim3(kpad / 4, n_img), dim3(64, 4), 0, stream, d_desc, d_counts, kmax,
-                           dim, kpad, da, a_form, b_form);
+        hipLaunchKernelGGL(pack_code_kernel, dim3(kpad / 4, n_img), dim3(64, 4), 0, stream, d_desc, d_counts, kmax,
+                           dim, kpad, da, code_poison(ib), a_form, b_form);
         GTSFM_CHECK_HIP(hipGetLastError());
+        const int ng = d_groups ? n_groups : n_pairs, gs = d_groups ? group_size : 1;
         int rc;
         if (g_mnn_events[0]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[0], stream));
         switch (nk) {
-            case 2: rc = launch_mnn<2>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
-            case 5: rc = launch_mnn<5>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
-            case 9: rc = launch_mnn<9>(a_form, b_form, d_counts, d_pairs, n_pairs, kpad, kmax, ib, rowres, colres, stream); break;
+            case 2: rc = launch_pp<2>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, rowres, colres, stream); break;
+            case 5: rc = launch_pp<5>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, rowres, colres, stream); break;
+            case 9: rc = launch_pp<9>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, rowres, colres, stream); break;
             default: return GTSFM_ERR_ARG;
         }
         if (rc != GTSFM_OK) return rc;
         if (g_mnn_events[1]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[1], stream));
-        // the GEMM's columns are image i1's keypoints (side1), its rows image i2's (side2)
-        if (ib <= 12)
-            return launch_finalize<kResValues>(colres, rowres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib,
-                                               ratio, d_out_idx, d_out_count, stream);
-        return launch_finalize<kResKeys>(colres, rowres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
-                                         d_out_idx, d_out_count, stream);
+#if defined(GTSFM_PP_SKIP_E) || defined(GTSFM_PP_SKIP_M)
+        return GTSFM_OK;  // timing-only diagnostic builds (tools/build_variants.sh): no results
+#endif
+        return launch_finalize<kResCodes>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
+                                          d_out_idx, d_out_count, stream);
     }
     if (mode == GTSFM_MATCH_F16_RERANK && dim <= kFlMaxDim)
         return run_fl_match(d_desc, d_counts, n_img, kmax, dim, d_pairs, n_pairs, ratio, ws, d_out_idx, d_out_count,
@@ -1067,6 +1257,13 @@ int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int
     GTSFM_CHECK_HIP(hipGetLastError());
     return launch_finalize<kResExact>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, 0, ratio,
                                       d_out_idx, d_out_count, stream);
+}
+
+int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim, const int* d_pairs,
+                        int n_pairs, double ratio, int mode, void* d_workspace, size_t workspace_bytes,
+                        uint32_t* d_out_idx, int* d_out_count, void* stream_v) {
+    return gtsfm_match_batched_grouped(d_desc, d_counts, n_img, kmax, dim, d_pairs, n_pairs, nullptr, 0, 0, ratio,
+                                       mode, d_workspace, workspace_bytes, d_out_idx, d_out_count, stream_v);
 }
 
 }  // extern "C"

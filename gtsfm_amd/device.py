@@ -7,6 +7,7 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import numpy as np
 import torch
 
 from gtsfm_amd import native
@@ -21,8 +22,8 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 
 def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, ratio: Optional[float],
-                mode: int = native.GTSFM_MATCH_INT_F16, stream: Optional[torch.cuda.Stream] = None
-                ) -> Tuple[torch.Tensor, torch.Tensor]:
+                mode: int = native.GTSFM_MATCH_INT_F16, stream: Optional[torch.cuda.Stream] = None,
+                groups: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Mutual-NN + ratio matching of every (i1, i2) row of `pairs`.
 
     Args:
@@ -31,6 +32,8 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
         pairs: (P, 2) int32 image index pairs.
         ratio: ratio-test threshold, or None for plain mutual NN.
         mode: GTSFM_MATCH_INT_F16 (integer descriptors, MFMA) or GTSFM_MATCH_EXACT_F32.
+        groups: optional (n_groups, G) int32 device tensor of pair indices (-1 = empty slot) for the INT_F16 kernel:
+            every pair exactly once, the pairs of a group sharing image i1 (pair_groups builds one).
 
     Returns:
         idx: (P, kmax, 2) int32 tensor holding uint32 keypoint indices, rows [0, count) valid per pair.
@@ -49,11 +52,43 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
     ws = _workspace(ws_bytes, desc.device)
     if stream is not None:
         ws.record_stream(stream)  # the kernels may still read it after this function returns
-    rc = L.gtsfm_match_batched(_ptr(desc), _ptr(counts), n_img, kmax, dim, _ptr(pairs), n_pairs,
-                               -1.0 if ratio is None else float(ratio), mode, _ptr(ws), ws.numel(), _ptr(idx),
-                               _ptr(cnt), native.stream_handle(stream))
-    native.check(rc, "gtsfm_match_batched")
+    if groups is not None:
+        assert groups.is_cuda and groups.dtype == torch.int32 and groups.dim() == 2 and groups.is_contiguous()
+    rc = L.gtsfm_match_batched_grouped(
+        _ptr(desc), _ptr(counts), n_img, kmax, dim, _ptr(pairs), n_pairs,
+        _ptr(groups) if groups is not None else None, 0 if groups is None else groups.shape[0],
+        0 if groups is None else groups.shape[1], -1.0 if ratio is None else float(ratio), mode, _ptr(ws),
+        ws.numel(), _ptr(idx), _ptr(cnt), native.stream_handle(stream))
+    native.check(rc, "gtsfm_match_batched_grouped")
     return idx, cnt
+
+
+def match_group_size(kmax: int, dim: int) -> int:
+    """Largest pairs-per-workgroup the INT_F16 distance GEMM holds for this kmax / dim (0: not supported)."""
+    return int(native.lib().gtsfm_match_max_group(int(kmax), int(dim)))
+
+
+def pair_groups(pairs: np.ndarray, group_size: int) -> np.ndarray:
+    """Tile an (P, 2) pair list into groups for the INT_F16 distance GEMM: each group = up to `group_size` pairs
+    (i1, i2) sharing i1 (the register operand) with i2 in one block of `group_size` consecutive image ids, ordered
+    block-major, so the ~32 workgroups resident on one XCD stream the same few i2 images from its L2 while each reads
+    its own i1 once. Returns (n_groups, group_size) int32 pair indices, -1 for empty slots."""
+    pairs = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    P = len(pairs)
+    if P == 0 or group_size <= 1:
+        return np.arange(P, dtype=np.int32).reshape(-1, 1)
+    blk = pairs[:, 1] // group_size
+    order = np.lexsort((pairs[:, 1], pairs[:, 0], blk))  # block-major, then i1, then i2
+    key = blk[order] * (int(pairs[:, 0].max()) + 1) + pairs[order, 0]
+    starts = np.flatnonzero(np.r_[True, key[1:] != key[:-1]])
+    sizes = np.diff(np.r_[starts, P])
+    rank = np.arange(P) - np.repeat(starts, sizes)           # position inside its (block, i1) run
+    n_sub = -(-sizes // group_size)                           # groups per run (> 1 only for repeated pairs)
+    first = np.r_[0, np.cumsum(n_sub)[:-1]]
+    gid = np.repeat(first, sizes) + rank // group_size
+    out = np.full((int(n_sub.sum()), group_size), -1, dtype=np.int32)
+    out[gid, rank % group_size] = order
+    return out
 
 
 class RansacResult:

@@ -56,6 +56,12 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_double, c_int, c_void_p, c_size_t, c_void_p,
          c_void_p, c_void_p],
     ),
+    "gtsfm_match_batched_grouped": (
+        c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_double, c_int, c_void_p,
+         c_size_t, c_void_p, c_void_p, c_void_p],
+    ),
+    "gtsfm_match_max_group": (c_int, [c_int, c_int]),
     "gtsfm_match_set_kernel_events": (c_int, [c_void_p, c_void_p]),
     "gtsfm_ransac_workspace_bytes": (c_size_t, [c_int, c_int]),
     "gtsfm_ransac_E_batched": (

@@ -160,3 +160,62 @@ def test_mfma_distance_is_exact_integer(dev, oracle_mod):
     b = a[::-1].copy()
     b[:, 100] = np.arange(64, dtype=np.float32)
     np.testing.assert_array_equal(match_descriptor_pair(a, b, None), oracle_mod.twoway_match(a, b, None))
+
+
+def _batch(dev, descs):
+    counts = [len(d) for d in descs]
+    kmax = max(counts)
+    host = np.zeros((len(descs), kmax, descs[0].shape[1]), np.float32)
+    for i, d in enumerate(descs):
+        host[i, : len(d)] = d
+    return torch.from_numpy(host).to(dev), torch.tensor(counts, dtype=torch.int32, device=dev)
+
+
+def test_grouped_workgroups_vs_oracle(dev, oracle_mod):
+    """The distance GEMM with several pairs per workgroup (gtsfm_match_batched_grouped): block-tiled groups from
+    pair_groups, and hand-made groups whose pairs do NOT share image i1 (the A-fragment reload path), both equal the
+    oracle pair for pair; so does a group list in reverse order with empty slots."""
+    from gtsfm_amd import device, native
+
+    rng = np.random.default_rng(31)
+    counts = [2048, 1300, 2048, 700, 1999, 2048, 513, 1024, 1]
+    descs = [_sift_like(rng, n) for n in counts]
+    for i in range(1, len(counts)):
+        k = min(counts[i], counts[0]) // 3
+        descs[i][:k] = np.clip(descs[0][:k] + rng.integers(-6, 7, size=(k, 128)), 0, 255)
+    d, c = _batch(dev, descs)
+    pairs = np.array([(i, j) for i in range(len(counts)) for j in range(i + 1, len(counts))], np.int32)
+    G = device.match_group_size(max(counts), 128)
+    assert G >= 2
+    tiled = device.pair_groups(pairs, G)
+    mixed = np.full((-(-len(pairs) // G), G), -1, np.int32)
+    mixed.flat[: len(pairs)] = np.arange(len(pairs))[::-1]
+    pt = torch.from_numpy(pairs).to(dev)
+    refs = [oracle_mod.twoway_match(descs[i], descs[j], 0.8) for i, j in pairs]
+    for groups in (tiled, mixed):
+        idx, cnt = device.match_pairs(d, c, pt, 0.8, native.GTSFM_MATCH_INT_F16,
+                                      groups=torch.from_numpy(groups).to(dev))
+        idx = idx.cpu().numpy().view(np.uint32)
+        cnt = cnt.cpu().numpy()
+        for p in range(len(pairs)):
+            np.testing.assert_array_equal(idx[p, : cnt[p]], refs[p], err_msg=f"pair {tuple(pairs[p])}")
+
+
+def test_contract_edge_norms_exact(dev, oracle_mod):
+    """Descriptors at the INT_F16 contract's edge (values up to 1023, squared norms just under 2^19): the folded
+    accumulator d2 + code/16 stays exact, so the matches equal the oracle's."""
+    from gtsfm_amd.frontend.matcher.twoway_matcher import match_descriptor_pair
+
+    rng = np.random.default_rng(41)
+    n, dim = 600, 128
+    a = np.zeros((n, dim), np.float32)
+    a[:, 0] = 724.0                                   # 724^2 = 524176 < 2^19
+    a[:, 1:4] = rng.integers(0, 6, size=(n, 3))       # small spread keeps |a|^2 < 2^19
+    b = np.zeros((n, dim), np.float32)
+    b[:, 1] = 724.0                                   # orthogonal to a: d2 ~ 2^20 - small
+    b[:, 2:5] = rng.integers(0, 6, size=(n, 3))
+    b[:200] = a[:200] + rng.integers(0, 2, size=(200, dim)) * (np.arange(dim) > 100)
+    assert (np.sum(a.astype(np.float64) ** 2, 1) < 2 ** 19).all() and (np.sum(b.astype(np.float64) ** 2, 1) < 2 ** 19).all()
+    for ratio in (0.8, None):
+        np.testing.assert_array_equal(match_descriptor_pair(a, b, ratio), oracle_mod.twoway_match(a, b, ratio))
+        np.testing.assert_array_equal(match_descriptor_pair(b, a, ratio), oracle_mod.twoway_match(b, a, ratio))
