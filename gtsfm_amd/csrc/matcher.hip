@@ -121,8 +121,11 @@ __global__ void pack_code_kernel(const float* __restrict__ desc, const int* __re
 // its A rows once and streams each pair's B image in turn (unit order: pass, slot, column unit). Groups are laid out
 // by the caller (gtsfm_match_batched_grouped) so that the ~32 workgroups resident on one XCD stream the same few B
 // images out of that XCD's L2 while each reads its own A image once.
-// Columns: each wave merges its per-lane top-2 into the pair's LDS column state with two LDS atomics per tile
-// (k1 -> ds_min_rtn on C1; min(max(old, k1), k2) -> ds_min on C2 keeps the exact top-2 under any interleaving).
+// B copies are staged through VGPRs (global_load_dwordx4 at the start of an even phase, ds_write_b128 at its end):
+// no LDS-DMA, whose per-instruction issue cost and LDS-alias waits showed up as whole-phase stalls.
+// Columns: each wave writes its per-(lane-half, column) top-2 keys to an LDS partial buffer with plain stores; one
+// phase later all 8 waves merge the unit's 16 partials per column (a lane per partial pair, three ds_swizzle steps)
+// into the pair's column state, 8 columns per wave.
 // Rows: value-only top-2 in registers across a pass; at the pass's last unit one 5-step halving exchange leaves lane
 // l of each half-wave with row l's top-2, stored to rowres.
 // ---------------------------------------------------------------------------------------------
@@ -133,9 +136,6 @@ constexpr int kPpRowsPerPass = kPpWaves * 64;  // 512
 constexpr int kUnitCols = 64;
 constexpr int kMaxGroup = 4;
 constexpr int kPpLdsBudget = 160 * 1024;
-#ifndef GTSFM_PP_DMA_MODE
-#define GTSFM_PP_DMA_MODE 0  // 0: every wave issues its share at the end of even phases; 1: group 1 at the start of E
-#endif
 constexpr int kRowAlign = 256;                 // kpad granularity of the packed forms
 
 template <int NK>
@@ -143,16 +143,11 @@ struct PpCfg {
     static constexpr int kDa = NK * 16;
     static constexpr int kChunkBytes = 32 * kDa * 2;    // one 32-column MFMA tile of B (9 KiB at NK = 9)
     static constexpr int kUnitBytes = 2 * kChunkBytes;  // 64 columns
-    static constexpr int kPieces = kUnitBytes / 1024;   // 1-KiB LDS-DMA wave-instructions per unit
-    static constexpr int kPiecesPerWave = GTSFM_PP_DMA_MODE == 1 ? (kPieces + 3) / 4 : (kPieces + 7) / 8;
-    static_assert(kUnitBytes % 1024 == 0, "unit must be whole 1-KiB LDS-DMA pieces");
+    static constexpr int kPieces = kUnitBytes / 1024;   // 1-KiB wave copies (lane l: bytes [16l, 16l+16)) per unit
+    static constexpr int kPiecesPerWave = (kPieces + 7) / 8;
+    static_assert(kUnitBytes % 1024 == 0, "unit must be whole 1-KiB pieces");
 };
-
-// Async HBM -> LDS copy of one 1-KiB piece by one wave (lane l moves bytes [16l, 16l+16)).
-__device__ __forceinline__ void glds16(const void* gsrc, void* ldst) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                     (__attribute__((address_space(3))) void*)ldst, 16, 0, 0);
-}
+typedef unsigned pp_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
@@ -217,7 +212,6 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                                                                uint2* __restrict__ rowres,
                                                                uint2* __restrict__ colres) {
     using Cfg = PpCfg<NK>;
-    // the B ring is its own LDS object, so the LDS-DMA into it provably never aliases the column state's atomics
     __shared__ __attribute__((aligned(1024))) unsigned char ring[2 * Cfg::kUnitBytes];
     __shared__ int sinfo[kMaxGroup * 8];
     extern __shared__ __attribute__((aligned(16))) uint32_t colstate[];  // [G][2][kmax64]
@@ -282,18 +276,20 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         advance(it);
     }
 
-    // LDS-DMA of one unit's 64 B columns (contiguous kUnitBytes in the B form) into ring buffer `buf`
-    auto issue_unit = [&](const PpIter& it) {
-        const unsigned char* src = (const unsigned char*)(b_form + ((size_t)it.cur.img_b * kpad + it.sc * kUnitCols) *
-                                                                       Cfg::kDa) + lane * 16;
-        unsigned char* dst = ring + (it.seq & 1) * Cfg::kUnitBytes;
-        // a fixed count per wave (surplus pieces rewrite a piece with the same bytes), so the compiler's vmcnt for a
-        // later A-fragment use can count past them instead of draining the DMA
+    // B unit copy, staged through VGPRs: this wave's kPiecesPerWave 1-KiB pieces (surplus pieces repeat one).
+    pp_u32x4 stage[Cfg::kPiecesPerWave];
+    auto stage_load = [&](const PpIter& it) {
+        const unsigned char* src =
+            (const unsigned char*)(b_form + ((size_t)it.cur.img_b * kpad + it.sc * kUnitCols) * Cfg::kDa) + lane * 16;
 #pragma unroll
-        for (int i = 0; i < Cfg::kPiecesPerWave; ++i) {
-            const int q = GTSFM_PP_DMA_MODE == 1 ? ((wave & 3) + 4 * i) % Cfg::kPieces : (wave + kPpWaves * i) % Cfg::kPieces;
-            glds16(src + q * 1024, dst + q * 1024);
-        }
+        for (int i = 0; i < Cfg::kPiecesPerWave; ++i)
+            stage[i] = *(const pp_u32x4*)(src + ((wave + kPpWaves * i) % Cfg::kPieces) * 1024);
+    };
+    auto stage_store = [&](const PpIter& it) {
+        unsigned char* dst = ring + (it.seq & 1) * Cfg::kUnitBytes + lane * 16;
+#pragma unroll
+        for (int i = 0; i < Cfg::kPiecesPerWave; ++i)
+            *(pp_u32x4*)(dst + ((wave + kPpWaves * i) % Cfg::kPieces) * 1024) = stage[i];
     };
 
     half8 afrag[2][NK];
@@ -312,7 +308,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 #pragma unroll
             for (int s = 0; s < NK; ++s) afrag[t][s] = *(const half8*)(arow + 16 * s);
         }
-        __builtin_amdgcn_s_waitcnt(0x0070);  // here, so the MFMA stream never waits on the in-flight LDS-DMA
+        __builtin_amdgcn_s_waitcnt(0x0070);  // here: the MFMA stream after the join carries no A-load waits
     };
 
     const uint32_t dsat = (1u << (32 - ib)) - 1u;
@@ -323,35 +319,33 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
     f32x16 acc[2][2];  // [sub (32-column tile)][t (32-row tile)]
 
-    PpIter work = first, dma = first;
-    if (first.valid) {
-        issue_unit(dma);
-        advance(dma);
+    PpIter work = first, cpy = first;
+    if (first.valid) {  // unit 0 -> ring[0]
+        stage_load(cpy);
+        stage_store(cpy);
+        advance(cpy);
     }
-    __syncthreads();  // unit 0 landed (vmcnt(0) + barrier)
+    __syncthreads();
 
-    // Phase barriers order LDS only. The LDS-DMA of unit k+1 is issued at the end of phase 2k (by every wave: group
-    // 0 right after its M(k), group 1 right after its E(k-1)) and waited for at the end of phase 2k+1, so it has a
-    // whole phase to land and nothing drains it earlier.
-    auto phase_barrier = [&](bool drain_dma) {
-        if (drain_dma) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) expcnt(7) lgkmcnt(0)
-        else __builtin_amdgcn_s_waitcnt(0xC07F);            // lgkmcnt(0), vmcnt/expcnt untouched
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    };
-    auto dma_next = [&]() {
-        if (dma.valid) {
-            issue_unit(dma);
-            advance(dma);
+    // Phases (one barrier each): group 0 runs M(k) in phase 2k and E(k) in phase 2k+1, group 1 one phase later. Every
+    // wave loads its share of unit k+1 into VGPRs at the start of phase 2k and stores it at the end of phase 2k+1
+    // into the ring buffer unit k-1 held (free since phase 2k-1): two phases of latency cover an HBM miss.
+    PpIter cpy_pending;
+    bool pending = false;
+    auto copy_begin = [&]() {
+        pending = cpy.valid;
+        if (pending) {
+            cpy_pending = cpy;
+            stage_load(cpy);
+            advance(cpy);
         }
     };
-    if (grp == 1 && n_units > 0) {  // group 1's leading phase 0: idle
-        if (GTSFM_PP_DMA_MODE == 0 || true) dma_next();
-        phase_barrier(false);
-    }
-    // One unit per iteration, straight-line M then E for both groups (group 1 one phase behind):
-    //   group 0: M(k) = phase 2k, E(k) = phase 2k+1;   group 1: M(k) = phase 2k+1, E(k) = phase 2k+2.
+    auto copy_end = [&]() {
+        if (pending) stage_store(cpy_pending);
+        pending = false;
+    };
+    if (grp == 1 && n_units > 0) copy_begin();  // group 1's leading phase 0: the load of unit 1
+    if (grp == 1 && n_units > 0) __syncthreads();
 #ifdef GTSFM_PP_STAMPS
     unsigned long long st[4] = {0, 0, 0, 0};
 #endif
@@ -360,53 +354,55 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         const PpSlot si = work.cur;
         const int r0w = work.pass * kPpRowsPerPass + wave * 64;
         const bool rows_here = r0w < si.na;
-        // ---- M: 2 x 2 tiles of 32 x 32, K = 16 NK. A new (pass, A image) reloads the A fragments first (once per
-        // pass: a short stall the partner wave's E covers).
+        // ---- phase A of this iteration: group 0 -> phase 2k (copy of unit k+1), group 1 -> phase 2k+1 (merge k-1)
+        // M: 2 x 2 tiles of 32 x 32, K = 16 NK. A new (pass, A image) reloads the A fragments first (once per pass:
+        // a short stall the partner wave's E covers).
         load_a(si.img_a, work.pass);
+        if (grp == 0) copy_begin();  // after the A loads, so the MFMAs never wait for the staged copy
         __builtin_amdgcn_s_setprio(2);  // the MFMA stream outranks the partner wave's VALU epilogue for issue
-#ifdef GTSFM_PP_SKIP_M
-        if (false) {
-#else
         if (rows_here) {
-#endif
             const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
+            half8 bf[2][2];  // [k-step parity][sub]: the next k-step's B fragments are read ahead
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) bf[0][sub] = *(const half8*)(bb + sub * Cfg::kChunkBytes);
 #pragma unroll
             for (int s = 0; s < NK; ++s) {
+                if (s + 1 < NK) {
+#pragma unroll
+                    for (int sub = 0; sub < 2; ++sub)
+                        bf[(s + 1) & 1][sub] = *(const half8*)(bb + sub * Cfg::kChunkBytes + 1024 * (s + 1));
+                }
 #pragma unroll
                 for (int sub = 0; sub < 2; ++sub) {
-                    const half8 bf = *(const half8*)(bb + sub * Cfg::kChunkBytes + 1024 * s);
-                    acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf, acc[sub][0], 0, 0, 0);
-                    acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf, acc[sub][1], 0, 0, 0);
+                    acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf[s & 1][sub], acc[sub][0], 0, 0, 0);
+                    acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf[s & 1][sub], acc[sub][1], 0, 0, 0);
                 }
             }
         }
+        if (grp == 1) copy_end();  // loaded at the start of phase 2k
         PP_STAMP(t1);
-        if (GTSFM_PP_DMA_MODE == 0 && grp == 0) dma_next();
-        phase_barrier(grp == 1);
+        __syncthreads();
         PP_STAMP(t2);
-        // ---- E
+        // ---- phase B: group 0 -> phase 2k+1, group 1 -> phase 2k+2 (load of unit k+2)
         __builtin_amdgcn_s_setprio(0);
-        if (GTSFM_PP_DMA_MODE == 1 && grp == 1) dma_next();
-#ifdef GTSFM_PP_SKIP_E
-        if (false) {
-#else
+        if (grp == 1) copy_begin();
         if (rows_here) {
-#endif
             // rows: both column tiles' values of row (t, g) in one paired insert
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int g = 0; g < 16; ++g)
                     ins2(rb1[t][g], rb2[t][g], __float_as_uint(acc[0][t][g]), __float_as_uint(acc[1][t][g]));
-            // columns: value-only top-2 over the lane's 16 rows of each (column tile, row tile), then keys
-            // (d2 << ib) | row with row = rowbase | code; all four returning atomics issued before any wait
-            uint32_t* c1s = colstate + work.slot * 2 * kmax64;
-            uint32_t* c2s = c1s + kmax64;
-            uint32_t k1[2][2], k2[2][2], old[2][2];
+            // columns: value-only top-2 over the lane's 16 rows of each (column tile, row tile) -> keys
+            // (d2 << ib) | row with row = rowbase | code; the two row tiles merged; a permlane32 swap then gives lane L
+            // both halves' top-2 of column tile L >> 5, column L & 31, so lane L owns unit column L: one returning
+            // atomic min on C1 and one on C2 per lane (min(max(old, k1), k2) keeps the exact top-2 in any order)
+            uint32_t s1[2], s2[2];
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) {
+                uint32_t k1[2], k2[2];
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
                     const f32x16& a = acc[sub][t];
@@ -418,23 +414,18 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                     uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
                     if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
                     const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 16 * half);
-                    k1[sub][t] = (d1 << ib) | rowbase | (u & 15u);
-                    k2[sub][t] = d2 << ib;  // the second's index never matters
+                    k1[t] = (d1 << ib) | rowbase | (u & 15u);
+                    k2[t] = d2 << ib;  // the second's index never matters
                 }
+                s1[sub] = umin(k1[0], k1[1]);
+                s2[sub] = med3u(k1[0], k1[1], umin(k2[0], k2[1]));
             }
-            const int col0 = work.sc * kUnitCols + lrow;
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-                    old[sub][t] = __hip_atomic_fetch_min(&c1s[col0 + 32 * sub], k1[sub][t], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-                for (int t = 0; t < 2; ++t)
-                    __hip_atomic_fetch_min(&c2s[col0 + 32 * sub], umin(umax(old[sub][t], k1[sub][t]), k2[sub][t]),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const auto x1 = __builtin_amdgcn_permlane32_swap(s1[0], s1[1], false, false);
+            const auto x2 = __builtin_amdgcn_permlane32_swap(s2[0], s2[1], false, false);
+            const uint32_t m1 = umin(x1[0], x1[1]), m2 = med3u(x1[0], x1[1], umin(x2[0], x2[1]));
+            uint32_t* c1s = colstate + work.slot * 2 * kmax64 + work.sc * kUnitCols + lane;
+            const uint32_t old = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_min(c1s + kmax64, umin(umax(old, m1), m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (work.sc == si.nsup - 1) {
                 // the pass is over for this pair: halving exchange across each half-wave's 32 lanes, then lane
                 // (lrow, half) holds register j = lrow = 16 t + g, i.e. keypoint r0w + 32 t + 16 half + g
@@ -459,10 +450,10 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                 for (int j = 0; j < 32; ++j) x1[j] = x2[j] = kNoKey;
             }
         }
+        if (grp == 0) copy_end();  // loaded in phase 2k
         advance(work);
         PP_STAMP(t3);
-        if (GTSFM_PP_DMA_MODE == 0 && grp == 1) dma_next();
-        phase_barrier(grp == 0);
+        __syncthreads();
         PP_STAMP(t4);
 #ifdef GTSFM_PP_STAMPS
         st[0] += t1 - t0; st[1] += t2 - t1; st[2] += t3 - t2; st[3] += t4 - t3;
@@ -472,7 +463,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
     if (lane == 0)
         for (int i = 0; i < 4; ++i) atomicAdd(&g_pp_stamps[wave * 4 + i], st[i]);
 #endif
-    if (grp == 0 && n_units > 0) phase_barrier(false);  // group 0's trailing phase 2U: idle
+    if (grp == 0 && n_units > 0) __syncthreads();  // group 0's trailing phase 2U (group 1's E of the last unit)
     __syncthreads();
     for (int s = 0; s < G; ++s) {
         const PpSlot si = slot_info(s);
@@ -747,7 +738,8 @@ inline size_t pp_dyn_lds_bytes(int kmax, int group_size) {
 }
 template <int NK>
 size_t pp_lds_bytes(int kmax, int group_size) {
-    return 2 * (size_t)PpCfg<NK>::kUnitBytes + kMaxGroup * 8 * sizeof(int) + pp_dyn_lds_bytes(kmax, group_size);
+    return 2 * (size_t)PpCfg<NK>::kUnitBytes + kMaxGroup * 8 * sizeof(int) +
+           pp_dyn_lds_bytes(kmax, group_size);  // B ring + slot table (static) + column state
 }
 
 // Largest group size (pairs per workgroup) whose column state fits the LDS next to the B ring.
@@ -1237,9 +1229,6 @@ int gtsfm_match_batched_grouped(const float* d_desc, const int* d_counts, int n_
         }
         if (rc != GTSFM_OK) return rc;
         if (g_mnn_events[1]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[1], stream));
-#if defined(GTSFM_PP_SKIP_E) || defined(GTSFM_PP_SKIP_M)
-        return GTSFM_OK;  // timing-only diagnostic builds (tools/build_variants.sh): no results
-#endif
         return launch_finalize<kResCodes>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, ib, ratio,
                                           d_out_idx, d_out_count, stream);
     }

@@ -65,8 +65,13 @@ class HipKernels:
     def sift(self, images, kpts, out, workspace):
         self._dev.sift_extract(images, kpts, out=out, workspace=workspace)
 
-    def match(self, desc, counts, pairs, ratio):
-        return self._dev.match_pairs(desc, counts, pairs, ratio, self._native.GTSFM_MATCH_INT_F16)
+    def match_groups(self, pairs: np.ndarray, kmax: int, dim: int) -> Optional[np.ndarray]:
+        """Block-tiled pair groups for the distance GEMM (gtsfm_match_batched_grouped), or None."""
+        g = self._dev.match_group_size(kmax, dim)
+        return self._dev.pair_groups(pairs, g) if g > 1 else None
+
+    def match(self, desc, counts, pairs, ratio, groups=None):
+        return self._dev.match_pairs(desc, counts, pairs, ratio, self._native.GTSFM_MATCH_INT_F16, groups=groups)
 
     def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_id_base):
         return self._dev.ransac_essential(xy, intr, pairs, idx, cnt, thresh_px, pair_id_base=pair_id_base)
@@ -171,6 +176,12 @@ class AllPairsFrontEnd:
         self.intr = torch.from_numpy(intr).to(self.dev)
         pc = max(1, self.cfg.pair_chunk)
         self.pchunks = [(a, min(a + pc, P)) for a in range(0, P, pc)]
+        # per pair chunk: workgroup groups of the distance GEMM (pairs sharing i1, i2 blocked), laid out once
+        slot_pairs = slot[self.my_pairs].astype(np.int32)
+        self.pgroups = []
+        for a, b in self.pchunks:
+            g = self.kern.match_groups(slot_pairs[a:b], k, 128) if hasattr(self.kern, "match_groups") else None
+            self.pgroups.append(None if g is None else torch.from_numpy(g).to(self.dev))
 
         # compact results on the device: per chunk c, offsets rows [a + c, b + c] and verified rows from a * k
         nc = len(self.pchunks)
@@ -255,7 +266,7 @@ class AllPairsFrontEnd:
         n_hyp, n_models, n_match = [], [], []
         for c, (a, b) in enumerate(self.pchunks):
             pairs = self.pairs_dev[a:b]
-            idx, mcnt = self.kern.match(desc_all, cnt_all, pairs, cfg.ratio)
+            idx, mcnt = self.kern.match(desc_all, cnt_all, pairs, cfg.ratio, groups=self.pgroups[c])
             self._mark("match")
             res = self.kern.verify(xy_all, self.intr, pairs, idx, mcnt, cfg.thresh_px, self.pair_id_base + a)
             self._mark("verify")

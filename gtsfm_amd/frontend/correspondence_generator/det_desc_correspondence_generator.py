@@ -69,10 +69,12 @@ def match_pairs_batched(feats: DeviceFeatures, image_pairs: Sequence[Tuple[int, 
     out: Dict[Tuple[int, int], np.ndarray] = {}
     pairs = np.asarray(image_pairs, dtype=np.int64).reshape(-1, 2)
     dev = feats.desc.device
+    G = device.match_group_size(feats.desc.shape[1], feats.desc.shape[2]) if mode == native.GTSFM_MATCH_INT_F16 else 0
     for s in range(0, len(pairs), chunk):
         blk = pairs[s: s + chunk]
+        groups = torch.from_numpy(device.pair_groups(blk, G)).to(dev) if G > 1 else None
         idx, cnt = device.match_pairs(feats.desc, feats.count, torch.from_numpy(blk.astype(np.int32)).to(dev),
-                                      ratio, mode)
+                                      ratio, mode, groups=groups)
         cnt_h = cnt.cpu().numpy()
         width = int(cnt_h.max()) if len(cnt_h) else 0
         idx_h = idx[:, :width].cpu().numpy().view(np.uint32)

@@ -53,8 +53,9 @@ const char* gtsfm_hip_target(void);
  * mode GTSFM_MATCH_EXACT_F32: any float descriptors; distances are sum_k (a_k-b_k)^2 in float32,
  *      sequential k (bit-exact with the oracle; equals OpenCV for integer data or dim == 1).
  * mode GTSFM_MATCH_INT_F16:   integer-valued descriptors in [0, 1023] with squared norm < 2^19
- *      (every SIFT descriptor). One fp16 MFMA distance GEMM per pair with the norms folded into
- *      extra K columns, fused row/column top-2. Exact integer arithmetic: bit-identical to EXACT_F32.
+ *      (every SIFT descriptor). One fp16 MFMA distance GEMM per pair with the norms and a 4-bit row code
+ *      folded into extra K columns (every accumulator is d2 + code/16, exact in any summation order), fused
+ *      row/column top-2. Exact integer arithmetic: bit-identical to EXACT_F32.
  *      kmax <= 8192, dim <= 139. (EXACT_F32: kmax <= 65535.)
  * mode GTSFM_MATCH_F16_RERANK: any float descriptors with dim <= 256 (e.g. SuperPoint's 256-D unit vectors).
  *      An fp16 MFMA distance GEMM shortlists 8 candidates per keypoint and side, an exact fp32 re-rank with
@@ -71,6 +72,23 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
 int gtsfm_match_batched(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim,
                         const int* d_pairs, int n_pairs, double ratio, int mode, void* d_workspace,
                         size_t workspace_bytes, uint32_t* d_out_idx, int* d_out_count, void* stream);
+
+/* gtsfm_match_batched with the INT_F16 distance GEMM's work laid out by the caller (no reference counterpart: the
+ * reference matches one pair per call, twoway_matcher.py:42-144 via det_desc_correspondence_generator.py:60-75).
+ * d_groups[n_groups][group_size] lists pair indices (-1 = empty slot); every pair must appear exactly once, and the
+ * pairs of one group should share image i1 (the operand a workgroup keeps in registers: it is then read once per
+ * group instead of once per pair; a group mixing i1 images is correct, only slower). group_size <=
+ * gtsfm_match_max_group(kmax, dim). Group order sets which workgroups run side by side on an XCD: consecutive groups
+ * that stream the same few i2 images share that XCD's L2. d_groups == NULL is gtsfm_match_batched. Other modes
+ * ignore the groups. */
+int gtsfm_match_batched_grouped(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim,
+                                const int* d_pairs, int n_pairs, const int* d_groups, int n_groups, int group_size,
+                                double ratio, int mode, void* d_workspace, size_t workspace_bytes,
+                                uint32_t* d_out_idx, int* d_out_count, void* stream);
+
+/* Largest group_size gtsfm_match_batched_grouped accepts for this kmax / dim (its LDS holds the column state of every
+ * pair of a group); 0 when INT_F16 does not support the shape. */
+int gtsfm_match_max_group(int kmax, int dim);
 
 /* Measurement hook (no reference counterpart): hipEvent_t handles recorded on the call's stream immediately before
  * and after the distance-GEMM kernel of every later GTSFM_MATCH_INT_F16 gtsfm_match_batched call, so a benchmark can

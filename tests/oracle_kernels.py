@@ -39,7 +39,7 @@ class OracleKernels:
             out.count[i] = n
             out.n_detected[i] = nd
 
-    def match(self, desc, counts, pairs, ratio):
+    def match(self, desc, counts, pairs, ratio, groups=None):  # groups only lay out GPU work
         P, kmax = pairs.shape[0], desc.shape[1]
         idx = torch.zeros((P, kmax, 2), dtype=torch.int32)
         cnt = torch.zeros(P, dtype=torch.int32)
