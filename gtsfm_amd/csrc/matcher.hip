@@ -196,7 +196,7 @@ struct PpIter {
 };
 
 #ifdef GTSFM_PP_STAMPS  // diagnostic builds only: per-wave cycle sums of M, barrier after M, E, barrier after E
-__device__ unsigned long long g_pp_stamps[kPpWaves * 4];
+__device__ unsigned long long g_pp_stamps[kPpWaves * 8];
 #define PP_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
 #else
 #define PP_STAMP(v)
@@ -347,7 +347,8 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
     if (grp == 1 && n_units > 0) copy_begin();  // group 1's leading phase 0: the load of unit 1
     if (grp == 1 && n_units > 0) __syncthreads();
 #ifdef GTSFM_PP_STAMPS
-    unsigned long long st[4] = {0, 0, 0, 0};
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long te0 = 0, te1 = 0, te2 = 0, te3 = 0;
 #endif
     for (int k = 0; k < n_units; ++k) {
         PP_STAMP(t0);
@@ -388,13 +389,13 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         // ---- phase B: group 0 -> phase 2k+1, group 1 -> phase 2k+2 (load of unit k+2)
         __builtin_amdgcn_s_setprio(0);
         if (grp == 1) copy_begin();
+#ifdef GTSFM_PP_STAMPS
+        te0 = te1 = te2 = te3 = __builtin_amdgcn_s_memtime();
+#endif
         if (rows_here) {
-            // rows: both column tiles' values of row (t, g) in one paired insert
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int g = 0; g < 16; ++g)
-                    ins2(rb1[t][g], rb2[t][g], __float_as_uint(acc[0][t][g]), __float_as_uint(acc[1][t][g]));
+#ifdef GTSFM_PP_STAMPS
+            te1 = __builtin_amdgcn_s_memtime();
+#endif
             // columns: value-only top-2 over the lane's 16 rows of each (column tile, row tile) -> keys
             // (d2 << ib) | row with row = rowbase | code; the two row tiles merged; a permlane32 swap then gives lane L
             // both halves' top-2 of column tile L >> 5, column L & 31, so lane L owns unit column L: one returning
@@ -423,9 +424,24 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
             const auto x1 = __builtin_amdgcn_permlane32_swap(s1[0], s1[1], false, false);
             const auto x2 = __builtin_amdgcn_permlane32_swap(s2[0], s2[1], false, false);
             const uint32_t m1 = umin(x1[0], x1[1]), m2 = med3u(x1[0], x1[1], umin(x2[0], x2[1]));
+#ifdef GTSFM_PP_STAMPS
+            te2 = __builtin_amdgcn_s_memtime();
+#endif
             uint32_t* c1s = colstate + work.slot * 2 * kmax64 + work.sc * kUnitCols + lane;
             const uint32_t old = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // the row inserts run while the returning atomic is in flight
+            __builtin_amdgcn_sched_barrier(0);
+            // rows: both column tiles' values of row (t, g) in one paired insert
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int g = 0; g < 16; ++g)
+                    ins2(rb1[t][g], rb2[t][g], __float_as_uint(acc[0][t][g]), __float_as_uint(acc[1][t][g]));
+            __builtin_amdgcn_sched_barrier(0);
             __hip_atomic_fetch_min(c1s + kmax64, umin(umax(old, m1), m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef GTSFM_PP_STAMPS
+            te3 = __builtin_amdgcn_s_memtime();
+#endif
             if (work.sc == si.nsup - 1) {
                 // the pass is over for this pair: halving exchange across each half-wave's 32 lanes, then lane
                 // (lrow, half) holds register j = lrow = 16 t + g, i.e. keypoint r0w + 32 t + 16 half + g
@@ -457,11 +473,12 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         PP_STAMP(t4);
 #ifdef GTSFM_PP_STAMPS
         st[0] += t1 - t0; st[1] += t2 - t1; st[2] += t3 - t2; st[3] += t4 - t3;
+        st[4] += te1 - te0; st[5] += te2 - te1; st[6] += te3 - te2; st[7] += t3 - te3;
 #endif
     }
 #ifdef GTSFM_PP_STAMPS
     if (lane == 0)
-        for (int i = 0; i < 4; ++i) atomicAdd(&g_pp_stamps[wave * 4 + i], st[i]);
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_pp_stamps[wave * 8 + i], st[i]);
 #endif
     if (grp == 0 && n_units > 0) __syncthreads();  // group 0's trailing phase 2U (group 1's E of the last unit)
     __syncthreads();
@@ -1181,7 +1198,7 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
 int gtsfm_pp_stamps(unsigned long long* out) {  // diagnostic builds: read and clear the per-wave cycle sums
     GTSFM_CHECK_HIP(hipDeviceSynchronize());
     GTSFM_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pp_stamps), sizeof(g_pp_stamps)));
-    static const unsigned long long zero[kPpWaves * 4] = {};
+    static const unsigned long long zero[kPpWaves * 8] = {};
     GTSFM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), zero, sizeof(zero)));
     return GTSFM_OK;
 }

@@ -55,10 +55,11 @@ for name, groups in (("ungrouped", None), ("grouped", torch.from_numpy(device.pa
 print(json.dumps(out))
 if hasattr(L, "gtsfm_pp_stamps"):  # diagnostic build: per-wave cycles of one grouped launch
     import ctypes
-    buf = (ctypes.c_ulonglong * 32)()
+    buf = (ctypes.c_ulonglong * 64)()
     L.gtsfm_pp_stamps(buf)  # clear
     device.match_pairs(desc, counts, pairs, 0.8, groups=torch.from_numpy(device.pair_groups(pairs_np, G)).to(dev))
     L.gtsfm_pp_stamps(buf)
     units = P * 4 * 32  # 2048 rows: 4 passes x 32 column units per pair
-    st = np.array(list(buf), np.float64).reshape(8, 4) / units
-    print(json.dumps({"cycles_per_unit_per_wave [M, bar1, E, bar2]": st.round(0).tolist()}))
+    st = np.array(list(buf), np.float64).reshape(8, 8) / units
+    print(json.dumps({"cycles_per_unit_per_wave [M, bar1, E, bar2, E.rows, E.colkeys, E.atomics, E.rest]":
+                      st.round(0).tolist()}))
