@@ -61,7 +61,7 @@ def images_for(n_gpus: int, base: int = 100) -> int:
 
 
 def pmc_traffic():
-    """HBM bytes per mnn_mfma_kernel launch from the committed rocprofv3 --pmc summary of this bench's command
+    """HBM bytes per mnn_pp_kernel launch (the distance GEMM) from the committed rocprofv3 --pmc summary of this bench's command
     (profiles/*_mnn_pmc.json, written by tools/pmc_summary.py --json): FETCH_SIZE doubled per MI355X_MICROARCH.md
     (gfx950 tallies 128-B reads at 64 B) + WRITE_SIZE, in bytes. None when no summary is committed."""
     import glob
@@ -346,7 +346,7 @@ def main_frontend(args, info, config: str):
     roof = {"bound": "mfma", "achieved": round(match_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(match_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
             "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
-            "kernel": "mnn_mfma_kernel (one launch per pair chunk)", "kernel_ms": round(mnn_ms, 3),
+            "kernel": "mnn_pp_kernel (one launch per pair chunk)", "kernel_ms": round(mnn_ms, 3),
             "work": "2*K1*K2*128 flop per pair, summed over the last launch's %d pairs (GFLOP: %.1f of %.1f per step)"
                     % (len(pl), match_flop / 1e9, match_flop_all / 1e9)}
     roof["stages"] = {

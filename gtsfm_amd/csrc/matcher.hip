@@ -360,7 +360,13 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         // a short stall the partner wave's E covers).
         load_a(si.img_a, work.pass);
         if (grp == 0) copy_begin();  // after the A loads, so the MFMAs never wait for the staged copy
-        __builtin_amdgcn_s_setprio(2);  // the MFMA stream outranks the partner wave's VALU epilogue for issue
+#ifndef GTSFM_PP_PRIO_M
+#define GTSFM_PP_PRIO_M 2
+#endif
+#ifndef GTSFM_PP_PRIO_E
+#define GTSFM_PP_PRIO_E 0
+#endif
+        __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_M);  // the MFMA stream outranks the partner wave's VALU epilogue
         if (rows_here) {
             const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
 #pragma unroll
@@ -387,7 +393,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         __syncthreads();
         PP_STAMP(t2);
         // ---- phase B: group 0 -> phase 2k+1, group 1 -> phase 2k+2 (load of unit k+2)
-        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_E);
         if (grp == 1) copy_begin();
 #ifdef GTSFM_PP_STAMPS
         te0 = te1 = te2 = te3 = __builtin_amdgcn_s_memtime();
@@ -771,7 +777,7 @@ int pp_max_group(int kmax, int dim) {
 
 template <int NK, bool kClamp>
 int launch_pp_t(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
-                const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, uint2* rowres,
+                const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, int dim, uint2* rowres,
                 uint2* colres, hipStream_t stream) {
     const int gs = groups ? group_size : 1;
     if (pp_lds_bytes<NK>(kmax, gs) > (size_t)kPpLdsBudget) return GTSFM_ERR_ARG;
@@ -785,13 +791,13 @@ int launch_pp_t(const _Float16* a_form, const _Float16* b_form, const int* count
 
 template <int NK>
 int launch_pp(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
-              const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, uint2* rowres,
+              const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, int dim, uint2* rowres,
               uint2* colres, hipStream_t stream) {
     if (ib <= 12)
         return launch_pp_t<NK, false>(a_form, b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad,
-                                      kmax, ib, rowres, colres, stream);
+                                      kmax, ib, dim, rowres, colres, stream);
     return launch_pp_t<NK, true>(a_form, b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax,
-                                 ib, rowres, colres, stream);
+                                 ib, dim, rowres, colres, stream);
 }
 
 // side1 / side2: per-keypoint top-2 of image i1 / image i2 of each pair (encoding kRes)
@@ -1239,9 +1245,9 @@ int gtsfm_match_batched_grouped(const float* d_desc, const int* d_counts, int n_
         int rc;
         if (g_mnn_events[0]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[0], stream));
         switch (nk) {
-            case 2: rc = launch_pp<2>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, rowres, colres, stream); break;
-            case 5: rc = launch_pp<5>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, rowres, colres, stream); break;
-            case 9: rc = launch_pp<9>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, rowres, colres, stream); break;
+            case 2: rc = launch_pp<2>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, dim, rowres, colres, stream); break;
+            case 5: rc = launch_pp<5>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, dim, rowres, colres, stream); break;
+            case 9: rc = launch_pp<9>(a_form, b_form, d_counts, d_pairs, n_pairs, d_groups, ng, gs, kpad, kmax, ib, dim, rowres, colres, stream); break;
             default: return GTSFM_ERR_ARG;
         }
         if (rc != GTSFM_OK) return rc;

@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc counter_collection CSVs: per kernel, dispatches and mean counter value per dispatch.
 
     python tools/pmc_summary.py <dir-with-run_counter_collection.csv> [...] > summary.txt
-    python tools/pmc_summary.py --json OUT.json --kernel mnn_mfma_kernel <dirs...>
+    python tools/pmc_summary.py --json OUT.json --kernel mnn_pp_kernel <dirs...>
         -> {"hbm_bytes_per_launch": 2*FETCH_SIZE*1024 + WRITE_SIZE*1024, ...} for bench.py's roofline "traffic"
            (FETCH_SIZE doubled: gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md "HBM"; both in KiB)
 """
