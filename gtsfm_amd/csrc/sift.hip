@@ -190,8 +190,9 @@ __device__ __forceinline__ void up_coord(int x, int W, int& s0, int& s1, float& 
 template <int R, bool kFromU8>
 __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(const float* __restrict__ src,
                                                                   const uint8_t* __restrict__ img8, int C, int H0,
-                                                                  int W0, float* __restrict__ dst, int H, int W,
-                                                                  int n_tx, int n_ty, int n_img, Taps t) {
+                                                                  int W0, float* __restrict__ dst,
+                                                                  float* __restrict__ dec, int H, int W, int n_tx,
+                                                                  int n_ty, int n_img, Taps t) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     constexpr int kBlurTY = blur_ty(R, kFromU8), kBlurTYT = blur_tyt(R, kFromU8), kBlurColRows = kBlurTY / kBlurTYT;
     constexpr int IW = kBlurTX + 2 * R, IH = kBlurTY + 2 * R, IWP = blur_iwp(R);
@@ -346,15 +347,18 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
         for (int j = 1; j <= R; ++j)
             acc = __builtin_elementwise_fma(pf2{k[j], k[j]},
                                             pf2{c[R + q - j], c[R + q + 1 - j]} + pf2{c[R + q + j], c[R + q + 1 + j]}, acc);
-        const int y = y0 + ly0 + q;
+        const int y = y0 + ly0 + q;  // even: tiles, ly0 and q are
         if (y < H) dst[base + (size_t)y * W + x] = acc.x;
         if (y + 1 < H) dst[base + (size_t)(y + 1) * W + x] = acc.y;
+        // the next octave's base, cv::resize INTER_NEAREST to (H/2, W/2) of this level: pixel (2y', 2x')
+        if (dec != nullptr && (x & 1) == 0 && (x >> 1) < (W >> 1) && y < H && (y >> 1) < (H >> 1))
+            dec[(size_t)b * (H >> 1) * (W >> 1) + (size_t)(y >> 1) * (W >> 1) + (x >> 1)] = acc.x;
     }
 }
 
 template <bool kFromU8>
 struct BlurTable {
-    using Fn = void (*)(const float*, const uint8_t*, int, int, int, float*, int, int, int, int, int, Taps);
+    using Fn = void (*)(const float*, const uint8_t*, int, int, int, float*, float*, int, int, int, int, int, Taps);
     static Fn get(int r) {
         switch (r) {
 #define GTSFM_BLUR_CASE(RR) \
@@ -371,12 +375,6 @@ struct BlurTable {
     }
 };
 
-__global__ void decimate_kernel(const float* __restrict__ src, int Hs, int Ws, float* __restrict__ dst, int H,
-                                int W) {
-    const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, b = blockIdx.z;
-    if (x >= W) return;
-    dst[(size_t)b * H * W + (size_t)y * W + x] = src[(size_t)b * Hs * Ws + (size_t)(2 * y) * Ws + 2 * x];
-}
 
 // ------------------------------------------------------------------ kernels: detection
 struct GaussSet {
@@ -1180,7 +1178,7 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
 
     for (int i = 0; i < kLevels; ++i)
         if (taps[i].r < 1 || taps[i].r > kBlurMaxR) return GTSFM_ERR_ARG;
-    auto blur = [&](const float* src, float* dst, int h, int w, const Taps& t) -> int {
+    auto blur = [&](const float* src, float* dst, float* dec, int h, int w, const Taps& t) -> int {
         const bool u8 = src == nullptr;
         const int ty = blur_ty(t.r, u8), tyt = blur_tyt(t.r, u8);
         const int n_tx = (w + kBlurTX - 1) / kBlurTX, n_ty = (h + ty - 1) / ty;
@@ -1194,22 +1192,21 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         }
         if (u8)
             hipLaunchKernelGGL(BlurTable<true>::get(t.r), grid, dim3(kBlurTX, tyt), lds, stream, nullptr,
-                               d_images, channels, H, W, dst, h, w, n_tx, n_ty, B, t);
+                               d_images, channels, H, W, dst, dec, h, w, n_tx, n_ty, B, t);
         else
             hipLaunchKernelGGL(BlurTable<false>::get(t.r), grid, dim3(kBlurTX, tyt), lds, stream, src, nullptr, 0,
-                               0, 0, dst, h, w, n_tx, n_ty, B, t);
+                               0, 0, dst, dec, h, w, n_tx, n_ty, B, t);
         return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
     };
     for (int o = 0; o < L.n_oct; ++o) {
         const int h = L.Ho[o], w = L.Wo[o];
-        if (o == 0) {
-            if (blur(nullptr, F(L.g[0][0]), h, w, taps[0])) return GTSFM_ERR_HIP;
-        } else {
-            hipLaunchKernelGGL(decimate_kernel, dim3((w + 255) / 256, h, B), dim3(256), 0, stream,
-                               F(L.g[o - 1][kLayers]), L.Ho[o - 1], L.Wo[o - 1], F(L.g[o][0]), h, w);
+        // octave o > 0 starts from the layer-3 level of octave o - 1, decimated by that level's blur launch
+        if (o == 0 && blur(nullptr, F(L.g[0][0]), nullptr, h, w, taps[0])) return GTSFM_ERR_HIP;
+        for (int i = 1; i < kLevels; ++i) {
+            float* dec = (i == kLayers && o + 1 < L.n_oct) ? F(L.g[o + 1][0]) : nullptr;
+            if (dec && (L.Ho[o + 1] != h / 2 || L.Wo[o + 1] != w / 2)) return GTSFM_ERR_ARG;
+            if (blur(F(L.g[o][i - 1]), F(L.g[o][i]), dec, h, w, taps[i])) return GTSFM_ERR_HIP;
         }
-        for (int i = 1; i < kLevels; ++i)
-            if (blur(F(L.g[o][i - 1]), F(L.g[o][i]), h, w, taps[i])) return GTSFM_ERR_HIP;
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
         GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, (kCandShards + 16) * sizeof(int), stream));
