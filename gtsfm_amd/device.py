@@ -396,3 +396,53 @@ def superglue_log_assignment(workspace: torch.Tensor, n_pairs: int, kmax: int, p
                                                      native.stream_handle(stream))
     native.check(rc, "gtsfm_superglue_log_assignment")
     return out
+
+
+def retrieval_similarity(desc: torch.Tensor, blocksize: int,
+                         stream: Optional[torch.cuda.Stream] = None) -> torch.Tensor:
+    """(N, N) f32 block-upper-triangular similarity of N global descriptors (N, D) f32 on the device
+    (gtsfm_retrieval_similarity; netvlad_retriever.py:77-149)."""
+    if desc.dim() != 2 or desc.dtype != torch.float32 or not desc.is_cuda:
+        raise ValueError("desc must be a (N, D) float32 device tensor")
+    desc = desc.contiguous()
+    n, d = desc.shape
+    sim = torch.empty((n, n), dtype=torch.float32, device=desc.device)
+    if n == 0:
+        return sim
+    native.check(native.lib().gtsfm_retrieval_similarity(_ptr(desc), n, d, int(blocksize), _ptr(sim),
+                                                         native.stream_handle(stream)),
+                 "gtsfm_retrieval_similarity")
+    return sim
+
+
+def retrieval_pairs(scores: torch.Tensor, num_select: int, min_score: Optional[float],
+                    invalid: Optional[torch.Tensor] = None,
+                    stream: Optional[torch.cuda.Stream] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Top-k valid pairs per row of a (K1, K2) f32 device score matrix (gtsfm_retrieval_pairs;
+    netvlad_retriever.py:196-228). invalid: (K1, K2) bool device mask, None = every entry not strictly above the
+    diagonal (:164-167). Returns (pairs (K1, k, 2) int32, row_count (K1,) int32): row i's first row_count[i] entries
+    are its finite top-k pairs in rank order."""
+    if scores.dim() != 2 or scores.dtype != torch.float32 or not scores.is_cuda:
+        raise ValueError("scores must be a (K1, K2) float32 device tensor")
+    if num_select < 0:
+        raise ValueError("num_select must be >= 0")
+    scores = scores.contiguous()
+    n1, n2 = scores.shape
+    k = min(int(num_select), n1)
+    if k > n2:
+        raise RuntimeError(f"selected index k={k} out of range for {n2} columns")  # torch.topk's error
+    inv = None
+    if invalid is not None:
+        if tuple(invalid.shape) != (n1, n2):
+            raise ValueError("invalid must have the shape of scores")
+        inv = invalid.to(device=scores.device, dtype=torch.uint8).contiguous()
+    out = torch.empty((n1, k, 2), dtype=torch.int32, device=scores.device)
+    cnt = torch.zeros((n1,), dtype=torch.int32, device=scores.device)
+    if n1 == 0:
+        return out, cnt
+    use_min = min_score is not None
+    native.check(native.lib().gtsfm_retrieval_pairs(_ptr(scores), n1, n2, _ptr(inv), int(num_select),
+                                                    float(min_score) if use_min else 0.0, int(use_min), _ptr(out),
+                                                    _ptr(cnt), native.stream_handle(stream)),
+                 "gtsfm_retrieval_pairs")
+    return out, cnt

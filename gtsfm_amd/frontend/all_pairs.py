@@ -126,7 +126,10 @@ class AllPairsFrontEnd:
     """One rank's share of the all-pairs front-end (images i with i % world == rank, one contiguous pair block)."""
 
     def __init__(self, host_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, rank: int, world: int,
-                 device: torch.device, cfg: Optional[FrontEndConfig] = None, kernels=None):
+                 device: torch.device, cfg: Optional[FrontEndConfig] = None, kernels=None,
+                 image_pairs: Optional[np.ndarray] = None):
+        """image_pairs: (P, 2) global (i1, i2) pairs to match and verify, e.g. a retriever's output
+        (gtsfm_amd.retriever; image_pairs_generator.py:29-47); None = every pair (ExhaustiveRetriever)."""
         self.cfg = cfg or FrontEndConfig()
         self.kern = kernels if kernels is not None else HipKernels()
         self.dev = torch.device(device)
@@ -163,7 +166,12 @@ class AllPairsFrontEnd:
         self.sift_ws = torch.empty(max(int(ws), 256), dtype=torch.uint8, **z)
 
         slot = sharding.global_slots(n_img, world)
-        pairs = sharding.all_pairs(n_img)
+        if image_pairs is None:
+            pairs = sharding.all_pairs(n_img)
+        else:
+            pairs = np.asarray(image_pairs, dtype=np.int64).reshape(-1, 2)
+            if len(pairs) and (pairs.min() < 0 or pairs.max() >= n_img or np.any(pairs[:, 0] == pairs[:, 1])):
+                raise ValueError("image_pairs must hold distinct image indices in [0, n_img)")
         self.total_pairs = len(pairs)
         block = sharding.rank_pairs(pairs, world, rank)
         self.pair_id_base = int(block[0]) if len(block) else 0  # global pair index keys the RANSAC sampler

@@ -92,6 +92,9 @@ SIGNATURES = {
          c_float, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     "gtsfm_superglue_log_assignment": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "gtsfm_retrieval_similarity": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "gtsfm_retrieval_pairs": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, ctypes.c_float, c_int, c_void_p, c_void_p,
+                                      c_void_p]),
     "gtsfm_compact_verified": (
         c_int,
         [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p,

@@ -17,6 +17,7 @@
  *                              gtsfm/frontend/inlier_support_processor.py:39-95 run_inlier_support
  *   gtsfm_sift_*            <- gtsfm/frontend/detector_descriptor/sift.py:27-56 detect_and_describe
  *                              (cv.cvtColor RGB2GRAY + cv.SIFT_create().detectAndCompute + Keypoints.get_top_k)
+ *   gtsfm_retrieval_*       <- gtsfm/retriever/netvlad_retriever.py:77-228 (similarity blocks + pairs_from_score_matrix)
  */
 #ifndef GTSFM_HIP_H_
 #define GTSFM_HIP_H_
@@ -266,6 +267,26 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
  * columns 0..n (the last of each being the dustbin), NaN elsewhere. Same n_pairs / kmax as the call. */
 int gtsfm_superglue_log_assignment(const void* d_workspace, size_t workspace_bytes, int n_pairs, int kmax, int pair,
                                    float* d_out, void* stream);
+
+/* ---- Retrieval (f3): NetVLAD global-descriptor similarity + top-k image pairs ---------------------------------- */
+
+/* Replaces NetVLADRetriever.compute_similarity_matrix (gtsfm/retriever/netvlad_retriever.py:77-107) together with
+ * _compute_similarity_subblock (:109-134, the einsum "id,jd->ij" per block pair block_j >= block_i) and
+ * _aggregate_subblocks (:136-149). d_desc: [n_img][dim] f32 global descriptors; d_sim: [n_img][n_img] f32, fully
+ * written: the dot product where block(j) >= block(i) (block = index / blocksize), 0 elsewhere, as the reference's
+ * zero-initialised aggregate. fp32 accumulation (summation order differs from torch: parity is a tolerance). */
+int gtsfm_retrieval_similarity(const float* d_desc, int n_img, int dim, int blocksize, float* d_sim, void* stream);
+
+/* Replaces pairs_from_score_matrix (netvlad_retriever.py:196-228). d_scores: [n_rows][n_cols] f32. d_invalid:
+ * [n_rows][n_cols] u8 (nonzero = invalid), or NULL for compute_pairs_from_similarity_matrix's mask (:164-167: every
+ * entry not strictly above the diagonal is invalid). k = min(num_select, n_rows) (:213-215; k > n_cols is
+ * GTSFM_ERR_ARG, as torch.topk raises); scores < min_score are invalid when use_min_score != 0. For row i,
+ * d_out_pairs[(i * k + r) * 2 + {0,1}] = (i, j_r) for r < d_row_count[i]: the finite entries of torch.topk(row, k) in
+ * rank order (NaN ranks first and takes a slot but is not emitted; equal scores by ascending column, an order torch
+ * leaves unspecified). The reference's pair list is the rows concatenated in order. d_scores is read only (the
+ * reference masks its argument in place). */
+int gtsfm_retrieval_pairs(const float* d_scores, int n_rows, int n_cols, const unsigned char* d_invalid, int num_select,
+                          float min_score, int use_min_score, int* d_out_pairs, int* d_row_count, void* stream);
 
 #ifdef __cplusplus
 }

@@ -266,3 +266,44 @@ def sift_level(gray: np.ndarray, o: int, i: int) -> np.ndarray:
     Ho, Wo = ctypes.c_int(0), ctypes.c_int(0)
     lib().oracle_sift_pyramid_level(gray.ravel(), H, W, o, i, out, ctypes.byref(Ho), ctypes.byref(Wo))
     return out[: Ho.value * Wo.value].reshape(Ho.value, Wo.value).copy()
+
+
+# ---- f3 retrieval (numpy; netvlad_retriever.py). Parity unpinned against the reference module itself: importing it
+# needs gtsam (absent here); pinned instead against the reference test's hand-made descriptors and expected pairs.
+def retrieval_similarity(desc: np.ndarray, blocksize: int) -> np.ndarray:
+    """netvlad_retriever.py:77-149: per block pair (bi <= bj) the f32 einsum "id,jd->ij", aggregated into zeros."""
+    desc = np.asarray(desc, np.float32)
+    n = desc.shape[0]
+    sim = np.zeros((n, n), np.float32)
+    nb = -(-n // blocksize)
+    for bi in range(nb):
+        for bj in range(bi, nb):
+            i0, i1 = bi * blocksize, min((bi + 1) * blocksize, n)
+            j0, j1 = bj * blocksize, min((bj + 1) * blocksize, n)
+            sim[i0:i1, j0:j1] = (desc[i0:i1].astype(np.float64) @ desc[j0:j1].astype(np.float64).T).astype(np.float32)
+    return sim
+
+
+def retrieval_select_row(row: np.ndarray, bad: np.ndarray, k: int, min_score: Optional[float]) -> list:
+    """One row of pairs_from_score_matrix (netvlad_retriever.py:218-228): the columns of the finite entries of
+    topk(row masked by `bad` and min_score, k) in rank order -- NaN first, then value descending, equal values by
+    ascending column."""
+    row = np.asarray(row, np.float32).copy()
+    bad = np.asarray(bad, bool).copy()
+    if min_score is not None:
+        bad |= row < min_score
+    row[bad] = -np.inf
+    nan = np.isnan(row)
+    order = np.lexsort((np.arange(row.shape[0]), -np.where(nan, 0, row), ~nan))
+    return [int(j) for j in order[:k] if np.isfinite(row[j])]
+
+
+def retrieval_pairs(scores: np.ndarray, num_select: int, min_score: Optional[float],
+                    invalid: Optional[np.ndarray] = None) -> list:
+    """netvlad_retriever.py:196-228 (+ the strict-upper mask of :164-167 when `invalid` is None): rows concatenated."""
+    scores = np.asarray(scores, np.float32)
+    n1, n2 = scores.shape
+    k = min(num_select, n1)
+    if invalid is None:
+        invalid = ~np.triu(np.ones((n1, n2), bool), 1)
+    return [(i, j) for i in range(n1) for j in retrieval_select_row(scores[i], invalid[i], k, min_score)]
