@@ -597,6 +597,54 @@ __device__ __forceinline__ bool sampson_inlier(const float* E, float4 p, float t
     return __fmul_rn(num, num) <= __fmul_rn(thr2, den);
 }
 
+// MSAC term of one correspondence (oracle/ransac.c msac_cost): the inlier test of sampson_inlier, then the squared
+// Sampson error quantised to floor(e * 2^16 / thr^2) (<= 65535) for an inlier, 65536 for an outlier. Every operation
+// is a single correctly rounded fp32 operation, so the integer matches the oracle's bit for bit.
+__device__ __forceinline__ uint32_t msac_cost(const float* E, float4 p, float thr2, float scale, bool& in) {
+    const float a0 = fmaf(E[1], p.y, fmaf(E[0], p.x, E[2]));
+    const float a1 = fmaf(E[4], p.y, fmaf(E[3], p.x, E[5]));
+    const float a2 = fmaf(E[7], p.y, fmaf(E[6], p.x, E[8]));
+    const float b0 = fmaf(E[3], p.w, fmaf(E[0], p.z, E[6]));
+    const float b1 = fmaf(E[4], p.w, fmaf(E[1], p.z, E[7]));
+    const float num = fmaf(p.w, a1, fmaf(p.z, a0, a2));
+    const float den = fmaf(b1, b1, fmaf(b0, b0, fmaf(a1, a1, __fmul_rn(a0, a0))));
+    const float nn = __fmul_rn(num, num);
+    in = nn <= __fmul_rn(thr2, den);
+    if (!in) return 65536u;
+    const float r = den > 0.0f ? __fdiv_rn(nn, den) : 0.0f;
+    const float q = __fmul_rn(r, scale);
+    return q < 65535.0f ? (uint32_t)q : 65535u;
+}
+
+// Wave-wide sum, uniform result: DPP prefix sum within each row of 16 (row_shr 1, 2, 4, 8), then row_bcast 15 / 31
+// carry the row totals forward; lane 63 holds the total. Six VALU ops, no LDS crossbar traffic.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    int x = (int)v;
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane(x, 63);
+}
+
+// Wave-wide MSAC score of E over M points (its inlier count in `count`).
+__device__ uint32_t wave_msac(const float* E, const float4* pts, int M, float thr2, float scale, int& count,
+                              int lane) {
+    uint32_t sc = 0;
+    int c = 0;
+    for (int base = 0; base < M; base += 64) {
+        const int i = base + lane;
+        bool in = false;
+        const uint32_t q = i < M ? msac_cost(E, pts[i], thr2, scale, in) : 0u;
+        c += __popcll(__ballot(in));
+        sc += wave_sum_u32(q);
+    }
+    count = c;
+    return sc;
+}
+
 // Wave-wide inlier count of E over M points; stops early (exactly) once count + remaining <= floor.
 __device__ int wave_count(const float* E, const float4* pts, int M, float thr2, int floor_count, int lane) {
     int c = 0;
@@ -991,8 +1039,9 @@ struct RansacOutputs {
 };
 
 struct PairState {
-    int best, best_h, best_s, done;
-    int niters, n_models, pad1, pad2;
+    int best, best_h, best_s, done;  // best: inlier count of the selected model
+    int niters, n_models;
+    uint32_t best_score, pad2;       // MSAC score of the selected model (0xFFFFFFFF: none yet)
     double bestE[9];
     double pad3;
 };
@@ -1006,6 +1055,7 @@ __global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int 
     s.best_s = -1;
     s.done = 0;
     s.niters = max_iters;
+    s.best_score = 0xFFFFFFFFu;
     st[p] = s;
 }
 
@@ -1101,9 +1151,12 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
 // sequential scan of oracle/ransac.c: a candidate stops once it can no longer beat the current best count, or only tie
 // it from a later index. The OpenCV iteration bound is applied after every chunk, and the pair stops there once
 // done >= niters, exactly as the oracle's batch loop (oracle/ransac.c:679-706).
+// kMsac: the key is (~score, ~index) with the quantised MSAC score (msac_cost); a candidate stops once its partial
+// score (which only grows) exceeds the best, or equals it from a later index. The winner's inlier count (for the
+// iteration bound and the status) is kept per candidate in LDS.
 constexpr int kScoreWaves = 4;
 
-template <bool kLds>
+template <bool kLds, bool kMsac>
 __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,
                                                                         const double* __restrict__ intr,
                                                                         const int* __restrict__ match_count, int mcap,
@@ -1117,17 +1170,20 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
     __shared__ unsigned long long best_key;
     __shared__ int flat_off[kBatch + 1];  // candidates of hypotheses < h
     __shared__ int sh_bound[2];           // best count, iteration bound after the chunk (from thread 0)
+    __shared__ int cand_cnt[kMsac ? kBatch * kMaxSol : 1];  // kMsac: inlier count of every unbeaten candidate
     const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int M = match_count[p];
     if (M < 6) return;
     // thread 0 updates the pair state after each chunk; the others follow best / niters / done
     int best = st[p].best, best_h = st[p].best_h, best_s = st[p].best_s, done = st[p].done, niters = st[p].niters;
     int n_models = st[p].n_models;
+    uint32_t best_score = st[p].best_score;
     if (done >= niters) return;
     const int i1 = pairs[2 * p], i2 = pairs[2 * p + 1];
     const double fx = fmax(intr[3 * i1], intr[3 * i2]);  // opencv_verifier_base.py:86
     const double thr = thr_px / fx;
     const float thr2 = (float)(thr * thr);
+    const float scale = __fdiv_rn(65536.0f, thr2);
     const float4* pts = pts_all + (size_t)p * mcap;
     // kLds: the putatives are staged in LDS once (M <= 9600); oversize pairs read them from L2/HBM instead
     if (kLds)
@@ -1147,7 +1203,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
             flat_off[lane + 1] = v;
             if (lane == 0) {
                 flat_off[0] = 0;
-                best_key = ((unsigned long long)(uint32_t)(best + 1) << 32) | 0xFFFFFFFFull;  // index -1: before all
+                const uint32_t hi = kMsac ? ~best_score : (uint32_t)(best + 1);
+                best_key = ((unsigned long long)hi << 32) | 0xFFFFFFFFull;  // index -1: before all
             }
         }
         __syncthreads();
@@ -1170,6 +1227,31 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
             const uint32_t my_low = 0xFFFFFFFEu - (uint32_t)ci;
             int c = 0;
             bool alive = true;
+            if constexpr (kMsac) {
+                uint32_t sc = 0;
+#pragma unroll 1
+                for (int base = 0; base < M; base += 128) {  // 128 points per reduction and exit test
+                    const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
+                    const int i = base + lane;
+                    bool in0 = false, in1 = false;
+                    const uint32_t q0 = i < M ? msac_cost(E, sp[i], thr2, scale, in0) : 0u;
+                    const uint32_t q1 = i + 64 < M ? msac_cost(E, sp[i + 64], thr2, scale, in1) : 0u;
+                    c += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
+                    sc += wave_sum_u32(q0 + q1);
+                    if (base + 128 < M) {
+                        const uint32_t bs = ~(uint32_t)(bk >> 32);
+                        if (sc > bs || (sc == bs && my_low < (uint32_t)bk)) {
+                            alive = false;
+                            break;
+                        }
+                    }
+                }
+                if (alive && lane == 0) {
+                    cand_cnt[ci] = c;
+                    atomicMax(&best_key, ((unsigned long long)(~sc) << 32) | my_low);
+                }
+                continue;
+            }
 #pragma unroll 1
             for (int base = 0; base < M; base += 64) {
                 // read before the test so the LDS latency hides under it; a stale best is smaller, so the exit stays
@@ -1198,7 +1280,12 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
                 int hl = 0;
                 while (flat_off[hl + 1] <= ci) ++hl;
                 const int sI = ci - flat_off[hl];
-                best = (int)(bk >> 32) - 1;
+                if (kMsac) {
+                    best = cand_cnt[ci];
+                    best_score = ~(uint32_t)(bk >> 32);
+                } else {
+                    best = (int)(bk >> 32) - 1;
+                }
                 best_h = done + hl;
                 best_s = sI;
                 best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
@@ -1221,6 +1308,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
         o.done = done;
         o.niters = niters;
         o.n_models = n_models;
+        o.best_score = best_score;
         if (best_off >= 0)
             for (int e = 0; e < 9; ++e) o.bestE[e] = cand[best_off + e];
     }
@@ -1233,7 +1321,8 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
                                                            const double2* __restrict__ x1n_all,
                                                            const double2* __restrict__ x2n_all,
                                                            const float4* __restrict__ pts_all, double thr_px,
-                                                           RansacOutputs out, const PairState* __restrict__ st) {
+                                                           int msac, RansacOutputs out,
+                                                           const PairState* __restrict__ st) {
     __shared__ double jac_a[81], jac_v[81];
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1271,12 +1360,24 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
     double bestE[9];
     for (int e = 0; e < 9; ++e) bestE[e] = ps.bestE[e];
     // iterative LO (oracle/ransac.c): thresholds kLoMult*thr -> thr, Sampson-weighted refits
+    const float scale = __fdiv_rn(65536.0f, thr2);
     auto count_d = [&](const double* Ed) {
         float Ef[9];
         for (int e = 0; e < 9; ++e) Ef[e] = (float)Ed[e];
         return wave_count(Ef, pts, M, thr2, -1, lane);
     };
-    int cur = count_d(bestE);
+    auto msac_d = [&](const double* Ed, int& cnt) {
+        float Ef[9];
+        for (int e = 0; e < 9; ++e) Ef[e] = (float)Ed[e];
+        return wave_msac(Ef, pts, M, thr2, scale, cnt, lane);
+    };
+    // a refit replaces the model when it has at least as many inliers (RANSAC) / a score no higher (MSAC)
+    int cur = 0;
+    uint32_t cur_sc = 0;
+    if (msac)
+        cur_sc = msac_d(bestE, cur);
+    else
+        cur = count_d(bestE);
     {
         double E[9];
         for (int e = 0; e < 9; ++e) E[e] = bestE[e];
@@ -1292,9 +1393,18 @@ __global__ __launch_bounds__(64) void ransac_refine_kernel(const int* __restrict
                 if (ok)
                     for (int e = 0; e < 9; ++e) En[e] = Et[e];
             }
-            const int c = count_d(En);
+            int c;
+            bool better;
+            if (msac) {
+                const uint32_t sc = msac_d(En, c);
+                better = sc <= cur_sc;
+                if (better) cur_sc = sc;
+            } else {
+                c = count_d(En);
+                better = c >= cur;
+            }
             for (int e = 0; e < 9; ++e) E[e] = En[e];
-            if (c >= cur) {
+            if (better) {
                 cur = c;
                 for (int e = 0; e < 9; ++e) bestE[e] = En[e];
             }
@@ -1387,7 +1497,7 @@ size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap) {
 
 int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
                            int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
-                           double thr_px, double prob, int max_iters, uint64_t seed, int pair_id_base,
+                           double thr_px, double prob, int max_iters, int scoring, uint64_t seed, int pair_id_base,
                            const int* d_pair_ids, void* d_workspace, size_t workspace_bytes, double* d_E, double* d_R, double* d_t,
                            int* d_n_inliers, int* d_status, int* d_n_hyp, int* d_n_models, uint8_t* d_inlier_mask,
                            void* stream_v) {
@@ -1395,8 +1505,10 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     if (n_pairs == 0) return GTSFM_OK;
     if (!d_kp_xy || !d_intrinsics || !d_pairs || !d_match_idx || !d_match_count || !d_E || !d_R || !d_t ||
         !d_n_inliers || !d_status || !d_inlier_mask || n_img <= 0 || kmax <= 0 || n_pairs < 0 || mcap <= 0 ||
-        max_iters <= 0 || !(thr_px > 0.0))
+        max_iters <= 0 || !(thr_px > 0.0) ||
+        (scoring != GTSFM_RANSAC_SCORING_RANSAC && scoring != GTSFM_RANSAC_SCORING_MSAC))
         return GTSFM_ERR_ARG;
+    const bool msac = scoring == GTSFM_RANSAC_SCORING_MSAC;
     size_t o_x2, o_pts, o_st, o_cand, o_nsol, o_stage;
     const size_t need = ransac_layout(n_pairs, mcap, &o_x2, &o_pts, &o_st, &o_cand, &o_nsol, &o_stage);
     if (workspace_bytes < need) return GTSFM_ERR_CAPACITY;
@@ -1419,8 +1531,12 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     // the score kernel stages a pair's putatives in LDS when they fit (16 B each, up to 150 KiB)
     const bool score_in_lds = (size_t)mcap * sizeof(float4) <= 150 * 1024;
     const size_t score_lds = score_in_lds ? (size_t)mcap * sizeof(float4) : 0;
-    if (score_lds > 65536)
-        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true>, (int)score_lds));
+    if (score_lds > 65536) {
+        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true, false>, (int)score_lds));
+        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true, true>, (int)score_lds));
+    }
+    const auto score_fn = score_in_lds ? (msac ? ransac_score_kernel<true, true> : ransac_score_kernel<true, false>)
+                                       : (msac ? ransac_score_kernel<false, true> : ransac_score_kernel<false, false>);
     // Chunks of 64 hypotheses, as the oracle; launches cover 1, 1, 2, 4, 8, 8, ... chunks. Most pairs stop within the
     // first two chunks; the pairs that run on are few, so their later chunks are solved together (speculatively: a
     // chunk the score kernel does not reach is discarded) to give the solver kernels enough waves.
@@ -1432,18 +1548,13 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            d_match_count, mcap, x1n, x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs, g), dim3(64), kRootLds, stream, d_match_count, st,
                            stage, cand, nsol);
-        if (score_in_lds)
-            hipLaunchKernelGGL(ransac_score_kernel<true>, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream,
-                               d_pairs, d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab,
-                               st);
-        else
-            hipLaunchKernelGGL(ransac_score_kernel<false>, dim3(n_pairs), dim3(64 * kScoreWaves), 0, stream, d_pairs,
-                               d_intrinsics, d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
+        hipLaunchKernelGGL(score_fn, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream, d_pairs, d_intrinsics,
+                           d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask, d_n_models};
     hipLaunchKernelGGL(ransac_refine_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics, d_match_count,
-                       mcap, x1n, x2n, pts, thr_px, o, st);
+                       mcap, x1n, x2n, pts, thr_px, msac ? 1 : 0, o, st);
     GTSFM_CHECK_HIP(hipGetLastError());
     return GTSFM_OK;
 }

@@ -104,8 +104,10 @@ class RansacResult:
 def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
                      match_count: torch.Tensor, thr_px: float, prob: float = 0.999999, max_iters: int = 1000,
                      seed: int = native.RANSAC_DEFAULT_SEED, pair_id_base: int = 0,
-                     pair_ids: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None) -> RansacResult:
+                     pair_ids: Optional[torch.Tensor] = None, stream: Optional[torch.cuda.Stream] = None,
+                     scoring: int = native.GTSFM_RANSAC_SCORING_MSAC) -> RansacResult:
     """Batched 5-point RANSAC + LO + recoverPose for every pair (gtsfm_ransac_E_batched).
+    scoring: GTSFM_RANSAC_SCORING_MSAC (USAC_ACCURATE, the reference's default) or _RANSAC (inlier count).
 
     Args:
         kp_xy: (n_img, kmax, 2) float32 keypoint pixels; intrinsics: (n_img, 3) float64 (f, u0, v0).
@@ -134,7 +136,8 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
         if stream is not None:
             ws.record_stream(stream)
         rc = L.gtsfm_ransac_E_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
-                                      _ptr(match_count), mcap, float(thr_px), float(prob), int(max_iters), int(seed),
+                                      _ptr(match_count), mcap, float(thr_px), float(prob), int(max_iters), int(scoring),
+                                      int(seed),
                                       int(pair_id_base), _ptr(pair_ids), _ptr(ws), ws.numel(), _ptr(E), _ptr(R), _ptr(t),
                                       _ptr(n_inl), _ptr(status), _ptr(n_hyp), _ptr(n_models), _ptr(mask),
                                       native.stream_handle(stream))

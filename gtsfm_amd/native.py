@@ -41,6 +41,8 @@ RANSAC_STATUS_OK = 0
 RANSAC_STATUS_TOO_FEW = 1
 RANSAC_STATUS_NO_MODEL = 2
 RANSAC_DEFAULT_SEED = 0x5EED5EED
+GTSFM_RANSAC_SCORING_RANSAC = 0
+GTSFM_RANSAC_SCORING_MSAC = 1
 BA2_STATUS_OK = 0
 BA2_STATUS_NO_TRACKS = 1
 BA2_STATUS_NONE_VALID = 2
@@ -66,7 +68,7 @@ SIGNATURES = {
     "gtsfm_ransac_workspace_bytes": (c_size_t, [c_int, c_int]),
     "gtsfm_ransac_E_batched": (
         c_int,
-        [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_int,
+        [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_double, c_double, c_int, c_int,
          c_uint64, c_int, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
          c_void_p, c_void_p],
     ),

@@ -105,6 +105,10 @@ int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop);
  * coordinates on the squared Sampson distance, success probability `prob`, at most `max_iters` hypotheses
  * (checked per batch of 64); `seed` and the pair id key the deterministic sampling of pair p: d_pair_ids[p]
  * when d_pair_ids is non-NULL (e.g. all 0 to reproduce one-pair calls), else pair_id_base + p.
+ * Model selection `scoring` (ransac.py:58 robust_estimation_type): GTSFM_RANSAC_SCORING_MSAC for USAC_* (the default
+ * USAC_ACCURATE scores models by MSAC: sum of min(squared Sampson error, thr^2)), each term quantised to
+ * floor(e * 2^16 / thr^2) (65536 for an outlier) so the sum is exact in any order; GTSFM_RANSAC_SCORING_RANSAC for
+ * cv2 RANSAC (inlier count). Local optimisation keeps a refit by the same criterion.
  * Outputs per pair: E, R (i2Ri1) row-major 3x3, unit t (i2ti1), inlier count, status (0 ok, 1 fewer than
  * 6 putatives, 2 no model), number of hypotheses evaluated (d_n_hyp may be NULL), number of candidate models scored
  * (the real 5-point solutions of those hypotheses; d_n_models may be NULL; a measurement output with no reference
@@ -113,10 +117,13 @@ int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop);
  * ---------------------------------------------------------------------------------------------- */
 size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap);
 
+#define GTSFM_RANSAC_SCORING_RANSAC 0 /* most inliers wins (cv2 RANSAC) */
+#define GTSFM_RANSAC_SCORING_MSAC 1   /* lowest truncated-quadratic cost wins (USAC_ACCURATE's MSAC score) */
+
 int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax,
                            const int* d_pairs, int n_pairs, const uint32_t* d_match_idx,
                            const int* d_match_count, int mcap, double thr_px, double prob, int max_iters,
-                           uint64_t seed, int pair_id_base, const int* d_pair_ids, void* d_workspace,
+                           int scoring, uint64_t seed, int pair_id_base, const int* d_pair_ids, void* d_workspace,
                            size_t workspace_bytes, double* d_E, double* d_R, double* d_t, int* d_n_inliers, int* d_status,
                            int* d_n_hyp, int* d_n_models, uint8_t* d_inlier_mask, void* stream);
 

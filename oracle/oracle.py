@@ -52,7 +52,7 @@ def _register_optional(l: ctypes.CDLL) -> None:
     if hasattr(l, "oracle_ransac_E"):
         l.oracle_ransac_E.restype = ctypes.c_int
         l.oracle_ransac_E.argtypes = [_f64p, _f64p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
-                                      ctypes.c_uint64, ctypes.c_int, _f64p, _u8p, _f64p, _f64p,
+                                      ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _f64p, _u8p, _f64p, _f64p,
                                       ctypes.POINTER(ctypes.c_int)]
         l.oracle_five_point.restype = ctypes.c_int
         l.oracle_five_point.argtypes = [_f64p, _f64p, _f64p]
@@ -118,6 +118,8 @@ def oneway_top2(q: np.ndarray, t: np.ndarray):
 
 
 RANSAC_SEED = 0x5EED5EED
+SCORING_RANSAC = 0  # == GTSFM_RANSAC_SCORING_RANSAC
+SCORING_MSAC = 1  # == GTSFM_RANSAC_SCORING_MSAC
 
 
 def five_point(x1: np.ndarray, x2: np.ndarray) -> np.ndarray:
@@ -134,8 +136,9 @@ def sample5(pair: int, h: int, M: int, seed: int = RANSAC_SEED) -> Optional[np.n
 
 
 def ransac_E(x1n: np.ndarray, x2n: np.ndarray, thr: float, prob: float = 0.999999, max_iters: int = 1000,
-             seed: int = RANSAC_SEED, pair_id: int = 0):
-    """Returns (E (3,3), inlier mask (M,) uint8, R (3,3), t (3,), n_inliers, n_hypotheses) or None."""
+             seed: int = RANSAC_SEED, pair_id: int = 0, scoring: int = SCORING_MSAC):
+    """Returns (E (3,3), inlier mask (M,) uint8, R (3,3), t (3,), n_inliers, n_hypotheses) or None.
+    scoring: SCORING_RANSAC (most inliers, cv2 RANSAC) or SCORING_MSAC (truncated quadratic, USAC_ACCURATE)."""
     x1n = np.ascontiguousarray(x1n, np.float64)
     x2n = np.ascontiguousarray(x2n, np.float64)
     M = x1n.shape[0]
@@ -144,8 +147,8 @@ def ransac_E(x1n: np.ndarray, x2n: np.ndarray, thr: float, prob: float = 0.99999
     t = np.zeros(3)
     mask = np.zeros(max(M, 1), np.uint8)
     nh = ctypes.c_int(0)
-    n = lib().oracle_ransac_E(x1n.ravel(), x2n.ravel(), M, thr, prob, max_iters, seed, pair_id, E, mask, R, t,
-                              ctypes.byref(nh))
+    n = lib().oracle_ransac_E(x1n.ravel(), x2n.ravel(), M, thr, prob, max_iters, seed, pair_id, int(scoring), E, mask,
+                              R, t, ctypes.byref(nh))
     if n < 0:
         return None
     return E.reshape(3, 3), mask[:M].copy(), R.reshape(3, 3), t, n, nh.value

@@ -18,7 +18,11 @@
  *   - inlier test: squared Sampson distance <= threshold^2 (OpenCV EMEstimatorCallback::computeError), written
  *     division-free: (x2'Ex1)^2 <= thr^2 * (|Ex1|_xy^2 + |E'x2|_xy^2), float32 with explicit fmaf.
  *   - RANSAC: hypotheses in batches of 64; the OpenCV iteration bound RANSACUpdateNumIters(p, 1-best/M, 5, n)
- *     is re-evaluated after each batch; maxIters 1000; best = most inliers (first one wins ties).
+ *     is re-evaluated after each batch (best = the inlier count of the selected model); maxIters 1000.
+ *     Model selection (`scoring`): 0 = RANSAC, most inliers (cv2 RANSAC); 1 = MSAC, as USAC_ACCURATE scores
+ *     (truncated quadratic sum_i min(e_i, thr^2), lowest wins), with each term quantised to an integer so the
+ *     sum is exact in any order: q_i = floor(e_i * 2^16 / thr^2) clamped to 65535 for an inlier, 65536 for an
+ *     outlier, e_i = num^2 / den in float32. The first candidate wins ties in both modes.
  *   - local optimisation (stand-in for USAC_ACCURATE's LO + final polish; iterative LO in the style of
  *     Lebeda et al. BMVC 2012): 4 steps with the selection threshold shrinking from 6*thr to thr, each 3 rounds
  *     of Sampson-weighted (IRLS) linear 8-point on the selected points, projected onto the essential manifold;
@@ -437,6 +441,40 @@ static int sampson_inlier(const float* E, float x1, float y1, float x2, float y2
     return num * num <= thr2 * den;
 }
 
+/* MSAC term of one correspondence (see the header): the inlier test of sampson_inlier, then the quantised error */
+static uint32_t msac_cost(const float* E, float x1, float y1, float x2, float y2, float thr2, float scale, int* in) {
+    const float a0 = fmaf(E[1], y1, fmaf(E[0], x1, E[2]));
+    const float a1 = fmaf(E[4], y1, fmaf(E[3], x1, E[5]));
+    const float a2 = fmaf(E[7], y1, fmaf(E[6], x1, E[8]));
+    const float b0 = fmaf(E[3], y2, fmaf(E[0], x2, E[6]));
+    const float b1 = fmaf(E[4], y2, fmaf(E[1], x2, E[7]));
+    const float num = fmaf(y2, a1, fmaf(x2, a0, a2));
+    const float den = fmaf(b1, b1, fmaf(b0, b0, fmaf(a1, a1, a0 * a0)));
+    const float nn = num * num;
+    *in = nn <= thr2 * den;
+    if (!*in) return 65536u;
+    const float r = den > 0.0f ? nn / den : 0.0f;
+    const float q = r * scale;
+    return q < 65535.0f ? (uint32_t)q : 65535u;
+}
+
+/* MSAC score of E (and its inlier count in *count, mask when non-NULL) */
+static uint32_t msac_score(const double* Ed, const float* pts, int M, float thr2, int* count, uint8_t* mask) {
+    float E[9];
+    for (int k = 0; k < 9; ++k) E[k] = (float)Ed[k];
+    const float scale = 65536.0f / thr2;
+    uint32_t s = 0;
+    int c = 0;
+    for (int i = 0; i < M; ++i) {
+        int in;
+        s += msac_cost(E, pts[4 * i], pts[4 * i + 1], pts[4 * i + 2], pts[4 * i + 3], thr2, scale, &in);
+        if (mask) mask[i] = (uint8_t)in;
+        c += in;
+    }
+    *count = c;
+    return s;
+}
+
 static int count_inliers(const double* Ed, const float* pts, int M, float thr2, uint8_t* mask) {
     float E[9];
     for (int k = 0; k < 9; ++k) E[k] = (float)Ed[k];
@@ -662,8 +700,8 @@ static int update_num_iters(double p, double ep, int model_points, int max_iters
  * *n_hyp receives the number of hypotheses evaluated.
  */
 int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, double prob, int max_iters,
-                    uint64_t seed, int pair_id, double* E_out, uint8_t* mask_out, double* R_out, double* t_out,
-                    int* n_hyp) {
+                    uint64_t seed, int pair_id, int scoring, double* E_out, uint8_t* mask_out, double* R_out,
+                    double* t_out, int* n_hyp) {
     init_tables();
     if (M < 6) return -1;
     float* pts = (float*)malloc(sizeof(float) * 4 * (size_t)M);
@@ -675,6 +713,7 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
     }
     const float thr2 = (float)(thr * thr);
     int best = -1, best_h = -1, best_s = -1;
+    uint32_t best_score = 0xFFFFFFFFu;
     double bestE[9];
     int niters = max_iters, done = 0;
     while (done < niters) {
@@ -690,13 +729,19 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
             }
             const int ns = oracle_five_point(s1, s2, Es);
             for (int s = 0; s < ns; ++s) {
-                const int c = count_inliers(Es + 9 * s, pts, M, thr2, NULL);
-                if (c > best) {
-                    best = c;
-                    best_h = h;
-                    best_s = s;
-                    memcpy(bestE, Es + 9 * s, sizeof(bestE));
+                int c;
+                if (scoring) {
+                    const uint32_t sc = msac_score(Es + 9 * s, pts, M, thr2, &c, NULL);
+                    if (sc >= best_score) continue;
+                    best_score = sc;
+                } else {
+                    c = count_inliers(Es + 9 * s, pts, M, thr2, NULL);
+                    if (c <= best) continue;
                 }
+                best = c;
+                best_h = h;
+                best_s = s;
+                memcpy(bestE, Es + 9 * s, sizeof(bestE));
             }
         }
         done += RANSAC_BATCH;
@@ -714,8 +759,10 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
     }
     /* local optimisation (iterative LO): 4 steps with the selection threshold shrinking linearly from
      * LO_MULT*thr to thr; each step = 3 rounds of Sampson-weighted 8-point on the selected points; a refined
-     * model replaces the best one when it has at least as many inliers at thr */
+     * model replaces the best one when it has at least as many inliers at thr (RANSAC) / a score no higher (MSAC) */
     int cur = count_inliers(bestE, pts, M, thr2, NULL);
+    uint32_t cur_score = 0;
+    if (scoring) cur_score = msac_score(bestE, pts, M, thr2, &cur, NULL);
     {
         double E[9];
         memcpy(E, bestE, sizeof(E));
@@ -729,9 +776,18 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
                 if (!refit_essential(x1n, x2n, M, Esel, th * th, En, Et)) break;
                 memcpy(En, Et, sizeof(En));
             }
-            const int c = count_inliers(En, pts, M, thr2, NULL);
+            int c;
+            int better;
+            if (scoring) {
+                const uint32_t sc = msac_score(En, pts, M, thr2, &c, NULL);
+                better = sc <= cur_score;
+                if (better) cur_score = sc;
+            } else {
+                c = count_inliers(En, pts, M, thr2, NULL);
+                better = c >= cur;
+            }
             memcpy(E, En, sizeof(E));
-            if (c >= cur) {
+            if (better) {
                 cur = c;
                 memcpy(bestE, En, sizeof(bestE));
             }

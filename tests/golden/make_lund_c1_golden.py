@@ -10,7 +10,8 @@ olsson_loader.py:126-147) into lund_door/gt.json.
 Expected outputs come from the CPU oracle, run with sift_front_end.yaml's parameters at max_resolution 1296 (the
 reference CI benchmark's setting, .github/workflows/benchmark.yml; the 1296 x 1936 images need no resize):
 SIFT max_keypoints 5000 -> TwoWayMatcher ratio 0.8 -> Ransac(use_intrinsics_in_verification=True,
-estimation_threshold_px=4) with the sampler stream of one verify() call per pair (pair id 0).
+estimation_threshold_px=4; MSAC model selection, USAC_ACCURATE's scoring) with the sampler stream of one verify()
+call per pair (pair id 0).
 Stored: keypoint counts and sha256 of each image's (xy, descriptors), every pair's putatives, and the verifier's
 status / inlier count / R / t.
 

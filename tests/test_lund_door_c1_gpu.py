@@ -7,9 +7,10 @@ Checked against the oracle's results (tests/golden/make_lund_c1_golden.py):
 - keypoints and descriptors of every image bit-exact (sha256 of the oracle's arrays);
 - putatives of every pair bit-exact (indices and order);
 - verifier: same status on every pair, inlier counts within 1 %, R / t within 0.05 deg of the oracle;
-and against the ground truth poses of data.mat: rotation error < 2 deg on every pair (the reference verifier tests'
-tolerance, tests/frontend/verifier/test_verifier_base.py:24-25) and median translation-direction error < 2 deg
-(adjacent views have short baselines, so single pairs reach 10 deg in the oracle as well).
+and against the ground truth poses of data.mat: rotation and translation-direction errors < 2 deg on every pair (the
+reference verifier tests' tolerance, tests/frontend/verifier/test_verifier_base.py:24-25). With inlier-count
+scoring single short-baseline pairs reached 10 deg of translation error; MSAC scoring (USAC_ACCURATE's) keeps all 66
+within 1.8 deg.
 The CPU half (test_lund_golden_consistent_with_oracle) re-derives one image's features and one pair's verification
 from the oracle, so the golden file cannot drift from the restatement.
 """
@@ -116,7 +117,7 @@ def test_lund_door_c1_all_pairs_vs_oracle_and_gt():
         Rg, tg = _gt_relative(gt, *key)
         assert np.rad2deg(np.linalg.norm(Rotation.from_matrix(Rm.T @ Rg).as_rotvec())) < 2.0, key
         t_err.append(scenes.direction_angle_deg(tm, tg))
-    assert np.median(t_err) < 2.0, t_err
+    assert np.max(t_err) < 2.0, t_err
 
 
 @pytest.mark.gpu

@@ -10,6 +10,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 from scipy.spatial.transform import Rotation
 
 from tests import scenes
@@ -23,16 +24,18 @@ def _argoverse(golden_dir):
     return a, (kp1 - pp) / a["fx"], (kp2 - pp) / a["fx"]
 
 
-def test_two_plane_scene(oracle_mod):
+@pytest.mark.parametrize("scoring", [0, 1])
+def test_two_plane_scene(oracle_mod, scoring):
     uv1, uv2, R, t = scenes.two_planes_scene(4, 4)
-    E, mask, Re, te, n, _ = oracle_mod.ransac_E(uv1, uv2, 0.5)
+    E, mask, Re, te, n, _ = oracle_mod.ransac_E(uv1, uv2, 0.5, scoring=scoring)
     assert n == 8 and mask.all()
     assert scenes.rotation_angle_deg(R, Re) < 2 and scenes.direction_angle_deg(t, te) < 2
 
 
-def test_argoverse_known_answer(oracle_mod, golden_dir):
+@pytest.mark.parametrize("scoring", [0, 1])
+def test_argoverse_known_answer(oracle_mod, golden_dir, scoring):
     a, x1, x2 = _argoverse(golden_dir)
-    E, mask, R, t, n, _ = oracle_mod.ransac_E(x1, x2, a["estimation_threshold_px"] / a["fx"])
+    E, mask, R, t, n, _ = oracle_mod.ransac_E(x1, x2, a["estimation_threshold_px"] / a["fx"], scoring=scoring)
     euler = Rotation.from_matrix(R.T).as_euler("zyx", degrees=True)
     np.testing.assert_allclose(euler, a["expected_euler_zyx_deg_i1Ri2"], atol=a["euler_tol_deg"])
     np.testing.assert_allclose(-R.T @ t, a["expected_i1ti2"], atol=a["translation_tol"])
@@ -65,13 +68,14 @@ def test_five_point_solutions_satisfy_constraints(oracle_mod):
             assert abs(np.linalg.det(E)) < 1e-6
 
 
-def test_synthetic_scenes_pose_accuracy(oracle_mod):
+@pytest.mark.parametrize("scoring", [0, 1])
+def test_synthetic_scenes_pose_accuracy(oracle_mod, scoring):
     rng = np.random.default_rng(0)
     for _ in range(8):
         kp1, kp2, K, R, t, inl = scenes.random_two_view(rng, 300, 300)
         x1 = (kp1 - K[:2, 2]) / K[0, 0]
         x2 = (kp2 - K[:2, 2]) / K[0, 0]
-        E, mask, Re, te, n, nh = oracle_mod.ransac_E(x1, x2, 4.0 / K[0, 0])
+        E, mask, Re, te, n, nh = oracle_mod.ransac_E(x1, x2, 4.0 / K[0, 0], scoring=scoring)
         assert scenes.rotation_angle_deg(R, Re) < 1.5
         assert scenes.direction_angle_deg(t, te) < 8
         assert (mask.astype(bool) & inl).sum() >= 0.95 * inl.sum()
@@ -127,3 +131,48 @@ def test_F_lmeds_branch_and_guards(oracle_mod):
     F, mask, n, nh = oracle_mod.ransac_F(kp1, kp2, 1.0)
     assert n == 12 and mask.all() and nh >= 64  # M < 15: LMedS with its fixed iteration count
     assert oracle_mod.ransac_F(kp1[:7], kp2[:7], 1.0) is None  # M < 8
+
+
+def _msac_score_np(E, x1, x2, thr):
+    """numpy restatement of the oracle's quantised MSAC score (float32 terms, fma emulated in float64 then rounded)."""
+    f = np.float32
+    Ef = E.astype(f).ravel()
+    p = [x1[:, 0].astype(f), x1[:, 1].astype(f), x2[:, 0].astype(f), x2[:, 1].astype(f)]
+
+    def fma(a, b, c):
+        return (a.astype(np.float64) * b + c).astype(f)
+
+    a0 = fma(Ef[1], p[1], fma(Ef[0], p[0], np.full_like(p[0], Ef[2])))
+    a1 = fma(Ef[4], p[1], fma(Ef[3], p[0], np.full_like(p[0], Ef[5])))
+    a2 = fma(Ef[7], p[1], fma(Ef[6], p[0], np.full_like(p[0], Ef[8])))
+    b0 = fma(Ef[3], p[3], fma(Ef[0], p[2], np.full_like(p[0], Ef[6])))
+    b1 = fma(Ef[4], p[3], fma(Ef[1], p[2], np.full_like(p[0], Ef[7])))
+    num = fma(p[3], a1, fma(p[2], a0, a2))
+    den = fma(b1, b1, fma(b0, b0, fma(a1, a1, a0 * a0)))
+    thr2 = f(thr * thr)
+    nn = num * num
+    inl = nn <= thr2 * den
+    with np.errstate(divide="ignore", invalid="ignore"):
+        r = np.where(den > 0, nn / den, f(0))
+    q = r * (f(65536) / thr2)
+    cost = np.where(inl, np.where(q < 65535, np.floor(q), 65535), 65536).astype(np.int64)
+    return int(cost.sum()), inl
+
+
+def test_msac_selects_lower_truncated_cost(oracle_mod):
+    """MSAC's final model scores no worse than RANSAC's under the MSAC objective, and its mask is that model's inlier
+    set; both modes agree on clean data."""
+    rng = np.random.default_rng(5)
+    wins = 0
+    for _ in range(6):
+        kp1, kp2, K, R, t, inl = scenes.random_two_view(rng, 200, 200, noise_px=1.5)
+        x1 = (kp1 - K[:2, 2]) / K[0, 0]
+        x2 = (kp2 - K[:2, 2]) / K[0, 0]
+        thr = 4.0 / K[0, 0]
+        Em, mm, *_ = oracle_mod.ransac_E(x1, x2, thr, scoring=1)
+        Er, mr, *_ = oracle_mod.ransac_E(x1, x2, thr, scoring=0)
+        sm, im = _msac_score_np(Em, x1, x2, thr)
+        sr, _ = _msac_score_np(Er, x1, x2, thr)
+        assert np.array_equal(im, mm.astype(bool))
+        wins += sm <= sr
+    assert wins >= 5
