@@ -4,7 +4,7 @@
 extern "C" {
 
 // 2.00: gtsfm_ransac_E_batched gained d_n_models; gtsfm_compact_verified added
-int gtsfm_hip_abi_version(void) { return 202; }
+int gtsfm_hip_abi_version(void) { return 300; }
 
 const char* gtsfm_hip_target(void) { return "gfx950"; }
 

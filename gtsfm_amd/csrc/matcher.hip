@@ -123,9 +123,10 @@ __global__ void pack_code_kernel(const float* __restrict__ desc, const int* __re
 // images out of that XCD's L2 while each reads its own A image once.
 // B copies are staged through VGPRs (global_load_dwordx4 at the start of an even phase, ds_write_b128 at its end):
 // no LDS-DMA, whose per-instruction issue cost and LDS-alias waits showed up as whole-phase stalls.
-// Columns: each wave writes its per-(lane-half, column) top-2 keys to an LDS partial buffer with plain stores; one
-// phase later all 8 waves merge the unit's 16 partials per column (a lane per partial pair, three ds_swizzle steps)
-// into the pair's column state, 8 columns per wave.
+// Columns: per (column tile, row tile) a value-only top-2 over the lane's 16 rows becomes a packed key (d2 << ib) |
+// row; the two row tiles merge in registers, a permlane32 swap hands lane L both halves of unit column L, and one
+// returning LDS atomicMin on C1 plus one on C2 (min(max(old, k1), k2): the exact top-2 in any arrival order) fold the
+// wave's 64 rows into the pair's column state. The row inserts run while the first atomic is in flight.
 // Rows: value-only top-2 in registers across a pass; at the pass's last unit one 5-step halving exchange leaves lane
 // l of each half-wave with row l's top-2, stored to rowres.
 // ---------------------------------------------------------------------------------------------
