@@ -20,9 +20,14 @@ Workloads:
   --config c4 (configs[3]): 1000 rendered 1080p images, all 499,500 pairs, split over the N ranks ("strong").
   --config c3-match: configs[2]'s matcher on SURVEY.md §8(d)'s synthetic descriptors -- 200 images x 4096
       SuperPoint-like 256-D unit vectors, all 19900 pairs through the fp16 MFMA shortlist + certified exact re-rank.
+  --config c3: configs[2] end to end -- HIP SuperPoint (4096 kpts, seeded random weights) on 200 rendered 1080p
+      images, then all pairs through the same matcher.
+  --config c5: a per-GPU slice of configs[4] -- SuperPoint (2048 kpts) + SuperGlue + 5-point RANSAC over all pairs
+      of 32 rendered images (configs[4]'s 2000 images x 8 GPUs is ~2M SuperGlue pairs; --images sets the slice).
 Pairs are cut into one contiguous block per rank, images dealt round-robin for extraction.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c3-match] [--images n] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c3-match|c3|c5] [--images n]
+                    [--no-cpu-baseline]
 
 --gpus N > 1 without a launcher starts N fresh rank processes first (gtsfm_amd/launch.py), before anything touches
 a GPU; under `torch.distributed.run` the ranks come from the environment.
@@ -194,7 +199,7 @@ def main_c3(args, world, rank, dev):
         native.check(lib.gtsfm_match_set_kernel_events(None, None), "set_kernel_events")
         kms.append(kev[0].elapsed_time(kev[1]))
     kernel_ms = float(np.median(kms))
-    flops = 2 * 2.0 * k * k * d * len(mine)
+    flops = 2.0 * k * k * d * len(mine)  # the distance matrix counted once per pair
     tf = flops / (kernel_ms * 1e-3) / 1e12
     out = {
         "metric": "matched image-pairs/sec (all-pairs SuperPoint-descriptor matching, configs[2])",
@@ -209,7 +214,7 @@ def main_c3(args, world, rank, dev):
         "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": None,
                      "kernel": "fl_shortlist_kernel<16> (one launch per step)", "kernel_ms": round(kernel_ms, 3),
-                     "work": "2 sides x 2*K1*K2*D flop per pair"},
+                     "work": "2*K1*K2*D flop per pair (the kernel computes the matrix once per side: 2x this)"},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = c3_cpu_baseline(desc)
@@ -217,6 +222,122 @@ def main_c3(args, world, rank, dev):
         print(json.dumps(out), flush=True)
 
 
+
+
+def timed_loop(step, steps: int, world: int, dev) -> float:
+    """Seconds for `steps` calls of step(): barrier + synchronize on both sides, max over ranks."""
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(el, op=torch.distributed.ReduceOp.MAX)
+    return float(el.item())
+
+
+def _random_weight_nets(dev, superglue: bool):
+    """Seeded random SuperPoint (and SuperGlue) weights in the ABI's packed layout: the pretrained .pth files are not
+    available offline (tests/superpoint_weights.py builds state dicts of the reference architectures)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from superpoint_weights import superglue_state_dict, superpoint_state_dict
+
+    from gtsfm_amd.frontend.detector_descriptor.superpoint import pack_superpoint_weights
+
+    sp = torch.from_numpy(pack_superpoint_weights(superpoint_state_dict(0))).to(dev)
+    if not superglue:
+        return sp, None
+    from gtsfm_amd.frontend.matcher.superglue_matcher import pack_superglue_weights
+
+    return sp, torch.from_numpy(pack_superglue_weights(superglue_state_dict(0))).to(dev)
+
+
+def main_dl(args, world, rank, dev, config: str):
+    """configs[2] end to end (c3: SuperPoint 4096 kpts + F16_RERANK mutual NN + ratio 0.8 over all pairs) and a
+    per-GPU slice of configs[4] (c5: SuperPoint 2048 kpts + SuperGlue + 5-point RANSAC (MSAC) over all pairs of a
+    smaller scene). Rendered 1080p images resident in HBM, seeded random network weights."""
+    from gtsfm_amd import device as hip
+    from gtsfm_amd import native, synthetic
+    from gtsfm_amd.frontend import sharding
+
+    c5 = config == "c5"
+    n_img = args.images or (32 if c5 else 200)
+    k = args.kpts if args.kpts != 2048 or c5 else 4096
+    scene = synthetic.render_scene(n_img, args.height, args.width, device=str(dev))
+    mine_img = sharding.local_images(n_img, world, rank)
+    sp_w, sg_w = _random_weight_nets(dev, c5)
+    all_pairs = sharding.all_pairs(n_img)
+    mine = all_pairs[sharding.rank_pairs(all_pairs, world, rank)]
+    pairs = torch.from_numpy(mine.astype(np.int32)).to(dev)
+    imgs = scene.images[torch.from_numpy(np.asarray(mine_img)).to(dev)].contiguous() if world > 1 else scene.images
+    intr = torch.from_numpy(scene.intrinsics).to(dev)
+    hw = torch.tensor([[args.height, args.width]] * n_img, dtype=torch.int32, device=dev)
+    st = {}
+
+    def gather(x):
+        if world == 1:
+            return x
+        return sharding.allgather_features([x], sharding.images_per_rank(n_img, world))[0]
+
+    def step():
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        f = hip.superpoint_extract(imgs, sp_w, k)
+        ev[1].record()
+        xy, sc, de, cn = (gather(t) for t in (f.xy, f.scores, f.desc, f.count))
+        if world > 1:  # rank-major rows -> image order
+            slot = torch.from_numpy(sharding.global_slots(n_img, world)).to(dev)
+            xy, sc, de, cn = xy[slot], sc[slot], de[slot], cn[slot]
+        if c5:
+            idx, cnt, _ = hip.superglue_match(xy.contiguous(), sc.contiguous(), de.contiguous(), cn.contiguous(), hw,
+                                              pairs, sg_w)
+            ev[2].record()
+            res = hip.ransac_essential(xy.contiguous(), intr, pairs, idx.contiguous(), cnt, THRESH_PX)
+            ev[3].record()
+            st["res"] = res
+        else:
+            idx, cnt = hip.match_pairs(de.contiguous(), cn.contiguous(), pairs, RATIO, native.GTSFM_MATCH_F16_RERANK)
+            ev[2].record()
+            ev[3].record()
+        st["ev"], st["cnt"] = ev, cnt
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_loop(step, args.steps, world, dev)
+    ev = st["ev"]
+    torch.cuda.synchronize()
+    stage = {"extract": ev[0].elapsed_time(ev[1]), "match": ev[1].elapsed_time(ev[2]),
+             "verify": ev[2].elapsed_time(ev[3])}
+    total_pairs = len(all_pairs)
+    out = {
+        "metric": ("verified image-pairs/sec (SuperPoint + SuperGlue + RANSAC, configs[4] per-GPU slice)" if c5 else
+                   "matched image-pairs/sec (SuperPoint + fp16 MFMA mutual-NN matcher, configs[2] end to end)"),
+        "value": round(total_pairs / (elapsed / args.steps), 2), "unit": "image-pairs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak" if world > 1 else "strong", "vs_baseline": None,
+        "dtype": ("fp32 MFMA convs / fp32 MFMA attention + Sinkhorn / fp64 RANSAC" if c5 else
+                  "fp32 MFMA convs / fp16 MFMA shortlist + fp32 exact re-rank"),
+        "data": "synthetic (rendered textured room), seeded random network weights",
+        "config": {"workload": (f"C5 slice: {n_img} 1080p images, all {total_pairs} pairs, SuperPoint {k} kpts, "
+                                f"SuperGlue 18 layers / 20 Sinkhorn iterations, 5-pt RANSAC {THRESH_PX}px" if c5 else
+                                f"C3: {n_img} 1080p images, SuperPoint {k} kpts, all {total_pairs} pairs, F16_RERANK "
+                                f"mutual NN + ratio {RATIO}"),
+                   "images": n_img, "pairs": total_pairs, "kpts": k, "parallelism": f"pair blocks x{world}",
+                   "world_size": world},
+        "stage_ms_last_step": {a: round(b, 3) for a, b in stage.items()},
+        "mean_matches": round(float(st["cnt"].float().mean().item()), 1),
+    }
+    if c5:
+        out["pairs_verified"] = int((st["res"].status == 0).sum().item())
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def timed_steps(fe, steps: int, resident: bool, world: int, dev) -> float:
@@ -415,7 +536,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba", action="store_true",
                     help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c3-match"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c3-match", "c3", "c5"])
     ap.add_argument("--launch-probe", action="store_true",
                     help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")
     args = ap.parse_args()
@@ -436,6 +557,8 @@ def main():
     try:
         if args.config == "c3-match":
             main_c3(args, info.world, info.rank, info.device)
+        elif args.config in ("c3", "c5"):
+            main_dl(args, info.world, info.rank, info.device, args.config)
         else:
             main_frontend(args, info, args.config)
     finally:

@@ -1003,7 +1003,8 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
                                                         const unsigned* __restrict__ img_unsafe,
                                                         const int* __restrict__ cand, const float* __restrict__ tkey,
                                                         ExactTop2* __restrict__ rowres, ExactTop2* __restrict__ colres,
-                                                        int* __restrict__ redo_count, int4* __restrict__ redo) {
+                                                        int* __restrict__ redo_count, int4* __restrict__ redo,
+                                                        int* __restrict__ unc) {
 #pragma clang fp contract(off)
     __shared__ float sacc[kFlRerankRows][kFlCand];
     __shared__ int sj[kFlRerankRows][kFlCand];
@@ -1082,16 +1083,124 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
         const float eps = 1.5f * (2.f * e_dot + (D + 4.f) * 2.f / 16777216.f * (na + bn * bn));
         certified = (na + tkey[((size_t)side * n_pairs + p) * kmax + ii]) - eps > a2 * (1.f + 1e-4f) + eps;
     }
-    if (!certified) redo[atomicAdd(redo_count, 1)] = make_int4(side, p, ii, 0);
+    if (!certified) {
+        redo[atomicAdd(redo_count, 1)] = make_int4(side, p, ii, 0);
+        atomicAdd(&unc[side * n_pairs + p], 1);
+    }
     (side ? colres : rowres)[(size_t)p * kmax + ii] = ExactTop2{b1, b2, j1, certified ? 0 : 1};
 }
 
-// Exact rescan of the uncertified keypoints: one 256-thread block per keypoint (block_exact_top2).
+// A (pair, side) whose uncertified share reaches 1/kFlTileFrac of its keypoints is recomputed whole by
+// fl_exact_tile_kernel (clustered descriptors, e.g. random-weight SuperPoint: the shortlist rarely certifies); fewer
+// uncertified keypoints are rescanned one by one.
+constexpr int kFlTileFrac = 32;
+__device__ __forceinline__ bool fl_use_tile(int n_unc, int nq) { return n_unc > 0 && n_unc * kFlTileFrac >= nq; }
+
+// Exact top-2 of every keypoint of a flagged (pair, side), tiled: a block takes 64 query rows against all train rows
+// in 64-row tiles, K in 32-deep LDS chunks; thread (tq, tt) runs the 16 chains of query rows tq + 16 i and train rows
+// tt + 16 j, each the sequential unfused sum over k of exact_top2_kernel (zero padding past dim adds exact zeros), and
+// folds its train rows in increasing order with the strict-'<' update. The 16 partial (b1, j1, b2) of a row merge by
+// (b1, j1) lexicographic minimum with b2 = min(other b1, own b2): the scan's result in any merge order.
+constexpr int kXT = 64, kXK = 32;
+__global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restrict__ desc,
+                                                            const int* __restrict__ counts, int kmax, int dim,
+                                                            const int* __restrict__ pairs, int n_pairs,
+                                                            const int* __restrict__ unc, ExactTop2* __restrict__ rowres,
+                                                            ExactTop2* __restrict__ colres) {
+#pragma clang fp contract(off)
+    __shared__ float Qs[kXT][kXK + 1];
+    __shared__ float Ts[kXT][kXK + 1];
+    __shared__ float mb1[16][kXT], mb2[16][kXT];
+    __shared__ int mj[16][kXT];
+    const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x;
+    const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
+    const int nq = counts[iq], nt = counts[it];
+    const int q0 = blockIdx.x * kXT;
+    if (q0 >= nq || !fl_use_tile(unc[side * n_pairs + p], nq)) return;
+    const int tq = tid & 15, tt = tid >> 4;
+    const float* Q = desc + ((size_t)iq * kmax + q0) * dim;
+    const float* T = desc + (size_t)it * kmax * dim;
+    float b1[4], b2[4];
+    int j1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { b1[i] = b2[i] = __builtin_inff(); j1[i] = -1; }
+    for (int t0 = 0; t0 < nt; t0 += kXT) {
+        float acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+        for (int k0 = 0; k0 < dim; k0 += kXK) {
+            __syncthreads();
+            for (int e = tid; e < kXT * kXK; e += 256) {
+                const int r = e / kXK, k = e % kXK;
+                const bool kin = k0 + k < dim;
+                Qs[r][k] = (kin && q0 + r < nq) ? Q[(size_t)r * dim + k0 + k] : 0.f;
+                Ts[r][k] = (kin && t0 + r < nt) ? T[(size_t)(t0 + r) * dim + k0 + k] : 0.f;
+            }
+            __syncthreads();
+#pragma unroll 4
+            for (int k = 0; k < kXK; ++k) {
+                float qv[4], tv[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) qv[i] = Qs[tq + 16 * i][k];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) tv[j] = Ts[tt + 16 * j][k];
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const float df = qv[i] - tv[j];
+                        acc[i][j] = acc[i][j] + df * df;  // unfused, k ascending: contract(off) above
+                    }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = t0 + tt + 16 * j;
+            if (t >= nt) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float d = sqrt_cr(acc[i][j]);
+                if (d < b2[i]) {
+                    if (d < b1[i]) { b2[i] = b1[i]; b1[i] = d; j1[i] = t; } else { b2[i] = d; }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        mb1[tt][tq + 16 * i] = b1[i];
+        mb2[tt][tq + 16 * i] = b2[i];
+        mj[tt][tq + 16 * i] = j1[i];
+    }
+    __syncthreads();
+    if (tid >= kXT || q0 + tid >= nq) return;
+    float c1 = __builtin_inff(), c2 = __builtin_inff();
+    int cj = -1;
+    for (int u = 0; u < 16; ++u) {
+        const float e1 = mb1[u][tid], e2 = mb2[u][tid];
+        const int ej = mj[u][tid];
+        if (ej < 0) continue;
+        if (cj < 0 || e1 < c1 || (e1 == c1 && ej < cj)) {
+            c2 = fminf(c1, e2);
+            c1 = e1;
+            cj = ej;
+        } else {
+            c2 = fminf(c2, e1);
+        }
+    }
+    (side ? colres : rowres)[(size_t)p * kmax + q0 + tid] = ExactTop2{c1, c2, cj, 1};
+}
+
+// Exact rescan of the uncertified keypoints: one 256-thread block per keypoint (block_exact_top2), except those of
+// (pair, side)s that fl_exact_tile_kernel recomputes whole.
 __global__ __launch_bounds__(kFinThreads) void fl_rescan_kernel(const float* __restrict__ desc,
                                                                 const int* __restrict__ counts, int kmax, int dim,
-                                                                const int* __restrict__ pairs,
+                                                                const int* __restrict__ pairs, int n_pairs,
                                                                 const int* __restrict__ redo_count,
                                                                 const int4* __restrict__ redo,
+                                                                const int* __restrict__ unc,
                                                                 ExactTop2* __restrict__ rowres,
                                                                 ExactTop2* __restrict__ colres) {
     __shared__ float red_d[2 * kFinThreads];
@@ -1101,6 +1210,7 @@ __global__ __launch_bounds__(kFinThreads) void fl_rescan_kernel(const float* __r
         const int4 r = redo[e];
         const int side = r.x, p = r.y, i = r.z;
         const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
+        if (fl_use_tile(unc[side * n_pairs + p], counts[iq])) continue;
         float d1, d2;
         int j1;
         block_exact_top2(desc + ((size_t)iq * kmax + i) * dim, desc + (size_t)it * kmax * dim, counts[it], dim, red_d,
@@ -1121,6 +1231,7 @@ size_t fl_layout(int n_img, int kmax, int dim, int n_pairs, size_t* off) {
     off[6] = o; o += gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);       // colres
     off[7] = o; o += 256;                                                                     // redo count
     off[8] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * sizeof(int4), 256);        // redo list
+    off[9] = o; o += gtsfm_align_up((size_t)2 * n_pairs * sizeof(int), 256);                // uncertified per side
     return o;
 }
 
@@ -1137,7 +1248,7 @@ int launch_fl_shortlist(const _Float16* form, const float* norm2, const int* cou
 int run_fl_match(const float* d_desc, const int* d_counts, int n_img, int kmax, int dim, const int* d_pairs,
                  int n_pairs, double ratio, unsigned char* ws, uint32_t* d_out_idx, int* d_out_count,
                  hipStream_t stream) {
-    size_t off[9];
+    size_t off[10];
     fl_layout(n_img, kmax, dim, n_pairs, off);
     const int kpad = fl_kpad(kmax), dpad = fl_dpad(dim);
     _Float16* form = (_Float16*)(ws + off[0]);
@@ -1150,8 +1261,10 @@ int run_fl_match(const float* d_desc, const int* d_counts, int n_img, int kmax, 
     ExactTop2* colres = (ExactTop2*)(ws + off[6]);
     int* redo_count = (int*)(ws + off[7]);
     int4* redo = (int4*)(ws + off[8]);
+    int* unc = (int*)(ws + off[9]);
     GTSFM_CHECK_HIP(hipMemsetAsync(maxnorm, 0, 2 * (size_t)n_img * sizeof(unsigned), stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(redo_count, 0, sizeof(int), stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(unc, 0, 2 * (size_t)n_pairs * sizeof(int), stream));
     hipLaunchKernelGGL(fl_prep_kernel, dim3(kpad / 4, n_img), dim3(256), 0, stream, d_desc, d_counts, kmax, dim, kpad,
                        dpad, form, norm2, maxnorm, unsafe);
     GTSFM_CHECK_HIP(hipGetLastError());
@@ -1166,10 +1279,12 @@ int run_fl_match(const float* d_desc, const int* d_counts, int n_img, int kmax, 
     if (g_mnn_events[1]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[1], stream));
     hipLaunchKernelGGL(fl_rerank_kernel, dim3((kmax + kFlRerankRows - 1) / kFlRerankRows, n_pairs, 2), dim3(256), 0,
                        stream, d_desc, d_counts, kmax, dim, d_pairs, n_pairs, kpad, norm2, maxnorm, unsafe, cand, tkey,
-                       rowres, colres, redo_count, redo);
+                       rowres, colres, redo_count, redo, unc);
     GTSFM_CHECK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(fl_exact_tile_kernel, dim3((kmax + kXT - 1) / kXT, n_pairs, 2), dim3(256), 0, stream, d_desc,
+                       d_counts, kmax, dim, d_pairs, n_pairs, unc, rowres, colres);
     hipLaunchKernelGGL(fl_rescan_kernel, dim3(2048), dim3(kFinThreads), 0, stream, d_desc, d_counts, kmax, dim,
-                       d_pairs, redo_count, redo, rowres, colres);
+                       d_pairs, n_pairs, redo_count, redo, unc, rowres, colres);
     GTSFM_CHECK_HIP(hipGetLastError());
     return launch_finalize<kResExact>(rowres, colres, d_desc, d_counts, d_pairs, n_pairs, kmax, dim, 0, ratio,
                                       d_out_idx, d_out_count, stream);
@@ -1195,7 +1310,7 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
         return forms + res;
     }
     if (mode == GTSFM_MATCH_F16_RERANK && dim <= kFlMaxDim) {
-        size_t off[9];
+        size_t off[10];
         return fl_layout(n_img, kmax, dim, n_pairs, off);
     }
     return 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);

@@ -151,3 +151,22 @@ def test_c3_size_4096_by_4096_256d(dev, oracle_mod):
     pairs = [(0, 1), (2, 3), (0, 3), (1, 2)]
     fast = _check(dev, oracle_mod, descs, pairs, 0.8, n_oracle=2)
     assert min(len(f) for f in fast) > 200  # ~0.3 x 0.3 x 4096 planted matches per pair
+
+
+@pytest.mark.parametrize("dim", [200, 256])
+def test_clustered_pairs_use_exact_tiles(dev, oracle_mod, dim):
+    """A batch mixing clustered pairs (most shortlists uncertified: the whole (pair, side) goes to the tiled exact
+    kernel, fl_exact_tile_kernel) with planted pairs (few uncertified: per-keypoint rescans), ragged counts and a dim
+    that is not a multiple of the tile's K chunk: identical to EXACT_F32 and to the oracle."""
+    rng = np.random.default_rng(60 + dim)
+    centres = _unit(rng, 4, dim)
+
+    def clustered(n):
+        return (centres[rng.integers(0, 4, n)] + 3e-3 * rng.normal(size=(n, dim)) / np.sqrt(dim)).astype(np.float32)
+
+    a, b = clustered(700), clustered(1000)
+    c, d = _planted(rng, 900, 650, dim)
+    descs = [a, b, c, d, clustered(65)]
+    pairs = [(0, 1), (2, 3), (1, 0), (0, 3), (4, 1), (3, 4)]
+    for ratio in (0.8, None):
+        _check(dev, oracle_mod, descs, pairs, ratio, n_oracle=3)
