@@ -384,16 +384,24 @@ struct GaussSet {
 // DoG levels are never stored: DoG_l = G_{l+1} - G_l is recomputed from the Gaussian levels (the same fp32
 // subtraction cv::subtract performs), which removes 5 level writes per octave.
 // Extrema scan: each wave sweeps a strip of kExStrip rows down 64 consecutive columns (lanes 1..62 produce outputs,
-// lanes 0 and 63 are the left/right halo), one image row per step. Per row a lane loads the 6 Gaussian levels at its
-// pixel (coalesced 256-B rows, saddr + 32-bit offset), forms the 5 DoG values, gets its horizontal neighbours by
-// wave-wide DPP shifts, and keeps per DoG level the 3-wide row max/min of the last three rows in registers (rolling
-// slots, the loop unrolled by three so no register moves). The 27-neighbourhood test "val >= every neighbour" is
-// val == max over the 3x3x3 block (the centre included), from those max3/min3 partials. Each pixel's levels are read
-// once (plus 2 halo rows per strip and 2 halo lanes per wave): the HBM-bound minimum is 24 B per pixel.
+// lanes 0 and 63 are the left/right halo), one image row per step. Per row a lane loads Gaussian levels 1..4 at its
+// pixel (coalesced 256-B rows, saddr + 32-bit offset), forms DoG 1..3, gets its horizontal neighbours by wave-wide DPP
+// shifts, and keeps per DoG level the 3-wide row max/min of the last three rows in registers (rolling slots, the loop
+// unrolled by three so no register moves). The 27-neighbourhood test "val >= every neighbour" is val == max over the
+// 3x3x3 block (the centre included), from those max3/min3 partials. The outer DoG levels 0 and 4 only matter for a
+// layer-1 / layer-3 pixel that already passed the threshold and beats its two in-register levels (a few per
+// thousand): they are queued in LDS and their 3x3 blocks gathered after the sweep, all lanes at once. Each pixel's
+// levels 1..4 are read once (plus 2 halo rows per strip and 2 halo lanes per wave): 16 B per pixel instead of all six
+// levels' 24.
 constexpr int kExWaves = 4, kExOut = 62, kExStrip = 64;
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
+constexpr int kExPend = 512;   // per-block queue of layer-1 / layer-3 pixels awaiting the outer-level test
+struct ExPend {
+    int y, c, layer;
+    float val;
+};
 
 __device__ __forceinline__ float dpp_from_left(float v) {  // lane l gets lane l-1's value (lane 0: its own)
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x138, 0xf, 0xf, false));
@@ -405,13 +413,17 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane l gets lane 
 __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
                                                                 int* __restrict__ n_cand, int cap) {
     __shared__ Cand list[kExList];
-    __shared__ int n_list, gbase;
+    __shared__ ExPend pend[kExPend];
+    __shared__ int n_list, n_pend, gbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, b = blockIdx.z;
     const int c = (blockIdx.x * kExWaves + wave) * kExOut + lane - 1;  // this lane's column
     const int y0 = blockIdx.y * kExStrip;
     const int shard = (int)((blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z)) %
                             kCandShards);  // cap is per shard
-    if (threadIdx.x == 0) n_list = 0;
+    if (threadIdx.x == 0) {
+        n_list = 0;
+        n_pend = 0;
+    }
     __syncthreads();
     const float* gl[kLevels];
 #pragma unroll
@@ -420,32 +432,57 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     const bool col_ok = lane >= 1 && lane <= kExOut && c >= kBorder && c < W - kBorder;
     const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
 
-    float hmax[kDogs][3], hmin[kDogs][3], ctr[kLayers][3];
-    // Row y (clamped) of the 6 levels -> g; then into slot s: DoG values, their 3-wide row extrema, and the centre
-    // values of layers 1..3.
-    auto fetch = [&](int y, float (&g)[kLevels]) {
+    // in registers: DoG levels 1..kLayers (index l - 1), from Gaussian levels 1..kLayers + 1
+    constexpr int kIn = kLayers, kInLv = kLayers + 1;
+    float hmax[kIn][3], hmin[kIn][3], ctr[kLayers][3];
+    // Row y (clamped) of Gaussian levels 1..4 -> g; then into slot s: DoG 1..3, their 3-wide row extrema, and the
+    // centre values of layers 1..3.
+    auto fetch = [&](int y, float (&g)[kInLv]) {
         const uint32_t off = (uint32_t)(min(max(y, 0), H - 1) * W + cx);
 #pragma unroll
-        for (int l = 0; l < kLevels; ++l) g[l] = gl[l][off];
+        for (int l = 0; l < kInLv; ++l) g[l] = gl[l + 1][off];
     };
-    auto finish = [&](const float (&g)[kLevels], auto slot) {
+    auto finish = [&](const float (&g)[kInLv], auto slot) {
         constexpr int s = decltype(slot)::value;
 #pragma unroll
-        for (int l = 0; l < kDogs; ++l) {
+        for (int l = 0; l < kIn; ++l) {
             const float d = g[l + 1] - g[l];
             const float lf = dpp_from_left(d), rt = dpp_from_right(d);
             hmax[l][s] = fmaxf(fmaxf(lf, d), rt);
             hmin[l][s] = fminf(fminf(lf, d), rt);
-            if (l >= 1 && l <= kLayers) ctr[l - 1][s] = d;
+            ctr[l][s] = d;
         }
     };
+    // 3x3 max / min of DoG level lo (= G_{lo+1} - G_lo, the same fp32 subtraction) around (y, c), from HBM/L2
+    auto outer_block = [&](int lo, int y, float& emax, float& emin) {
+        emax = -__builtin_inff();
+        emin = __builtin_inff();
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const uint32_t off = (uint32_t)((y + dy) * W + c + dx);
+                const float d = gl[lo + 1][off] - gl[lo][off];
+                emax = fmaxf(emax, d);
+                emin = fminf(emin, d);
+            }
+    };
     // Test row y: the three slots hold DoG rows y-1, y, y+1, row y in `slot`.
+    auto emit = [&](int layer, int y) {
+        const int slot_i = atomicAdd(&n_list, 1);
+        if (slot_i < kExList) {
+            list[slot_i] = Cand{b, layer, y, c};
+        } else {  // plateau-heavy block: spill straight to the global list
+            const int gi = atomicAdd(&n_cand[shard], 1);
+            if (gi < cap) cands[(size_t)shard * cap + gi] = Cand{b, layer, y, c};
+        }
+    };
     auto test_row = [&](int y, auto slot) {
         constexpr int s = decltype(slot)::value;
         if (!col_ok || y < kBorder || y >= H - kBorder) return;
-        float bmax[kDogs], bmin[kDogs];
+        float bmax[kIn], bmin[kIn];
 #pragma unroll
-        for (int l = 0; l < kDogs; ++l) {
+        for (int l = 0; l < kIn; ++l) {
             bmax[l] = fmaxf(fmaxf(hmax[l][0], hmax[l][1]), hmax[l][2]);
             bmin[l] = fminf(fminf(hmin[l][0], hmin[l][1]), hmin[l][2]);
         }
@@ -453,17 +490,25 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         for (int layer = 1; layer <= kLayers; ++layer) {
             const float val = ctr[layer - 1][s];
             if (!(fabsf(val) > threshold)) continue;
-            const float mx = fmaxf(fmaxf(bmax[layer - 1], bmax[layer]), bmax[layer + 1]);
-            const float mn = fminf(fminf(bmin[layer - 1], bmin[layer]), bmin[layer + 1]);
-            const bool ismax = val > 0 && val >= mx, ismin = val < 0 && val <= mn;
+            // DoG levels layer - 1 .. layer + 1; in registers: indices layer - 2 .. layer within [0, kIn)
+            float mx = bmax[layer - 1], mn = bmin[layer - 1];
+            if (layer >= 2) { mx = fmaxf(mx, bmax[layer - 2]); mn = fminf(mn, bmin[layer - 2]); }
+            if (layer < kIn) { mx = fmaxf(mx, bmax[layer]); mn = fminf(mn, bmin[layer]); }
+            bool ismax = val > 0 && val >= mx, ismin = val < 0 && val <= mn;
             if (!ismax && !ismin) continue;
-            const int slot_i = atomicAdd(&n_list, 1);
-            if (slot_i < kExList) {
-                list[slot_i] = Cand{b, layer, y, c};
-            } else {  // plateau-heavy block: spill straight to the global list
-                const int gi = atomicAdd(&n_cand[shard], 1);
-                if (gi < cap) cands[(size_t)shard * cap + gi] = Cand{b, layer, y, c};
+            if (layer == 1 || layer == kLayers) {  // the outer DoG level (0 or kLayers + 1): queued
+                const int qi = atomicAdd(&n_pend, 1);
+                if (qi < kExPend) {
+                    pend[qi] = ExPend{y, c, layer, val};
+                    continue;
+                }
+                float emax, emin;  // queue full: test in place
+                outer_block(layer == 1 ? 0 : kLayers + 1, y, emax, emin);
+                ismax = ismax && val >= emax;
+                ismin = ismin && val <= emin;
+                if (!ismax && !ismin) continue;
             }
+            emit(layer, y);
         }
     };
     using S0 = std::integral_constant<int, 0>;
@@ -471,20 +516,23 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     using S2 = std::integral_constant<int, 2>;
     // rows y0-1 (slot 0) and y0 (slot 1) first; then row y0+1+3k+j goes to slot (2+j)%3 and completes the window of
     // row y0+3k+j, whose centre sits in slot (1+j)%3.
-    // The three rows of an iteration are fetched up front (18 loads in flight per wave).
+    // The six rows of an iteration are fetched up front.
     {
-        float ga[kLevels], gb[kLevels];
+        float ga[kInLv], gb[kInLv];
         fetch(y0 - 1, ga);
         fetch(y0, gb);
         finish(ga, S0{});
         finish(gb, S1{});
     }
     const int y_end = min(y0 + kExStrip, H);
-    for (int y = y0; y < y_end; y += 3) {
-        float g1[kLevels], g2[kLevels], g3[kLevels];
+    for (int y = y0; y < y_end; y += 6) {  // six rows' loads (24 per lane) in flight before the first is used
+        float g1[kInLv], g2[kInLv], g3[kInLv], g4[kInLv], g5[kInLv], g6[kInLv];
         fetch(y + 1, g1);
         fetch(y + 2, g2);
         fetch(y + 3, g3);
+        fetch(y + 4, g4);
+        fetch(y + 5, g5);
+        fetch(y + 6, g6);
         finish(g1, S2{});
         test_row(y, S1{});
         if (y + 1 >= y_end) break;
@@ -493,6 +541,40 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         if (y + 2 >= y_end) break;
         finish(g3, S1{});
         test_row(y + 2, S0{});
+        if (y + 3 >= y_end) break;
+        finish(g4, S2{});
+        test_row(y + 3, S1{});
+        if (y + 4 >= y_end) break;
+        finish(g5, S0{});
+        test_row(y + 4, S2{});
+        if (y + 5 >= y_end) break;
+        finish(g6, S1{});
+        test_row(y + 5, S0{});
+    }
+    __syncthreads();
+    // the queued layer-1 / layer-3 pixels: outer DoG level's 3x3 block, every lane gathering at once
+    for (int i = threadIdx.x; i < min(n_pend, kExPend); i += 64 * kExWaves) {
+        const ExPend e = pend[i];
+        const int lo = e.layer == 1 ? 0 : kLayers + 1;
+        float emax = -__builtin_inff(), emin = __builtin_inff();
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const uint32_t off = (uint32_t)((e.y + dy) * W + e.c + dx);
+                const float d = gl[lo + 1][off] - gl[lo][off];
+                emax = fmaxf(emax, d);
+                emin = fminf(emin, d);
+            }
+        if ((e.val > 0 && e.val >= emax) || (e.val < 0 && e.val <= emin)) {
+            const int slot_i = atomicAdd(&n_list, 1);
+            if (slot_i < kExList) {
+                list[slot_i] = Cand{b, e.layer, e.y, e.c};
+            } else {
+                const int gi = atomicAdd(&n_cand[shard], 1);
+                if (gi < cap) cands[(size_t)shard * cap + gi] = Cand{b, e.layer, e.y, e.c};
+            }
+        }
     }
     __syncthreads();
     const int n = min(n_list, kExList);
