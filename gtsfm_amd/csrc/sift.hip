@@ -710,8 +710,13 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
         // bins of 64 different neighbourhoods instead of the same few bins (fixed-point sums: order-independent).
         const int total = side * side, chunk = (total + 63) / 64;
         const int kbeg = lane * chunk, kend = min(kbeg + chunk, total);
+        int ci = kbeg / side, cj = kbeg % side;  // (row, column) of sample k, advanced incrementally
         for (int k = kbeg; k < kend; ++k) {
-            const int i = k / side - radius, j = k % side - radius;
+            const int i = ci - radius, j = cj - radius;
+            if (++cj == side) {
+                cj = 0;
+                ++ci;
+            }
             const int y = rf.r + i, x = rf.c + j;
             if (y <= 0 || y >= H - 1 || x <= 0 || x >= W - 1) continue;
             const float dx = img[(size_t)y * W + x + 1] - img[(size_t)y * W + x - 1];
@@ -725,46 +730,45 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
             atomicAdd(&hist[bin], to_fix_nn(w * mag));
         }
         __syncthreads();
-        if (lane == 0) {
-            const int n = kOriBins;
-            float t[kOriBins + 4], h[kOriBins];
-            for (int i = 0; i < n; ++i) t[i + 2] = from_fix(hist[i]);
-            t[1] = t[n + 1];
-            t[0] = t[n];
-            t[n + 2] = t[2];
-            t[n + 3] = t[3];
-            float maxval = 0.f;
-            for (int i = 0; i < n; i++) {
-                h[i] = (t[i] + t[i + 4]) * (1.f / 16.f) + (t[i + 1] + t[i + 3]) * (4.f / 16.f) + t[i + 2] * (6.f / 16.f);
-                maxval = i == 0 ? h[0] : fmaxf(maxval, h[i]);
-            }
+        // smoothing, maximum and peaks one bin per lane (the serial loops' arithmetic per bin; t[q] = hist[(q - 2) mod n]
+        // is the circularly padded histogram)
+        {
+            constexpr int n = kOriBins;
+            auto T = [&](int q) { return from_fix(hist[(q - 2 + n) % n]); };
+            float hj = -__builtin_inff();
+            if (lane < n)
+                hj = (T(lane) + T(lane + 4)) * (1.f / 16.f) + (T(lane + 1) + T(lane + 3)) * (4.f / 16.f) +
+                     T(lane + 2) * (6.f / 16.f);
+            float maxval = hj;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) maxval = fmaxf(maxval, __shfl_xor(maxval, m));
             const float mag_thr = maxval * kOriPeakRatio;
-            for (int j = 0; j < n; j++) {
-                const int l = j > 0 ? j - 1 : n - 1;
-                const int r2 = j < n - 1 ? j + 1 : 0;
-                if (h[j] > h[l] && h[j] > h[r2] && h[j] >= mag_thr) {
-                    float bin = j + 0.5f * (h[l] - h[r2]) / (h[l] - 2 * h[j] + h[r2]);
-                    bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
-                    float angle = 360.f - (360.f / n) * bin;
-                    if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
-                    const int slot = atomicAdd(&kp_counts[rf.img], 1);
-                    if (slot < kp_cap) {
-                        const float sc = (float)(1 << o) * 0.5f;
-                        KeyRec kr;
-                        kr.x = ((float)rf.c + rf.xc) * sc;
-                        kr.y = ((float)rf.r + rf.xr) * sc;
-                        kr.size = size_oct * (float)(1 << o) * 2.f * 0.5f;
-                        kr.angle = angle;
-                        kr.response = fabsf(rf.contr);
-                        kr.xc = rf.xc;
-                        kr.xr = rf.xr;
-                        kr.scl = scl;
-                        kr.o = o;
-                        kr.layer = rf.layer;
-                        kr.r = rf.r;
-                        kr.c = rf.c;
-                        kps[(size_t)rf.img * kp_cap + slot] = kr;
-                    }
+            const int j = lane;
+            const int l = j > 0 ? j - 1 : n - 1;
+            const int r2 = j < n - 1 ? j + 1 : 0;
+            const float hl = __shfl(hj, l), hr = __shfl(hj, r2);
+            if (j < n && hj > hl && hj > hr && hj >= mag_thr) {
+                float bin = j + 0.5f * (hl - hr) / (hl - 2 * hj + hr);
+                bin = bin < 0 ? n + bin : bin >= n ? bin - n : bin;
+                float angle = 360.f - (360.f / n) * bin;
+                if (fabsf(angle - 360.f) < FLT_EPSILON) angle = 0.f;
+                const int slot = atomicAdd(&kp_counts[rf.img], 1);
+                if (slot < kp_cap) {
+                    const float sc = (float)(1 << o) * 0.5f;
+                    KeyRec kr;
+                    kr.x = ((float)rf.c + rf.xc) * sc;
+                    kr.y = ((float)rf.r + rf.xr) * sc;
+                    kr.size = size_oct * (float)(1 << o) * 2.f * 0.5f;
+                    kr.angle = angle;
+                    kr.response = fabsf(rf.contr);
+                    kr.xc = rf.xc;
+                    kr.xr = rf.xr;
+                    kr.scl = scl;
+                    kr.o = o;
+                    kr.layer = rf.layer;
+                    kr.r = rf.r;
+                    kr.c = rf.c;
+                    kps[(size_t)rf.img * kp_cap + slot] = kr;
                 }
             }
         }
