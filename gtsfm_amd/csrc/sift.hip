@@ -317,17 +317,18 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
         }
         asm volatile("" ::: "memory");  // all window reads issue before the in-place writes (neighbour lanes' windows)
         // two outputs per packed-fp32 op (v_pk_add_f32 / v_pk_fma_f32); per-lane rounding unchanged
+        // tap-major over the output pairs (independent neighbours between dependent packed ops: no hazard NOPs)
         pf2 o[kBlurRowOut / 2];
 #pragma unroll
-        for (int h = 0; h < kBlurRowOut / 2; ++h) {
-            const int q = 2 * h;
-            pf2 acc = pf2{k[0], k[0]} * pf2{v[R + q], v[R + q + 1]};
+        for (int h = 0; h < kBlurRowOut / 2; ++h) o[h] = pf2{k[0], k[0]} * pf2{v[R + 2 * h], v[R + 2 * h + 1]};
 #pragma unroll
-            for (int j = 1; j <= R; ++j)
-                acc = __builtin_elementwise_fma(pf2{k[j], k[j]},
-                                                pf2{v[R + q - j], v[R + q + 1 - j]} + pf2{v[R + q + j], v[R + q + 1 + j]},
-                                                acc);
-            o[h] = acc;
+        for (int j = 1; j <= R; ++j) {
+            pf2 sm[kBlurRowOut / 2];
+#pragma unroll
+            for (int h = 0; h < kBlurRowOut / 2; ++h)
+                sm[h] = pf2{v[R + 2 * h - j], v[R + 2 * h + 1 - j]} + pf2{v[R + 2 * h + j], v[R + 2 * h + 1 + j]};
+#pragma unroll
+            for (int h = 0; h < kBlurRowOut / 2; ++h) o[h] = __builtin_elementwise_fma(pf2{k[j], k[j]}, sm[h], o[h]);
         }
 #pragma unroll
         for (int h = 0; h < kBlurRowOut / 2; ++h) *(float2*)(rowp + g8 + 2 * h) = make_float2(o[h].x, o[h].y);
@@ -340,19 +341,48 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
     float c[kBlurColRows + 2 * R];
 #pragma unroll
     for (int i = 0; i < kBlurColRows + 2 * R; ++i) c[i] = in[(ly0 + i) * IWP + tx];
+    // tap-major: the kBlurColRows / 2 output pairs' chains advance together (independent neighbours between dependent
+    // packed ops, so no hazard NOPs); each output's operation order is unchanged
+    constexpr int NP = kBlurColRows / 2;
+    pf2 acc[NP];
 #pragma unroll
-    for (int q = 0; q < kBlurColRows; q += 2) {
-        pf2 acc = pf2{k[0], k[0]} * pf2{c[R + q], c[R + q + 1]};
+    for (int h = 0; h < NP; ++h) acc[h] = pf2{k[0], k[0]} * pf2{c[R + 2 * h], c[R + 2 * h + 1]};
 #pragma unroll
-        for (int j = 1; j <= R; ++j)
-            acc = __builtin_elementwise_fma(pf2{k[j], k[j]},
-                                            pf2{c[R + q - j], c[R + q + 1 - j]} + pf2{c[R + q + j], c[R + q + 1 + j]}, acc);
-        const int y = y0 + ly0 + q;  // even: tiles, ly0 and q are
-        if (y < H) dst[base + (size_t)y * W + x] = acc.x;
-        if (y + 1 < H) dst[base + (size_t)(y + 1) * W + x] = acc.y;
-        // the next octave's base, cv::resize INTER_NEAREST to (H/2, W/2) of this level: pixel (2y', 2x')
-        if (dec != nullptr && (x & 1) == 0 && (x >> 1) < (W >> 1) && y < H && (y >> 1) < (H >> 1))
-            dec[(size_t)b * (H >> 1) * (W >> 1) + (size_t)(y >> 1) * (W >> 1) + (x >> 1)] = acc.x;
+    for (int j = 1; j <= R; ++j) {
+        pf2 sm[NP];
+#pragma unroll
+        for (int h = 0; h < NP; ++h)
+            sm[h] = pf2{c[R + 2 * h - j], c[R + 2 * h + 1 - j]} + pf2{c[R + 2 * h + j], c[R + 2 * h + 1 + j]};
+#pragma unroll
+        for (int h = 0; h < NP; ++h) acc[h] = __builtin_elementwise_fma(pf2{k[j], k[j]}, sm[h], acc[h]);
+    }
+    // output rows y0 + ly0 + 2h (even: tiles and ly0 are) and the next; running store pointers
+    float* dp = dst + base + (size_t)(y0 + ly0) * W + x;
+    const int rows_left = H - (y0 + ly0);  // rows of this thread's outputs inside the image
+    if (rows_left >= kBlurColRows && dec == nullptr) {
+#pragma unroll
+        for (int h = 0; h < NP; ++h) {
+            dp[0] = acc[h].x;
+            dp[W] = acc[h].y;
+            dp += 2 * (size_t)W;
+        }
+        return;
+    }
+    // the image's last tile row, or the one level per octave that also writes the next octave's base (dec:
+    // cv::resize INTER_NEAREST to (H/2, W/2) of this level, pixel (2y', 2x'))
+    const bool dec_lane = dec != nullptr && (x & 1) == 0 && (x >> 1) < (W >> 1);
+    float* decp = dec_lane ? dec + (size_t)b * (H >> 1) * (W >> 1) + (size_t)((y0 + ly0) >> 1) * (W >> 1) + (x >> 1)
+                           : nullptr;
+#pragma unroll
+    for (int h = 0; h < NP; ++h) {
+        if (2 * h < rows_left) dp[0] = acc[h].x;
+        if (2 * h + 1 < rows_left) dp[W] = acc[h].y;
+        dp += 2 * (size_t)W;
+        if (decp != nullptr) {
+            const int y = y0 + ly0 + 2 * h;
+            if (y < H && (y >> 1) < (H >> 1)) *decp = acc[h].x;
+            decp += W >> 1;
+        }
     }
 }
 
