@@ -123,10 +123,12 @@ __global__ void pack_code_kernel(const float* __restrict__ desc, const int* __re
 // images out of that XCD's L2 while each reads its own A image once.
 // B copies are staged through VGPRs (global_load_dwordx4 at the start of an even phase, ds_write_b128 at its end):
 // no LDS-DMA, whose per-instruction issue cost and LDS-alias waits showed up as whole-phase stalls.
-// Columns: per (column tile, row tile) a value-only top-2 over the lane's 16 rows becomes a packed key (d2 << ib) |
-// row; the two row tiles merge in registers, a permlane32 swap hands lane L both halves of unit column L, and one
+// Columns: per (column tile, row tile) a value-only top-2 over the lane's 16 rows (the four chains advance together,
+// four inserts per asm statement); the two row tiles merge on the raw values (ties to the first tile) and become one
+// packed key (d2 << ib) | row per column tile; a permlane32 swap hands lane L both halves of unit column L, and one
 // returning LDS atomicMin on C1 plus one on C2 (min(max(old, k1), k2): the exact top-2 in any arrival order) fold the
-// wave's 64 rows into the pair's column state. The row inserts run while the first atomic is in flight.
+// wave's 64 rows into the pair's column state. The C2 atomic is issued in the NEXT unit's epilogue (C2 is a plain
+// min, so its timing does not matter), by when the C1 return has long arrived.
 // Rows: value-only top-2 in registers across a pass; at the pass's last unit one 5-step halving exchange leaves lane
 // l of each half-wave with row l's top-2, stored to rowres.
 // ---------------------------------------------------------------------------------------------
@@ -176,12 +178,57 @@ __device__ __forceinline__ uint32_t min3u(uint32_t a, uint32_t b, uint32_t c) {
 }
 // running top-2 insert of two values, updated IN PLACE (tied asm operands): the loop-carried row state keeps its
 // registers instead of rotating through copies
+#ifdef GTSFM_PP_C_INS2  // plain C: the compiler forms v_med3_u32 / v_min3_u32 and schedules freely
+__device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
+    const uint32_t m = umin(umax(b1, a), umax(umin(b1, a), b));
+    b1 = umin(umin(b1, a), b);
+    b2 = umin(b2, m);
+}
+#elif defined(GTSFM_PP_ONE_ASM)  // one asm statement per insert
+__device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
+    uint32_t m;
+    asm("v_med3_u32 %2, %0, %3, %4\n\tv_min3_u32 %0, %0, %3, %4\n\tv_min_u32 %1, %1, %2"
+        : "+v"(b1), "+v"(b2), "=&v"(m) : "v"(a), "v"(b));
+}
+#else
 __device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
     uint32_t m;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(b1), "v"(a), "v"(b));
     asm("v_min3_u32 %0, %0, %1, %2" : "+v"(b1) : "v"(a), "v"(b));
     asm("v_min_u32 %0, %0, %1" : "+v"(b2) : "v"(m));
 }
+#endif
+// four independent inserts in ONE asm statement, interleaved (each dependent pair three instructions apart). The
+// compiler puts an s_nop after every inline-asm statement that is followed by another, so fewer, larger statements
+// issue fewer of them.
+__device__ __forceinline__ void ins2x4(uint32_t& b10, uint32_t& b20, uint32_t a0, uint32_t c0,
+                                       uint32_t& b11, uint32_t& b21, uint32_t a1, uint32_t c1,
+                                       uint32_t& b12, uint32_t& b22, uint32_t a2, uint32_t c2,
+                                       uint32_t& b13, uint32_t& b23, uint32_t a3, uint32_t c3) {
+    uint32_t m0, m1, m2, m3;
+    asm("v_med3_u32 %8, %0, %12, %13\n\t"
+        "v_med3_u32 %9, %2, %14, %15\n\t"
+        "v_med3_u32 %10, %4, %16, %17\n\t"
+        "v_med3_u32 %11, %6, %18, %19\n\t"
+        "v_min3_u32 %0, %0, %12, %13\n\t"
+        "v_min3_u32 %2, %2, %14, %15\n\t"
+        "v_min3_u32 %4, %4, %16, %17\n\t"
+        "v_min3_u32 %6, %6, %18, %19\n\t"
+        "v_min_u32 %1, %1, %8\n\t"
+        "v_min_u32 %3, %3, %9\n\t"
+        "v_min_u32 %5, %5, %10\n\t"
+        "v_min_u32 %7, %7, %11"
+        : "+v"(b10), "+v"(b20), "+v"(b11), "+v"(b21), "+v"(b12), "+v"(b22), "+v"(b13), "+v"(b23),
+          "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3)
+        : "v"(a0), "v"(c0), "v"(a1), "v"(c1), "v"(a2), "v"(c2), "v"(a3), "v"(c3));
+}
+
+#ifndef GTSFM_PP_LEGACY  // default epilogue: 4-way asm inserts, t-merged column keys, deferred C2 atomic, pinned B reads
+#define GTSFM_PP_X4 1
+#define GTSFM_PP_DEFER 1
+#define GTSFM_PP_TMERGE 1
+#define GTSFM_PP_SGB 1
+#endif
 
 // Per-slot (pair) description, wave-uniform.
 struct PpSlot {
@@ -319,6 +366,11 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 #pragma unroll
         for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
     f32x16 acc[2][2];  // [sub (32-column tile)][t (32-row tile)]
+#ifdef GTSFM_PP_DEFER
+    uint32_t dold = 0, dm1 = 0, dm2 = 0;  // the pending C2 update of the previous unit
+    uint32_t* dptr = colstate;
+    bool dpend = false;
+#endif
 
     PpIter work = first, cpy = first;
     if (first.valid) {  // unit 0 -> ring[0]
@@ -345,6 +397,9 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         if (pending) stage_store(cpy_pending);
         pending = false;
     };
+#ifdef GTSFM_PP_STATIC_PRIO
+    if (grp == 1) __builtin_amdgcn_s_setprio(1);  // the younger half wins arbitration, no per-segment flips
+#endif
     if (grp == 1 && n_units > 0) copy_begin();  // group 1's leading phase 0: the load of unit 1
     if (grp == 1 && n_units > 0) __syncthreads();
 #ifdef GTSFM_PP_STAMPS
@@ -361,20 +416,34 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         // a short stall the partner wave's E covers).
         load_a(si.img_a, work.pass);
         if (grp == 0) copy_begin();  // after the A loads, so the MFMAs never wait for the staged copy
+#ifndef GTSFM_PP_ABL_NOM
+#define GTSFM_PP_ABL_NOM 0
+#endif
+#ifndef GTSFM_PP_ABL_NOE
+#define GTSFM_PP_ABL_NOE 0
+#endif
 #ifndef GTSFM_PP_PRIO_M
 #define GTSFM_PP_PRIO_M 2
 #endif
 #ifndef GTSFM_PP_PRIO_E
 #define GTSFM_PP_PRIO_E 0
 #endif
+#ifndef GTSFM_PP_STATIC_PRIO
         __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_M);  // the MFMA stream outranks the partner wave's VALU epilogue
-        if (rows_here) {
+#endif
+        if (GTSFM_PP_ABL_NOM)
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
+        if (rows_here && !GTSFM_PP_ABL_NOM) {  // ABL: timing ablations only
             const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
             half8 bf[2][2];  // [k-step parity][sub]: the next k-step's B fragments are read ahead
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) bf[0][sub] = *(const half8*)(bb + sub * Cfg::kChunkBytes);
+#ifdef GTSFM_PP_SGB
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#endif
 #pragma unroll
             for (int s = 0; s < NK; ++s) {
                 if (s + 1 < NK) {
@@ -387,6 +456,10 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                     acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf[s & 1][sub], acc[sub][0], 0, 0, 0);
                     acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf[s & 1][sub], acc[sub][1], 0, 0, 0);
                 }
+#ifdef GTSFM_PP_SGB  // pin the schedule: the next k-step's two B reads ahead of this k-step's four MFMAs
+                if (s + 1 < NK) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#endif
             }
         }
         if (grp == 1) copy_end();  // loaded at the start of phase 2k
@@ -394,12 +467,14 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         __syncthreads();
         PP_STAMP(t2);
         // ---- phase B: group 0 -> phase 2k+1, group 1 -> phase 2k+2 (load of unit k+2)
+#ifndef GTSFM_PP_STATIC_PRIO
         __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_E);
+#endif
         if (grp == 1) copy_begin();
 #ifdef GTSFM_PP_STAMPS
         te0 = te1 = te2 = te3 = __builtin_amdgcn_s_memtime();
 #endif
-        if (rows_here) {
+        if (rows_here && !GTSFM_PP_ABL_NOE) {
 #ifdef GTSFM_PP_STAMPS
             te1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -408,16 +483,53 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
             // both halves' top-2 of column tile L >> 5, column L & 31, so lane L owns unit column L: one returning
             // atomic min on C1 and one on C2 per lane (min(max(old, k1), k2) keeps the exact top-2 in any order)
             uint32_t s1[2], s2[2];
+#ifdef GTSFM_PP_X4
+            uint32_t cv1[2][2], cv2[2][2];  // the four (sub, t) column chains, advanced together
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    cv1[sub][t] = umin(__float_as_uint(acc[sub][t][0]), __float_as_uint(acc[sub][t][1]));
+                    cv2[sub][t] = umax(__float_as_uint(acc[sub][t][0]), __float_as_uint(acc[sub][t][1]));
+                }
+#define PPU(sub, t, g) __float_as_uint(acc[sub][t][g])
+#pragma unroll
+            for (int g = 2; g < 16; g += 2)
+                ins2x4(cv1[0][0], cv2[0][0], PPU(0, 0, g), PPU(0, 0, g + 1), cv1[0][1], cv2[0][1], PPU(0, 1, g),
+                       PPU(0, 1, g + 1), cv1[1][0], cv2[1][0], PPU(1, 0, g), PPU(1, 0, g + 1), cv1[1][1], cv2[1][1],
+                       PPU(1, 1, g), PPU(1, 1, g + 1));
+#endif
+#ifdef GTSFM_PP_TMERGE
+            // the two row tiles of a column merge on the raw values (ties to t = 0: its rows come first), so one key
+            // is built per column tile instead of two
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
+                const uint32_t a0 = cv1[sub][0], a1 = cv1[sub][1];
+                const bool take1 = a1 < a0;
+                const uint32_t v1 = take1 ? a1 : a0;
+                const uint32_t v2 = med3u(a0, a1, umin(cv2[sub][0], cv2[sub][1]));
+                const uint32_t u = (uint32_t)(__uint_as_float(v1) * 16.f);
+                uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
+                if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
+                const uint32_t rowbase = (uint32_t)(r0w + 16 * half) + (take1 ? 32u : 0u);
+                s1[sub] = (d1 << ib) | rowbase | (u & 15u);
+                s2[sub] = d2 << ib;
+            }
+#else
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) {
                 uint32_t k1[2], k2[2];
 #pragma unroll
                 for (int t = 0; t < 2; ++t) {
+#ifdef GTSFM_PP_X4
+                    const uint32_t v1 = cv1[sub][t], v2 = cv2[sub][t];
+#else
                     const f32x16& a = acc[sub][t];
                     uint32_t v1 = umin(__float_as_uint(a[0]), __float_as_uint(a[1]));
                     uint32_t v2 = umax(__float_as_uint(a[0]), __float_as_uint(a[1]));
 #pragma unroll
                     for (int g = 2; g < 16; g += 2) ins2(v1, v2, __float_as_uint(a[g]), __float_as_uint(a[g + 1]));
+#endif
                     const uint32_t u = (uint32_t)(__uint_as_float(v1) * 16.f);
                     uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
                     if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
@@ -428,6 +540,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                 s1[sub] = umin(k1[0], k1[1]);
                 s2[sub] = med3u(k1[0], k1[1], umin(k2[0], k2[1]));
             }
+#endif
             const auto x1 = __builtin_amdgcn_permlane32_swap(s1[0], s1[1], false, false);
             const auto x2 = __builtin_amdgcn_permlane32_swap(s2[0], s2[1], false, false);
             const uint32_t m1 = umin(x1[0], x1[1]), m2 = med3u(x1[0], x1[1], umin(x2[0], x2[1]));
@@ -435,17 +548,40 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
             te2 = __builtin_amdgcn_s_memtime();
 #endif
             uint32_t* c1s = colstate + work.slot * 2 * kmax64 + work.sc * kUnitCols + lane;
+#ifdef GTSFM_PP_DEFER
+            if (dpend) __hip_atomic_fetch_min(dptr + kmax64, umin(umax(dold, dm1), dm2), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+            dold = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            dm1 = m1; dm2 = m2; dptr = c1s; dpend = true;
+#elif defined(GTSFM_PP_NRT)  // timing bound only (wrong second-best): both atomics without return
+            __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            const uint32_t old = 0;
+#else
             const uint32_t old = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
             // the row inserts run while the returning atomic is in flight
             __builtin_amdgcn_sched_barrier(0);
             // rows: both column tiles' values of row (t, g) in one paired insert
+#ifdef GTSFM_PP_X4
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int g = 0; g < 16; g += 4)
+                    ins2x4(rb1[t][g], rb2[t][g], PPU(0, t, g), PPU(1, t, g), rb1[t][g + 1], rb2[t][g + 1],
+                           PPU(0, t, g + 1), PPU(1, t, g + 1), rb1[t][g + 2], rb2[t][g + 2], PPU(0, t, g + 2),
+                           PPU(1, t, g + 2), rb1[t][g + 3], rb2[t][g + 3], PPU(0, t, g + 3), PPU(1, t, g + 3));
+#undef PPU
+#else
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int g = 0; g < 16; ++g)
                     ins2(rb1[t][g], rb2[t][g], __float_as_uint(acc[0][t][g]), __float_as_uint(acc[1][t][g]));
+#endif
             __builtin_amdgcn_sched_barrier(0);
+#ifndef GTSFM_PP_DEFER
             __hip_atomic_fetch_min(c1s + kmax64, umin(umax(old, m1), m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
 #ifdef GTSFM_PP_STAMPS
             te3 = __builtin_amdgcn_s_memtime();
 #endif
@@ -486,6 +622,10 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 #ifdef GTSFM_PP_STAMPS
     if (lane == 0)
         for (int i = 0; i < 8; ++i) atomicAdd(&g_pp_stamps[wave * 8 + i], st[i]);
+#endif
+#ifdef GTSFM_PP_DEFER
+    if (dpend) __hip_atomic_fetch_min(dptr + kmax64, umin(umax(dold, dm1), dm2), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
     if (grp == 0 && n_units > 0) __syncthreads();  // group 0's trailing phase 2U (group 1's E of the last unit)
     __syncthreads();

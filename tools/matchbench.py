@@ -1,6 +1,7 @@
 """Distance-GEMM microbench: all pairs of N synthetic SIFT-like images at 2048 keypoints, whole match_pairs call and the
 mnn kernel alone (HIP events through gtsfm_match_set_kernel_events), without and with block-tiled pair groups.
 Usage: python tools/matchbench.py [N]"""
+import hashlib
 import json
 import os
 import sys
@@ -17,6 +18,8 @@ K = 2048
 rng = np.random.default_rng(3)
 x = rng.gamma(0.6, 1.0, size=(n_img, K, 128)).astype(np.float32)
 x = np.clip(np.round(x / np.linalg.norm(x, axis=2, keepdims=True) * 512), 0, 255).astype(np.float32)
+n_pl = int(0.3 * K)  # planted: 30% of the keypoints share a latent descriptor (+ integer noise) across images
+x[:, :n_pl] = np.clip(x[0, :n_pl][None] + rng.integers(-8, 9, size=(n_img, n_pl, 128)), 0, 255)
 dev = torch.device("cuda")
 desc = torch.from_numpy(x).to(dev)
 counts = torch.full((n_img,), K, dtype=torch.int32, device=dev)
@@ -51,7 +54,8 @@ for name, groups in (("ungrouped", None), ("grouped", torch.from_numpy(device.pa
     out[name] = {"call_ms": round(dt * 1e3, 3), "kernel_ms": round(km, 3),
                  "kernel_TFLOPs": round(flops / (km * 1e-3) / 1e12, 1),
                  "kernel_frac_f16_peak": round(flops / (km * 1e-3) / 2.5e15, 4),
-                 "mean_matches": float(cnt.float().mean())}
+                 "mean_matches": float(cnt.float().mean()),
+                 "checksum": hashlib.sha1(cnt.cpu().numpy().tobytes() + idx.cpu().numpy().tobytes()).hexdigest()[:16]}
 print(json.dumps(out))
 if hasattr(L, "gtsfm_pp_stamps"):  # diagnostic build: per-wave cycles of one grouped launch
     import ctypes
