@@ -268,8 +268,9 @@ class AllPairsFrontEnd:
         self._mark("start")
         self._extract(resident)
         self._mark("extract")
+        # SIFT descriptors are integer-valued in [0, 255]: they travel as u8 (lossless, a quarter of the f32 bytes)
         xy_all, desc_all, cnt_all = sharding.allgather_features((self.feats.xy, self.feats.desc, self.feats.count),
-                                                                self.n_per)
+                                                                self.n_per, wire=(None, torch.uint8, None))
         self._mark("allgather")
         n_hyp, n_models, n_match = [], [], []
         for c, (a, b) in enumerate(self.pchunks):

@@ -52,17 +52,22 @@ def rank_pairs(pairs: np.ndarray, world: int, rank: int) -> np.ndarray:
 
 
 def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
-                       group: Optional[torch.distributed.ProcessGroup] = None) -> Tuple[torch.Tensor, ...]:
+                       group: Optional[torch.distributed.ProcessGroup] = None,
+                       wire: Optional[Sequence[Optional[torch.dtype]]] = None) -> Tuple[torch.Tensor, ...]:
     """Pads each rank's (n_local, ...) feature tensors to n_per rows and all-gathers them rank-major.
 
-    One collective per tensor (descriptors dominate: 2048 x 128 x 4 B per image). With world == 1 the inputs are
-    returned unchanged.
+    One collective per tensor. wire[i] (optional) is the dtype tensor i travels in; it is cast back afterwards, so
+    the caller must only name a lossless one: SIFT descriptors are integers in [0, 255], so u8 carries them exactly
+    (2048 x 128 B per image instead of 4x that in f32). With world == 1 the inputs are returned unchanged.
     """
     world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
     if world == 1:
         return tuple(tensors)
     out = []
-    for t in tensors:
+    for i, t in enumerate(tensors):
+        dtype = t.dtype
+        if wire is not None and wire[i] is not None:
+            t = t.to(wire[i])
         pad = n_per - t.shape[0]
         if pad < 0:
             raise ValueError(f"rank holds {t.shape[0]} images, more than n_per={n_per}")
@@ -71,7 +76,7 @@ def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
         t = t.contiguous()
         g = torch.empty((world * n_per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         torch.distributed.all_gather_into_tensor(g, t, group=group)
-        out.append(g)
+        out.append(g if g.dtype == dtype else g.to(dtype))
     return tuple(out)
 
 

@@ -44,7 +44,7 @@ def _worker(rank: int, world: int, port: int, n_img: int, out_dir: str):
         desc = torch.from_numpy(np.stack([f[1] for f in feats]))
         cnt = torch.tensor([f[2] for f in feats], dtype=torch.int32)
         n_per = sharding.images_per_rank(n_img, world)
-        xy_all, desc_all, cnt_all = sharding.allgather_features((xy, desc, cnt), n_per)
+        xy_all, desc_all, cnt_all = sharding.allgather_features((xy, desc, cnt), n_per, wire=(None, torch.uint8, None))
         slot = sharding.global_slots(n_img, world)
         for i in range(n_img):
             exy, edesc, en = _features(i)
