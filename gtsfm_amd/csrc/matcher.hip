@@ -178,26 +178,12 @@ __device__ __forceinline__ uint32_t min3u(uint32_t a, uint32_t b, uint32_t c) {
 }
 // running top-2 insert of two values, updated IN PLACE (tied asm operands): the loop-carried row state keeps its
 // registers instead of rotating through copies
-#ifdef GTSFM_PP_C_INS2  // plain C: the compiler forms v_med3_u32 / v_min3_u32 and schedules freely
-__device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
-    const uint32_t m = umin(umax(b1, a), umax(umin(b1, a), b));
-    b1 = umin(umin(b1, a), b);
-    b2 = umin(b2, m);
-}
-#elif defined(GTSFM_PP_ONE_ASM)  // one asm statement per insert
-__device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
-    uint32_t m;
-    asm("v_med3_u32 %2, %0, %3, %4\n\tv_min3_u32 %0, %0, %3, %4\n\tv_min_u32 %1, %1, %2"
-        : "+v"(b1), "+v"(b2), "=&v"(m) : "v"(a), "v"(b));
-}
-#else
 __device__ __forceinline__ void ins2(uint32_t& b1, uint32_t& b2, uint32_t a, uint32_t b) {
     uint32_t m;
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m) : "v"(b1), "v"(a), "v"(b));
     asm("v_min3_u32 %0, %0, %1, %2" : "+v"(b1) : "v"(a), "v"(b));
     asm("v_min_u32 %0, %0, %1" : "+v"(b2) : "v"(m));
 }
-#endif
 // four independent inserts in ONE asm statement, interleaved (each dependent pair three instructions apart). The
 // compiler puts an s_nop after every inline-asm statement that is followed by another, so fewer, larger statements
 // issue fewer of them.
@@ -416,12 +402,6 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         // a short stall the partner wave's E covers).
         load_a(si.img_a, work.pass);
         if (grp == 0) copy_begin();  // after the A loads, so the MFMAs never wait for the staged copy
-#ifndef GTSFM_PP_ABL_NOM
-#define GTSFM_PP_ABL_NOM 0
-#endif
-#ifndef GTSFM_PP_ABL_NOE
-#define GTSFM_PP_ABL_NOE 0
-#endif
 #ifndef GTSFM_PP_PRIO_M
 #define GTSFM_PP_PRIO_M 2
 #endif
@@ -431,10 +411,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 #ifndef GTSFM_PP_STATIC_PRIO
         __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_M);  // the MFMA stream outranks the partner wave's VALU epilogue
 #endif
-        if (GTSFM_PP_ABL_NOM)
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
-        if (rows_here && !GTSFM_PP_ABL_NOM) {  // ABL: timing ablations only
+        if (rows_here) {
             const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) acc[sub][0] = acc[sub][1] = f32x16{};
@@ -474,7 +451,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 #ifdef GTSFM_PP_STAMPS
         te0 = te1 = te2 = te3 = __builtin_amdgcn_s_memtime();
 #endif
-        if (rows_here && !GTSFM_PP_ABL_NOE) {
+        if (rows_here) {
 #ifdef GTSFM_PP_STAMPS
             te1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -553,9 +530,6 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
             dold = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             dm1 = m1; dm2 = m2; dptr = c1s; dpend = true;
-#elif defined(GTSFM_PP_NRT)  // timing bound only (wrong second-best): both atomics without return
-            __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            const uint32_t old = 0;
 #else
             const uint32_t old = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #endif
