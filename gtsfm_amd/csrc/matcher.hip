@@ -986,6 +986,7 @@ __global__ __launch_bounds__(256) void fl_prep_kernel(const float* __restrict__ 
 typedef _Float16 fl_half8 __attribute__((ext_vector_type(8)));
 typedef unsigned fl_u32x4 __attribute__((ext_vector_type(4)));
 typedef float fl_float16 __attribute__((ext_vector_type(16)));
+typedef float fl_float2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void fl_insert(float x, int j, float (&v)[kFlCand], int (&id)[kFlCand]) {
     // v sorted ascending and x < v[kFlCand - 1]: branch-free insertion (each slot takes its left neighbour, x or itself)
@@ -1222,8 +1223,10 @@ __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restr
                                                             const int* __restrict__ unc, ExactTop2* __restrict__ rowres,
                                                             ExactTop2* __restrict__ colres) {
 #pragma clang fp contract(off)
-    __shared__ float Qs[kXT][kXK + 1];
-    __shared__ float Ts[kXT][kXK + 1];
+    // k-major tiles (row stride kXT + 4: 16-B aligned b128 reads, 2-way store conflicts): a thread's 4 rows / columns
+    // of one k are one ds_read_b128 each
+    __shared__ __attribute__((aligned(16))) float Qs[kXK][kXT + 4];
+    __shared__ __attribute__((aligned(16))) float Ts[kXK][kXT + 4];
     __shared__ float mb1[16][kXT], mb2[16][kXT];
     __shared__ int mj[16][kXT];
     const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x;
@@ -1239,39 +1242,42 @@ __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < 4; ++i) { b1[i] = b2[i] = __builtin_inff(); j1[i] = -1; }
     for (int t0 = 0; t0 < nt; t0 += kXT) {
-        float acc[4][4];
+        // packed fp32 (v_pk_add_f32 / v_pk_mul_f32: two IEEE lanes, never fused): acc2[i][h] holds columns j = 2h, 2h+1
+        fl_float2 acc2[4][2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+        for (int i = 0; i < 4; ++i) acc2[i][0] = acc2[i][1] = fl_float2{0.f, 0.f};
         for (int k0 = 0; k0 < dim; k0 += kXK) {
             __syncthreads();
             for (int e = tid; e < kXT * kXK; e += 256) {
                 const int r = e / kXK, k = e % kXK;
                 const bool kin = k0 + k < dim;
-                Qs[r][k] = (kin && q0 + r < nq) ? Q[(size_t)r * dim + k0 + k] : 0.f;
-                Ts[r][k] = (kin && t0 + r < nt) ? T[(size_t)(t0 + r) * dim + k0 + k] : 0.f;
+                Qs[k][r] = (kin && q0 + r < nq) ? Q[(size_t)r * dim + k0 + k] : 0.f;
+                Ts[k][r] = (kin && t0 + r < nt) ? T[(size_t)(t0 + r) * dim + k0 + k] : 0.f;
             }
             __syncthreads();
 #pragma unroll 4
             for (int k = 0; k < kXK; ++k) {
-                float qv[4], tv[4];
+                const f32x4 qv = *(const f32x4*)&Qs[k][4 * tq];  // rows 4 tq + i
+                const f32x4 tv = *(const f32x4*)&Ts[k][4 * tt];  // columns 4 tt + j
+                const fl_float2 t01 = {tv[0], tv[1]}, t23 = {tv[2], tv[3]};
 #pragma unroll
-                for (int i = 0; i < 4; ++i) qv[i] = Qs[tq + 16 * i][k];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) tv[j] = Ts[tt + 16 * j][k];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const float df = qv[i] - tv[j];
-                        acc[i][j] = acc[i][j] + df * df;  // unfused, k ascending: contract(off) above
-                    }
+                for (int i = 0; i < 4; ++i) {
+                    const fl_float2 qq = {qv[i], qv[i]};
+                    const fl_float2 d0 = qq - t01, d1 = qq - t23;
+                    acc2[i][0] = acc2[i][0] + d0 * d0;  // unfused, k ascending: contract(off) above
+                    acc2[i][1] = acc2[i][1] + d1 * d1;
+                }
             }
+        }
+        float acc[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            acc[i][0] = acc2[i][0].x; acc[i][1] = acc2[i][0].y;
+            acc[i][2] = acc2[i][1].x; acc[i][3] = acc2[i][1].y;
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int t = t0 + tt + 16 * j;
+            const int t = t0 + 4 * tt + j;
             if (t >= nt) continue;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -1284,9 +1290,9 @@ __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restr
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        mb1[tt][tq + 16 * i] = b1[i];
-        mb2[tt][tq + 16 * i] = b2[i];
-        mj[tt][tq + 16 * i] = j1[i];
+        mb1[tt][4 * tq + i] = b1[i];
+        mb2[tt][4 * tq + i] = b2[i];
+        mj[tt][4 * tq + i] = j1[i];
     }
     __syncthreads();
     if (tid >= kXT || q0 + tid >= nq) return;
