@@ -1144,7 +1144,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
     *ns_out = ns;
 }
 
-// One 4-wave workgroup per active pair: the pair's putatives are staged in LDS once, then the launch's chunks are
+// One kScoreWaves-wave workgroup per active pair: the pair's putatives are staged in LDS once, then the launch's chunks are
 // scored in order. A chunk's candidates (flattened in (hypothesis, solution) order) are dealt round-robin to the
 // waves, each counted by one wave with an exact early exit against the running best. The best is an LDS atomicMax on
 // the key (count + 1, ~index), so the winner is the FIRST candidate in order with the largest count, as in the
@@ -1154,7 +1154,10 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
 // kMsac: the key is (~score, ~index) with the quantised MSAC score (msac_cost); a candidate stops once its partial
 // score (which only grows) exceeds the best, or equals it from a later index. The winner's inlier count (for the
 // iteration bound and the status) is kept per candidate in LDS.
-constexpr int kScoreWaves = 4;
+#ifndef GTSFM_SCORE_WAVES
+#define GTSFM_SCORE_WAVES 8  // waves per pair (r02: 4 -> 8 took 0.3 ms off verify; 16 was slower)
+#endif
+constexpr int kScoreWaves = GTSFM_SCORE_WAVES;
 
 template <bool kLds, bool kMsac>
 __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,

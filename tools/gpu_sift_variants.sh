@@ -9,5 +9,5 @@ for v in base "$@"; do
   echo "== $v"
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/sv_$v -o run -- python $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $R/gpurun_out/sv_$v.log 2>&1) || exit 1
   grep -o '"stage_ms": {[^}]*}' $R/gpurun_out/sv_$v.log
-  python $R/tools/kstats.py "$(find $R/gpurun_out/sv_$v -name "*kernel_stats.csv" | head -1)" | grep -E "blur|extrema|descriptor|orientation|refine|topk"
+  python $R/tools/kstats.py "$(find $R/gpurun_out/sv_$v -name "*kernel_stats.csv" | head -1)" | grep -E "${KPAT:-blur|extrema|descriptor|orientation|refine|topk}"
 done
