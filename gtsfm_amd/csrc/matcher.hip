@@ -137,7 +137,10 @@ constexpr int kPpWaves = 2 * kPpGroupWaves;
 constexpr int kPpThreads = kPpWaves * 64;
 constexpr int kPpRowsPerPass = kPpWaves * 64;  // 512
 constexpr int kUnitCols = 64;
-constexpr int kMaxGroup = 4;
+#ifndef GTSFM_PP_MAX_GROUP
+#define GTSFM_PP_MAX_GROUP 4
+#endif
+constexpr int kMaxGroup = GTSFM_PP_MAX_GROUP;
 constexpr int kPpLdsBudget = 160 * 1024;
 constexpr int kRowAlign = 256;                 // kpad granularity of the packed forms
 
