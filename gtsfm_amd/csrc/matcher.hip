@@ -1075,18 +1075,32 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
 #pragma unroll
             for (int s = 0; s < NS; ++s)
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const fl_half8*)(arow + 16 * s), bq[s], acc, 0, 0, 0);
+            // the tile's 16 keys of this lane, a mask of those below the shortlist's current last key, then one
+            // insert per wave iteration for every lane that still has a set bit, in index order: the same insertion
+            // sequence as testing the keys one by one, but the wave runs max(popcount) inserts instead of one per
+            // key that ANY lane accepts
+            float kk[16];
+            uint32_t mask = 0;
+            const float thr = v[kFlCand - 1];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4 nb = *(const float4*)(nbl + buf * kFlRows + t * 32 + 8 * g + 4 * h);
-                const float k0 = fmaf(-2.f, acc[4 * g], nb.x), k1 = fmaf(-2.f, acc[4 * g + 1], nb.y);
-                const float k2 = fmaf(-2.f, acc[4 * g + 2], nb.z), k3 = fmaf(-2.f, acc[4 * g + 3], nb.w);
-                const float kmin = fminf(fminf(k0, k1), fminf(k2, k3));
-                if (__ballot(kmin < v[kFlCand - 1]) == 0ull) continue;
-                const int jb = c0 + t * 32 + 8 * g + 4 * h;
-                if (k0 < v[kFlCand - 1]) fl_insert(k0, jb, v, id);
-                if (k1 < v[kFlCand - 1]) fl_insert(k1, jb + 1, v, id);
-                if (k2 < v[kFlCand - 1]) fl_insert(k2, jb + 2, v, id);
-                if (k3 < v[kFlCand - 1]) fl_insert(k3, jb + 3, v, id);
+                kk[4 * g] = fmaf(-2.f, acc[4 * g], nb.x);
+                kk[4 * g + 1] = fmaf(-2.f, acc[4 * g + 1], nb.y);
+                kk[4 * g + 2] = fmaf(-2.f, acc[4 * g + 2], nb.z);
+                kk[4 * g + 3] = fmaf(-2.f, acc[4 * g + 3], nb.w);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) mask |= (kk[4 * g + e] < thr ? 1u : 0u) << (4 * g + e);
+            }
+            while (__ballot(mask != 0u) != 0ull) {
+                if (mask != 0u) {
+                    const int i = __builtin_ctz(mask);
+                    mask &= mask - 1u;
+                    float x = kk[0];
+#pragma unroll
+                    for (int q = 1; q < 16; ++q) x = i == q ? kk[q] : x;
+                    if (x < v[kFlCand - 1]) fl_insert(x, c0 + t * 32 + 8 * (i >> 2) + 4 * h + (i & 3), v, id);
+                }
             }
         }
         if (c + 1 < n_chunks) {
