@@ -992,14 +992,19 @@ typedef float fl_float16 __attribute__((ext_vector_type(16)));
 typedef float fl_float2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void fl_insert(float x, int j, float (&v)[kFlCand], int (&id)[kFlCand]) {
-    // v sorted ascending and x < v[kFlCand - 1]: branch-free insertion (each slot takes its left neighbour, x or itself)
+    // v sorted ascending and x < v[kFlCand - 1]: branch-free insertion (each slot takes its left neighbour, x or
+    // itself). The key of slot m is med3(v[m-1], x, v[m]) -- v[m-1] when x < v[m-1], x when v[m-1] <= x < v[m], else
+    // v[m] -- one v_med3_f32; the ids follow the same strict comparisons, each computed once.
+    bool lt[kFlCand];
+#pragma unroll
+    for (int m = 0; m < kFlCand; ++m) lt[m] = x < v[m];
 #pragma unroll
     for (int m = kFlCand - 1; m > 0; --m) {
-        const bool sh = x < v[m - 1], here = x < v[m];
-        v[m] = sh ? v[m - 1] : (here ? x : v[m]);
-        id[m] = sh ? id[m - 1] : (here ? j : id[m]);
+        v[m] = __builtin_amdgcn_fmed3f(v[m - 1], x, v[m]);
+        id[m] = lt[m - 1] ? id[m - 1] : (lt[m] ? j : id[m]);
     }
-    if (x < v[0]) { v[0] = x; id[0] = j; }
+    v[0] = lt[0] ? x : v[0];
+    id[0] = lt[0] ? j : id[0];
 }
 
 template <int NV, int DP>
