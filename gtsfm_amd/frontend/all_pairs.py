@@ -42,7 +42,7 @@ class FrontEndConfig:
     extract_chunk: int = 40          # host steps: images per SIFT launch sequence (the next chunk's H2D overlaps it)
     extract_first: int = 20          # host steps: size of a smaller first chunk (less exposed H2D); 0 = extract_chunk
     resident_chunk: int = 100        # device-resident steps: images per SIFT launch sequence (bounded by workspace)
-    pair_chunk: int = 32768          # pairs per match / verify / compact launch sequence
+    pair_chunk: int = 131072         # pairs per match / verify / compact launch sequence (C4: 272k -> 283k pairs/s vs 32768)
     bundle_adjust: bool = False      # TwoViewEstimator bundle_adjust_2view: two-view triangulation + BA after RANSAC
     ba_max_iters: int = 100          # bundle_adjust_2view_maxiters
     ba_reproj_thresh: float = 0.5    # ba_reproj_error_thresholds[-1]
