@@ -1232,13 +1232,23 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
 // uncertified keypoints are rescanned one by one.
 constexpr int kFlTileFrac = 32;
 __device__ __forceinline__ bool fl_use_tile(int n_unc, int nq) { return n_unc > 0 && n_unc * kFlTileFrac >= nq; }
+// both sides of pair p are tiled: one pass computes each exact distance once and reduces it both ways
+__device__ __forceinline__ bool fl_both(const int* unc, const int* counts, const int* pairs, int n_pairs, int p) {
+    return fl_use_tile(unc[p], counts[pairs[2 * p]]) && fl_use_tile(unc[n_pairs + p], counts[pairs[2 * p + 1]]);
+}
 
 // Exact top-2 of every keypoint of a flagged (pair, side), tiled: a block takes 64 query rows against all train rows
 // in 64-row tiles, K in 32-deep LDS chunks; thread (tq, tt) runs the 16 chains of query rows tq + 16 i and train rows
 // tt + 16 j, each the sequential unfused sum over k of exact_top2_kernel (zero padding past dim adds exact zeros), and
 // folds its train rows in increasing order with the strict-'<' update. The 16 partial (b1, j1, b2) of a row merge by
 // (b1, j1) lexicographic minimum with b2 = min(other b1, own b2): the scan's result in any merge order.
+// kBoth (pairs with both sides tiled, grid z = 1): the block's distances also feed the columns -- per column a
+// top-2 over the thread's 4 rows, merged across the 16 row threads by shuffles, then folded into the pair's side-1
+// state in colres with a returning 64-bit atomicMin on (d1 bits << 32 | row) (slots j1 | pad of the record) and a
+// 32-bit atomicMin of min(max(old d1, d1), d2) on d2 -- the exact top-2 in any arrival order, ties to the lowest row,
+// as the strict-'<' scan of that side. Distances are symmetric bit for bit ((a - b)^2 == (b - a)^2).
 constexpr int kXT = 64, kXK = 32;
+template <bool kBoth>
 __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restrict__ desc,
                                                             const int* __restrict__ counts, int kmax, int dim,
                                                             const int* __restrict__ pairs, int n_pairs,
@@ -1251,11 +1261,12 @@ __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restr
     __shared__ __attribute__((aligned(16))) float Ts[kXK][kXT + 4];
     __shared__ float mb1[16][kXT], mb2[16][kXT];
     __shared__ int mj[16][kXT];
-    const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x;
+    const int p = blockIdx.y, side = kBoth ? 0 : blockIdx.z, tid = threadIdx.x;
     const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
     const int nq = counts[iq], nt = counts[it];
     const int q0 = blockIdx.x * kXT;
     if (q0 >= nq || !fl_use_tile(unc[side * n_pairs + p], nq)) return;
+    if (fl_both(unc, counts, pairs, n_pairs, p) != kBoth) return;
     const int tq = tid & 15, tt = tid >> 4;
     const float* Q = desc + ((size_t)iq * kmax + q0) * dim;
     const float* T = desc + (size_t)it * kmax * dim;
@@ -1297,15 +1308,57 @@ __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restr
             acc[i][0] = acc2[i][0].x; acc[i][1] = acc2[i][0].y;
             acc[i][2] = acc2[i][1].x; acc[i][3] = acc2[i][1].y;
         }
+        float dd[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dd[i][j] = sqrt_cr(acc[i][j]);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int t = t0 + 4 * tt + j;
             if (t >= nt) continue;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const float d = sqrt_cr(acc[i][j]);
+                const float d = dd[i][j];
                 if (d < b2[i]) {
                     if (d < b1[i]) { b2[i] = b1[i]; b1[i] = d; j1[i] = t; } else { b2[i] = d; }
+                }
+            }
+        }
+        if constexpr (kBoth) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                // this thread's 4 rows of column t0 + 4 tt + j (rows past nq excluded), in row order
+                float c1 = __builtin_inff(), c2 = __builtin_inff();
+                int ci = 0x7fffffff;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int r = q0 + 4 * tq + i;
+                    if (r < nq) {
+                        const float d = dd[i][j];
+                        if (d < c2) {
+                            if (d < c1) { c2 = c1; c1 = d; ci = r; } else { c2 = d; }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int m = 1; m < 16; m <<= 1) {  // the 16 row threads of this column group: lanes tq ^ m
+                    const float o1 = __shfl_xor(c1, m), o2 = __shfl_xor(c2, m);
+                    const int oi = __shfl_xor(ci, m);
+                    const bool tb = o1 < c1 || (o1 == c1 && oi < ci);
+                    const float n2 = tb ? fminf(c1, o2) : fminf(c2, o1);
+                    c1 = tb ? o1 : c1;
+                    ci = tb ? oi : ci;
+                    c2 = n2;
+                }
+                const int t = t0 + 4 * tt + j;
+                if (tq == 0 && t < nt && ci != 0x7fffffff) {
+                    ExactTop2* e = colres + (size_t)p * kmax + t;
+                    const unsigned long long key =
+                        ((unsigned long long)__float_as_uint(c1) << 32) | (unsigned long long)(uint32_t)ci;
+                    const unsigned long long old = atomicMin((unsigned long long*)&e->j1, key);
+                    const uint32_t oh = (uint32_t)(old >> 32);
+                    atomicMin((unsigned int*)&e->d2, umin(umax(oh, __float_as_uint(c1)), __float_as_uint(c2)));
                 }
             }
         }
@@ -1333,6 +1386,24 @@ __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restr
         }
     }
     (side ? colres : rowres)[(size_t)p * kmax + q0 + tid] = ExactTop2{c1, c2, cj, 1};
+}
+
+// Side-1 state of the both-sides pairs before / after fl_exact_tile_kernel<true>: (d2 = +inf, j1 | pad = ~0), then
+// d1 from the pad slot and pad = 1 (recomputed), as the per-side kernel leaves its records.
+__global__ __launch_bounds__(256) void fl_tile2_init_kernel(const int* __restrict__ counts,
+                                                            const int* __restrict__ pairs, int n_pairs, int kmax,
+                                                            const int* __restrict__ unc, ExactTop2* __restrict__ colres,
+                                                            int fix) {
+    const int p = blockIdx.y, t = blockIdx.x * 256 + threadIdx.x;
+    if (!fl_both(unc, counts, pairs, n_pairs, p)) return;
+    if (t >= counts[pairs[2 * p + 1]]) return;
+    ExactTop2* e = colres + (size_t)p * kmax + t;
+    if (!fix) {
+        *e = ExactTop2{0.f, __builtin_inff(), -1, -1};
+    } else {
+        const ExactTop2 v = *e;
+        *e = ExactTop2{__int_as_float(v.pad), v.d2, v.j1, 1};
+    }
 }
 
 // Exact rescan of the uncertified keypoints: one 256-thread block per keypoint (block_exact_top2), except those of
@@ -1423,8 +1494,14 @@ int run_fl_match(const float* d_desc, const int* d_counts, int n_img, int kmax, 
                        stream, d_desc, d_counts, kmax, dim, d_pairs, n_pairs, kpad, norm2, maxnorm, unsafe, cand, tkey,
                        rowres, colres, redo_count, redo, unc);
     GTSFM_CHECK_HIP(hipGetLastError());
-    hipLaunchKernelGGL(fl_exact_tile_kernel, dim3((kmax + kXT - 1) / kXT, n_pairs, 2), dim3(256), 0, stream, d_desc,
-                       d_counts, kmax, dim, d_pairs, n_pairs, unc, rowres, colres);
+    hipLaunchKernelGGL(fl_exact_tile_kernel<false>, dim3((kmax + kXT - 1) / kXT, n_pairs, 2), dim3(256), 0, stream,
+                       d_desc, d_counts, kmax, dim, d_pairs, n_pairs, unc, rowres, colres);
+    hipLaunchKernelGGL(fl_tile2_init_kernel, dim3((kmax + 255) / 256, n_pairs), dim3(256), 0, stream, d_counts,
+                       d_pairs, n_pairs, kmax, unc, colres, 0);
+    hipLaunchKernelGGL(fl_exact_tile_kernel<true>, dim3((kmax + kXT - 1) / kXT, n_pairs, 1), dim3(256), 0, stream,
+                       d_desc, d_counts, kmax, dim, d_pairs, n_pairs, unc, rowres, colres);
+    hipLaunchKernelGGL(fl_tile2_init_kernel, dim3((kmax + 255) / 256, n_pairs), dim3(256), 0, stream, d_counts,
+                       d_pairs, n_pairs, kmax, unc, colres, 1);
     hipLaunchKernelGGL(fl_rescan_kernel, dim3(2048), dim3(kFinThreads), 0, stream, d_desc, d_counts, kmax, dim,
                        d_pairs, n_pairs, redo_count, redo, unc, rowres, colres);
     GTSFM_CHECK_HIP(hipGetLastError());
