@@ -1247,7 +1247,10 @@ __device__ __forceinline__ bool fl_both(const int* unc, const int* counts, const
 // state in colres with a returning 64-bit atomicMin on (d1 bits << 32 | row) (slots j1 | pad of the record) and a
 // 32-bit atomicMin of min(max(old d1, d1), d2) on d2 -- the exact top-2 in any arrival order, ties to the lowest row,
 // as the strict-'<' scan of that side. Distances are symmetric bit for bit ((a - b)^2 == (b - a)^2).
-constexpr int kXT = 64, kXK = 32;
+#ifndef GTSFM_XK
+#define GTSFM_XK 16  // 16: the transposed tile stores hit 64 distinct banks (C3: 32 -> 16 took 8.09 -> 7.63 s of matching)
+#endif
+constexpr int kXT = 64, kXK = GTSFM_XK;
 template <bool kBoth>
 __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restrict__ desc,
                                                             const int* __restrict__ counts, int kmax, int dim,
