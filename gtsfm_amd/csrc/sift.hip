@@ -411,6 +411,100 @@ struct GaussSet {
     const float* g[kLevels];
 };
 
+#define DAT(l, r, c) (G.g[(l) + 1][base + (size_t)(r) * W + (c)] - G.g[(l)][base + (size_t)(r) * W + (c)])
+
+// Sub-pixel refinement (cv::SIFT adjustLocalExtrema) of one candidate: true and `res` for a kept keypoint. Duplicates
+// (same refined location) are identical keypoints: the first claimant of the location's `seen` bit keeps it.
+__device__ __forceinline__ bool refine_one(const Cand cd, const GaussSet& G, int H, int W, uint32_t* __restrict__ seen,
+                                           Refined& res) {
+    const float img_scale = 1.f / 255.f;
+    const float deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale, cross_deriv_scale = img_scale * 0.25f;
+    const size_t base = (size_t)cd.img * H * W;
+    int layer = cd.layer, r = cd.r, c = cd.c;
+    float xi = 0, xr = 0, xc = 0;
+    int i = 0;
+    bool ok = true;
+    for (; i < kMaxInterp; i++) {
+        const int img = layer, prev = layer - 1, next = layer + 1;
+        const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
+        const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
+        const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
+        const float v2 = DAT(img, r, c) * 2;
+        const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
+        const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
+        const float dss = (DAT(next, r, c) + DAT(prev, r, c) - v2) * second_deriv_scale;
+        const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
+                           DAT(img, r - 1, c - 1)) * cross_deriv_scale;
+        const float dxs = (DAT(next, r, c + 1) - DAT(next, r, c - 1) - DAT(prev, r, c + 1) +
+                           DAT(prev, r, c - 1)) * cross_deriv_scale;
+        const float dys = (DAT(next, r + 1, c) - DAT(next, r - 1, c) - DAT(prev, r + 1, c) +
+                           DAT(prev, r - 1, c)) * cross_deriv_scale;
+        const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
+                    a22 = dss;
+        float det = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
+        float X0 = 0, X1 = 0, X2 = 0;
+        if (det != 0) {
+            det = 1 / det;
+            X0 = det * (dD0 * (a11 * a22 - a12 * a21) - a01 * (dD1 * a22 - a12 * dD2) + a02 * (dD1 * a21 - a11 * dD2));
+            X1 = det * (a00 * (dD1 * a22 - a12 * dD2) - dD0 * (a10 * a22 - a12 * a20) + a02 * (a10 * dD2 - dD1 * a20));
+            X2 = det * (a00 * (a11 * dD2 - dD1 * a21) - a01 * (a10 * dD2 - dD1 * a20) + dD0 * (a10 * a21 - a11 * a20));
+        }
+        xi = -X2;
+        xr = -X1;
+        xc = -X0;
+        if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
+        if (fabsf(xi) > (float)(INT32_MAX / 3) || fabsf(xr) > (float)(INT32_MAX / 3) ||
+            fabsf(xc) > (float)(INT32_MAX / 3)) {
+            ok = false;
+            break;
+        }
+        c += (int)rintf(xc);
+        r += (int)rintf(xr);
+        layer += (int)rintf(xi);
+        if (layer < 1 || layer > kLayers || c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) {
+            ok = false;
+            break;
+        }
+    }
+    if (!ok || i >= kMaxInterp) return false;
+    const int img = layer, prev = layer - 1, next = layer + 1;
+    const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
+    const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
+    const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
+    const float tt = dD0 * xc + dD1 * xr + dD2 * xi;
+    const float contr = DAT(img, r, c) * img_scale + tt * 0.5f;
+    if (fabsf(contr) * kLayers < kContrast) return false;
+    const float v2 = DAT(img, r, c) * 2.f;
+    const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
+    const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
+    const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
+                       DAT(img, r - 1, c - 1)) * cross_deriv_scale;
+    const float tr = dxx + dyy;
+    const float det = dxx * dyy - dxy * dxy;
+    if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) return false;
+    // duplicates (same refined location) are identical keypoints: keep the first claimant
+    const size_t bit = (((size_t)cd.img * kLayers + (layer - 1)) * H + r) * W + c;
+    const uint32_t m = 1u << (bit & 31);
+    if (atomicOr(&seen[bit >> 5], m) & m) return false;
+    res = Refined{cd.img, layer, r, c, xc, xr, xi, contr};
+    return true;
+}
+
+// Wave-aggregated append of the kept refinements (ballot + prefix popcount, one atomic per wave); every lane of the
+// wave calls it.
+__device__ __forceinline__ void append_refined(bool keep, const Refined& res, Refined* __restrict__ out,
+                                               int* __restrict__ n_out, int out_cap) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long bal = __ballot(keep);
+    if (bal) {
+        int wbase = 0;
+        if (lane == 0) wbase = atomicAdd(n_out, (int)__popcll(bal));
+        wbase = __shfl(wbase, 0);
+        const int slot = wbase + (int)__popcll(bal & ((1ull << lane) - 1ull));
+        if (keep && slot < out_cap) out[slot] = res;
+    }
+}
+
 // DoG levels are never stored: DoG_l = G_{l+1} - G_l is recomputed from the Gaussian levels (the same fp32
 // subtraction cv::subtract performs), which removes 5 level writes per octave.
 // Extrema scan: each wave sweeps a strip of kExStrip rows down 64 consecutive columns (lanes 1..62 produce outputs,
@@ -440,8 +534,16 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane l gets lane 
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
+#ifndef GTSFM_ORI_SCRAMBLE
+#define GTSFM_ORI_SCRAMBLE 1
+#endif
+#ifndef GTSFM_SIFT_FUSED_REFINE
+#define GTSFM_SIFT_FUSED_REFINE 1
+#endif
 __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
-                                                                int* __restrict__ n_cand, int cap) {
+                                                                int* __restrict__ n_cand, int cap,
+                                                                uint32_t* __restrict__ seen, Refined* __restrict__ out,
+                                                                int* __restrict__ n_out, int out_cap) {
     __shared__ Cand list[kExList];
     __shared__ ExPend pend[kExPend];
     __shared__ int n_list, n_pend, gbase;
@@ -608,112 +710,38 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     }
     __syncthreads();
     const int n = min(n_list, kExList);
+#if GTSFM_SIFT_FUSED_REFINE
+    // refine the block's own candidates now, while the strip's Gaussian rows are still in L2 (a separate pass
+    // re-fetched each candidate's 3x3x3 window from HBM)
+    // (entries dealt round-robin to the waves: a short list keeps every wave busy on the dependent gathers)
+    for (int base0 = 0; base0 < n; base0 += 64 * kExWaves) {
+        const int i = base0 + lane * kExWaves + wave;
+        Refined res;
+        const bool keep = i < n && refine_one(list[i], G, H, W, seen, res);
+        append_refined(keep, res, out, n_out, out_cap);
+    }
+#else
     if (threadIdx.x == 0) gbase = n ? atomicAdd(&n_cand[shard], n) : 0;
     __syncthreads();
     for (int i = threadIdx.x; i < n; i += 64 * kExWaves)
         if (gbase + i < cap) cands[(size_t)shard * cap + gbase + i] = list[i];
+#endif
 }
 
-#define DAT(l, r, c) (G.g[(l) + 1][base + (size_t)(r) * W + (c)] - G.g[(l)][base + (size_t)(r) * W + (c)])
-
-// Sub-pixel refinement (cv::SIFT adjustLocalExtrema). Candidates come from kCandShards segments of `cap` entries;
-// survivors are appended with one atomic per wave (ballot + prefix popcount).
+// Candidates left in the kCandShards global segments (extrema blocks whose LDS list overflowed; with
+// GTSFM_SIFT_FUSED_REFINE 0, all of them) are refined here.
 __global__ __launch_bounds__(256) void refine_kernel(const Cand* __restrict__ cands,
                                                      const int* __restrict__ shard_counts, int cap, GaussSet G, int H,
                                                      int W, int n_img, uint32_t* __restrict__ seen,
                                                      Refined* __restrict__ out, int* __restrict__ n_out, int out_cap) {
-    const int lane = threadIdx.x & 63;
-    const float img_scale = 1.f / 255.f;
-    const float deriv_scale = img_scale * 0.5f, second_deriv_scale = img_scale, cross_deriv_scale = img_scale * 0.25f;
     // gridDim.x is a multiple of kCandShards: each shard is worked by gridDim.x / kCandShards blocks
-    {
     const int sh = blockIdx.x % kCandShards, sub = blockIdx.x / kCandShards, nsub = gridDim.x / kCandShards;
     const int n_cand = min(shard_counts[sh], cap);
     for (int base0 = sub * blockDim.x; base0 < n_cand; base0 += nsub * blockDim.x) {
         const int id = base0 + threadIdx.x;
         Refined res;
-        bool keep = false;
-        if (id < n_cand) do {
-        const Cand cd = cands[(size_t)sh * cap + id];
-        const size_t base = (size_t)cd.img * H * W;
-        int layer = cd.layer, r = cd.r, c = cd.c;
-        float xi = 0, xr = 0, xc = 0;
-        int i = 0;
-        bool ok = true;
-        for (; i < kMaxInterp; i++) {
-            const int img = layer, prev = layer - 1, next = layer + 1;
-            const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
-            const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
-            const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
-            const float v2 = DAT(img, r, c) * 2;
-            const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
-            const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
-            const float dss = (DAT(next, r, c) + DAT(prev, r, c) - v2) * second_deriv_scale;
-            const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
-                               DAT(img, r - 1, c - 1)) * cross_deriv_scale;
-            const float dxs = (DAT(next, r, c + 1) - DAT(next, r, c - 1) - DAT(prev, r, c + 1) +
-                               DAT(prev, r, c - 1)) * cross_deriv_scale;
-            const float dys = (DAT(next, r + 1, c) - DAT(next, r - 1, c) - DAT(prev, r + 1, c) +
-                               DAT(prev, r - 1, c)) * cross_deriv_scale;
-            const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
-                        a22 = dss;
-            float det = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
-            float X0 = 0, X1 = 0, X2 = 0;
-            if (det != 0) {
-                det = 1 / det;
-                X0 = det * (dD0 * (a11 * a22 - a12 * a21) - a01 * (dD1 * a22 - a12 * dD2) + a02 * (dD1 * a21 - a11 * dD2));
-                X1 = det * (a00 * (dD1 * a22 - a12 * dD2) - dD0 * (a10 * a22 - a12 * a20) + a02 * (a10 * dD2 - dD1 * a20));
-                X2 = det * (a00 * (a11 * dD2 - dD1 * a21) - a01 * (a10 * dD2 - dD1 * a20) + dD0 * (a10 * a21 - a11 * a20));
-            }
-            xi = -X2;
-            xr = -X1;
-            xc = -X0;
-            if (fabsf(xi) < 0.5f && fabsf(xr) < 0.5f && fabsf(xc) < 0.5f) break;
-            if (fabsf(xi) > (float)(INT32_MAX / 3) || fabsf(xr) > (float)(INT32_MAX / 3) ||
-                fabsf(xc) > (float)(INT32_MAX / 3)) {
-                ok = false;
-                break;
-            }
-            c += (int)rintf(xc);
-            r += (int)rintf(xr);
-            layer += (int)rintf(xi);
-            if (layer < 1 || layer > kLayers || c < kBorder || c >= W - kBorder || r < kBorder || r >= H - kBorder) {
-                ok = false;
-                break;
-            }
-        }
-        if (!ok || i >= kMaxInterp) break;
-        const int img = layer, prev = layer - 1, next = layer + 1;
-        const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
-        const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
-        const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
-        const float tt = dD0 * xc + dD1 * xr + dD2 * xi;
-        const float contr = DAT(img, r, c) * img_scale + tt * 0.5f;
-        if (fabsf(contr) * kLayers < kContrast) break;
-        const float v2 = DAT(img, r, c) * 2.f;
-        const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
-        const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
-        const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
-                           DAT(img, r - 1, c - 1)) * cross_deriv_scale;
-        const float tr = dxx + dyy;
-        const float det = dxx * dyy - dxy * dxy;
-        if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) break;
-        // duplicates (same refined location) are identical keypoints: keep the first claimant
-        const size_t bit = (((size_t)cd.img * kLayers + (layer - 1)) * H + r) * W + c;
-        const uint32_t m = 1u << (bit & 31);
-        if (atomicOr(&seen[bit >> 5], m) & m) break;
-        res = Refined{cd.img, layer, r, c, xc, xr, xi, contr};
-        keep = true;
-        } while (0);
-        const unsigned long long bal = __ballot(keep);
-        if (bal) {
-            int wbase = 0;
-            if (lane == 0) wbase = atomicAdd(n_out, (int)__popcll(bal));
-            wbase = __shfl(wbase, 0);
-            const int slot = wbase + (int)__popcll(bal & ((1ull << lane) - 1ull));
-            if (keep && slot < out_cap) out[slot] = res;
-        }
-    }
+        const bool keep = id < n_cand && refine_one(cands[(size_t)sh * cap + id], G, H, W, seen, res);
+        append_refined(keep, res, out, n_out, out_cap);
     }
 }
 
@@ -728,7 +756,13 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
     for (int id = blockIdx.x; id < n_ref; id += gridDim.x) {
         if (lane < kOriBins) hist[lane] = 0ull;
         __syncthreads();
+#if GTSFM_ORI_SCRAMBLE
+        // the refinement appends in extrema-block order (spatial clusters); a fixed bijective scramble spreads
+        // concurrent waves over the image (2654435761 is prime, n_ref < 2^31)
+        const Refined rf = refs[(int)(((unsigned long long)id * 2654435761ull) % (unsigned)n_ref)];
+#else
         const Refined rf = refs[id];
+#endif
         const float size_oct = kSigma * exp2_det(((float)rf.layer + rf.xi) / kLayers);
         const float scl = size_oct;
         const int radius = (int)rintf(kOriRadius * scl);
@@ -1333,7 +1367,9 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         const int shard_cap = (int)((size_t)B * kCandCapPerImg / kCandShards);
         hipLaunchKernelGGL(extrema_kernel, dim3((w + kExWaves * kExOut - 1) / (kExWaves * kExOut),
                                                 (h + kExStrip - 1) / kExStrip, B),
-                           dim3(64 * kExWaves), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap);
+                           dim3(64 * kExWaves), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap,
+                           (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref), counters + kCandShards,
+                           B * kCandCapPerImg);
         hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
                            shard_cap, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg);

@@ -153,7 +153,10 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
 constexpr int kAttnKeys = 64;
 constexpr int kKvStride = kHd + 1;
 
-__global__ __launch_bounds__(256) void sg_attention_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
+#ifndef GTSFM_SG_ATT_OCC
+#define GTSFM_SG_ATT_OCC 3  // 168 VGPRs (4 spilled), 3 x 49.9 KB LDS per CU: C5 281 -> 315 pairs/s (r02m)
+#endif
+__global__ __launch_bounds__(256, GTSFM_SG_ATT_OCC) void sg_attention_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
                                                            const int* __restrict__ side_counts /*(2P)*/, int kmax,
                                                            int cross, float* __restrict__ out /*(2P, kmax, 256)*/) {
     __shared__ float Kc[kAttnKeys * kKvStride];
