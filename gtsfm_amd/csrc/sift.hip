@@ -1041,6 +1041,12 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __rest
 }
 
 // ------------------------------------------------------------------ descriptors: one wave per kept keypoint
+#ifndef GTSFM_DESC_SPREAD
+#define GTSFM_DESC_SPREAD 1
+#endif
+#ifndef GTSFM_DESC_COPIES
+#define GTSFM_DESC_COPIES 2
+#endif
 constexpr int kDescChunk = 512;
 
 __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict__ kps, int kp_cap,
@@ -1051,7 +1057,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
     constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
     // kCopies private histograms (lane & 1 picks one): adjacent samples usually land in the same bins, and same-address
     // LDS atomics of one instruction serialise. Integer (fixed-point) sums, so merging the copies is exact.
-    constexpr int kCopies = 2, HBP = HB + 1;  // +1: copies start on different banks
+    constexpr int kCopies = GTSFM_DESC_COPIES, HBP = HB + 1;  // +1: copies start on different banks
     __shared__ unsigned long long hist[kCopies * HBP];
     __shared__ int slist[kDescChunk];  // valid samples of the current chunk, (i << 16) | (j & 0xffff)
     __shared__ float dst[128];
@@ -1110,7 +1116,16 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
                 nv += __popcll(m);
             }
             __syncthreads();
+#if GTSFM_DESC_SPREAD
+            // lane l takes the contiguous run [l nit, (l + 1) nit) of the chunk's samples: one instruction's 64 atomics
+            // spread over the whole chunk's rows (and bins) instead of one or two raster rows
+            const int nit = (nv + 63) >> 6;
+            for (int it = 0; it < nit; ++it) {
+            const int t = lane * nit + it;
+            if (t >= nv) continue;
+#else
             for (int t = lane; t < nv; t += 64) {
+#endif
             const int sv = slist[t];
             const int i = sv >> 16, j = (short)(sv & 0xffff);
             const float c_rot = j * cos_t - i * sin_t;
