@@ -1158,6 +1158,10 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
 #define GTSFM_SCORE_WAVES 8  // waves per pair (r02: 4 -> 8 took 0.3 ms off verify; 16 was slower)
 #endif
 constexpr int kScoreWaves = GTSFM_SCORE_WAVES;
+#ifndef GTSFM_MSAC_PPL
+#define GTSFM_MSAC_PPL 2  // points per lane between two MSAC exit tests
+#endif
+constexpr int kMsacPpl = GTSFM_MSAC_PPL;
 
 template <bool kLds, bool kMsac>
 __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,
@@ -1233,15 +1237,18 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
             if constexpr (kMsac) {
                 uint32_t sc = 0;
 #pragma unroll 1
-                for (int base = 0; base < M; base += 128) {  // 128 points per reduction and exit test
+                for (int base = 0; base < M; base += 64 * kMsacPpl) {  // 64 kMsacPpl points per reduction and exit test
                     const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
                     const int i = base + lane;
-                    bool in0 = false, in1 = false;
-                    const uint32_t q0 = i < M ? msac_cost(E, sp[i], thr2, scale, in0) : 0u;
-                    const uint32_t q1 = i + 64 < M ? msac_cost(E, sp[i + 64], thr2, scale, in1) : 0u;
-                    c += __popcll(__ballot(in0)) + __popcll(__ballot(in1));
-                    sc += wave_sum_u32(q0 + q1);
-                    if (base + 128 < M) {
+                    uint32_t q = 0;
+#pragma unroll
+                    for (int u = 0; u < kMsacPpl; ++u) {
+                        bool in = false;
+                        q += i + 64 * u < M ? msac_cost(E, sp[i + 64 * u], thr2, scale, in) : 0u;
+                        c += __popcll(__ballot(in));
+                    }
+                    sc += wave_sum_u32(q);
+                    if (base + 64 * kMsacPpl < M) {
                         const uint32_t bs = ~(uint32_t)(bk >> 32);
                         if (sc > bs || (sc == bs && my_low < (uint32_t)bk)) {
                             alive = false;
