@@ -150,8 +150,16 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 constexpr int kBlurTX = 64;
 // Tile height per radius: 64 rows x 4 waves, or for the wide kernels (and the upsampling one) 96 rows x 8 waves, where
 // the smaller row-pass halo share pays for the coarser tiling (measured per radius on octave 0).
-__host__ __device__ constexpr int blur_ty(int r, bool u8) { return (u8 || r >= 9) ? 96 : 64; }
-__host__ __device__ constexpr int blur_tyt(int r, bool u8) { return blur_ty(r, u8) == 96 ? 8 : 4; }
+#ifndef GTSFM_BLUR_WIDE_R
+#define GTSFM_BLUR_WIDE_R 9
+#endif
+#ifndef GTSFM_BLUR_WIDE_TY
+#define GTSFM_BLUR_WIDE_TY 96
+#endif
+__host__ __device__ constexpr int blur_ty(int r, bool u8) {
+    return u8 ? 96 : (r >= GTSFM_BLUR_WIDE_R ? GTSFM_BLUR_WIDE_TY : 64);
+}
+__host__ __device__ constexpr int blur_tyt(int r, bool u8) { return blur_ty(r, u8) == 64 ? 4 : 8; }
 constexpr int kBlurRowOut = 8, kBlurRowThr = kBlurTX / kBlurRowOut;  // row pass: outputs per thread, threads per row
 typedef float pf2 __attribute__((ext_vector_type(2)));
 constexpr int kBlurMaxR = 16;
