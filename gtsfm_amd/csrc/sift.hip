@@ -1393,7 +1393,8 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
                            dim3(64 * kExWaves), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap,
                            (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref), counters + kCandShards,
                            B * kCandCapPerImg);
-        hipLaunchKernelGGL(refine_kernel, dim3(2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
+        // fused: only list overflows reach the shards, so one block per shard
+        hipLaunchKernelGGL(refine_kernel, dim3(GTSFM_SIFT_FUSED_REFINE ? kCandShards : 2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
                            shard_cap, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg);
         hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),

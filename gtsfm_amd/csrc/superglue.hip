@@ -49,7 +49,11 @@ __host__ __device__ constexpr size_t sg_weights_floats(int n_layers) {
 
 // ------------------------------------------------------------------ batched GEMM on fp32 MFMA
 constexpr int kGemmThreads = 256;
-constexpr int kKc = 16;  // K chunk staged in LDS
+#ifndef GTSFM_SG_KC
+#define GTSFM_SG_KC 16
+#endif
+constexpr int kKc = GTSFM_SG_KC;  // K chunk staged in LDS (a multiple of 16; chunks past K are zero-filled)
+static_assert(kKc % 16 == 0, "K chunk");
 
 struct GemmArgs {
     const float* A;   // A[z][m][k] (k < Ksplit), row stride lda, batch stride a_batch
@@ -90,40 +94,49 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
     const int r = lane & 31, kh = lane >> 5;
     f32x16 acc = {};
     for (int k0 = 0; k0 < g.K; k0 += kKc) {
-        // A tile: 64 rows x 16 k (float4 per thread)
-        {
-            const int row = tid >> 2, q = tid & 3;
+        // A tile: 64 rows x kKc k (float4 per thread and step)
+#pragma unroll
+        for (int it = 0; it < kKc / 16; ++it) {
+            const int idx = tid + kGemmThreads * it;
+            const int row = idx / (kKc / 4), q = idx % (kKc / 4);
             const int gm = m0 + row, gk = k0 + 4 * q;
             f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (gm < g.M) {
+            if (gm < g.M && gk < g.K) {
                 if (gk < g.Ksplit) v = *(const f32x4_t*)(A + (long)gm * g.lda + gk);
                 else v = *(const f32x4_t*)(A2 + (long)gm * g.lda2 + (gk - g.Ksplit));
             }
             float* d = As + row * (kKc + 1) + 4 * q;
             d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
         }
-        // B tile: 16 k x 64 n
-        if (!g.b_trans) {
-            const int kk = tid >> 4, q = tid & 15;
-            const int gn = n0 + 4 * q;
-            f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (gn < g.N) v = *(const f32x4_t*)(B + (long)(k0 + kk) * g.ldb + gn);
-            *(f32x4_t*)(Bs + kk * 64 + 4 * q) = v;
-        } else {
-            const int nn = tid >> 2, q = tid & 3;
-            const int gn = n0 + nn;
-            f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (gn < g.N) v = *(const f32x4_t*)(B + (long)gn * g.ldb + k0 + 4 * q);
-            Bs[(4 * q + 0) * 64 + nn] = v[0];
-            Bs[(4 * q + 1) * 64 + nn] = v[1];
-            Bs[(4 * q + 2) * 64 + nn] = v[2];
-            Bs[(4 * q + 3) * 64 + nn] = v[3];
+        // B tile: kKc k x 64 n
+#pragma unroll
+        for (int it = 0; it < kKc / 16; ++it) {
+            const int idx = tid + kGemmThreads * it;
+            if (!g.b_trans) {
+                const int kk = idx >> 4, q = idx & 15;
+                const int gn = n0 + 4 * q;
+                f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (gn < g.N && k0 + kk < g.K) v = *(const f32x4_t*)(B + (long)(k0 + kk) * g.ldb + gn);
+                *(f32x4_t*)(Bs + kk * 64 + 4 * q) = v;
+            } else {
+                const int nn = idx / (kKc / 4), q = idx % (kKc / 4);
+                const int gn = n0 + nn;
+                f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
+                if (gn < g.N && k0 + 4 * q < g.K) v = *(const f32x4_t*)(B + (long)gn * g.ldb + k0 + 4 * q);
+                Bs[(4 * q + 0) * 64 + nn] = v[0];
+                Bs[(4 * q + 1) * 64 + nn] = v[1];
+                Bs[(4 * q + 2) * 64 + nn] = v[2];
+                Bs[(4 * q + 3) * 64 + nn] = v[3];
+            }
         }
         __syncthreads();
         const float* pa = As + (32 * wm + r) * (kKc + 1) + 8 * kh;
         const float* pb = Bs + (8 * kh) * 64 + 32 * wn + r;
 #pragma unroll
-        for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], pb[s * 64], acc, 0, 0, 0);
+        for (int g16 = 0; g16 < kKc / 16; ++g16)
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[16 * g16 + s], pb[(16 * g16 + s) * 64], acc, 0, 0, 0);
         __syncthreads();
     }
     const int n = n0 + 32 * wn + r;
