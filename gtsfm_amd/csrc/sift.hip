@@ -153,11 +153,14 @@ constexpr int kBlurTX = 64;
 #ifndef GTSFM_BLUR_WIDE_R
 #define GTSFM_BLUR_WIDE_R 9
 #endif
+#ifndef GTSFM_BLUR_U8_TY
+#define GTSFM_BLUR_U8_TY 96
+#endif
 #ifndef GTSFM_BLUR_WIDE_TY
 #define GTSFM_BLUR_WIDE_TY 96
 #endif
 __host__ __device__ constexpr int blur_ty(int r, bool u8) {
-    return u8 ? 96 : (r >= GTSFM_BLUR_WIDE_R ? GTSFM_BLUR_WIDE_TY : 64);
+    return u8 ? GTSFM_BLUR_U8_TY : (r >= GTSFM_BLUR_WIDE_R ? GTSFM_BLUR_WIDE_TY : 64);
 }
 __host__ __device__ constexpr int blur_tyt(int r, bool u8) { return blur_ty(r, u8) == 64 ? 4 : 8; }
 constexpr int kBlurRowOut = 8, kBlurRowThr = kBlurTX / kBlurRowOut;  // row pass: outputs per thread, threads per row
