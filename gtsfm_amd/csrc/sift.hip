@@ -528,7 +528,10 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 // thousand): they are queued in LDS and their 3x3 blocks gathered after the sweep, all lanes at once. Each pixel's
 // levels 1..4 are read once (plus 2 halo rows per strip and 2 halo lanes per wave): 16 B per pixel instead of all six
 // levels' 24.
-constexpr int kExWaves = 4, kExOut = 62, kExStrip = 64;
+#ifndef GTSFM_EX_STRIP
+#define GTSFM_EX_STRIP 64
+#endif
+constexpr int kExWaves = 4, kExOut = 62, kExStrip = GTSFM_EX_STRIP;
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
