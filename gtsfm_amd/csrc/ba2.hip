@@ -14,7 +14,12 @@
 //      builds the 12 x 12 reduced camera system: every lane adds its tracks' Schur contributions into a private LDS
 //      column, a 64-way reduction sums them, lane 0 solves it (Cholesky), and a second pass back-substitutes the
 //      points and evaluates the linearized and nonlinear costs of the step;
-//   4. filter_landmarks(reproj_thresh): tracks whose two reprojections are in front and within the threshold.
+//   4. filter_landmarks(reproj_thresh): tracks whose two reprojections are in front and within the threshold; an
+//      infinite reproj_thresh (the reference's reproj_error_thresh None) keeps every triangulated track.
+// Calibration is held fixed: the reference also optimises one Cal3Bundler (f, k1, k2) variable per camera under a
+// 1e-5 prior (GeneralSFMFactor2Cal3Bundler + PriorFactorCal3Bundler, bundle_adjustment.py:106-136,180-200). Holding
+// K at its prior value with k1 = k2 = 0 is the limit of that prior; the host refuses non-zero k1 / k2
+// (geometry.calibration_params), so the approximation is the prior's 1e-5 freedom in f only.
 // Outputs per pair: status (0 BA ok, 1 no track triangulated, 2 no track valid, 3 not run: verification failed or
 // fewer than min_inliers verified rows -- the reference's guard at :312), R / unit t (the verifier's for statuses 1-3),
 // the post-BA mask over the putatives (the pre-BA mask when not run), its count and the LM iterations.
@@ -574,7 +579,7 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
     double lambda = 1e-5;
     int iters = 0;
     if (err > 0.0) {
-        for (int outer = 0; outer < 1000; ++outer) {
+        for (;;) {  // ends: every outer step either accepts (iters <= max_iters) or leaves err unchanged (dec = 0)
             const double cur = err;
             double xi0[6];
             pose_log(X[0], xi0);
@@ -770,7 +775,9 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
         bool good = false;
         if (j < m) {
             good = true;
-            for (int c = 0; c < 2 && good; ++c) {
+            // reproj_error_thresh None (an infinite threshold): no filter at all, every track valid
+            // (bundle_adjustment.py:346-355), without the cheirality test of filter_landmarks
+            for (int c = 0; c < 2 && good && isfinite(a.reproj_thresh); ++c) {
                 double pc[3], pr[2];
                 if (!project(X[c], c ? K2 : K1, P + 3 * j, pc, pr)) { good = false; break; }
                 const double dx = pr[0] - UV[4 * j + 2 * c], dy = pr[1] - UV[4 * j + 2 * c + 1];

@@ -5,9 +5,9 @@ The reference fans the front-end out as Dask tasks, one per image and one per pa
 every pair task. Here each rank owns a fixed share instead:
 
 - extraction: image i -> rank i mod world (rank-local order i // world);
-- exchange: ONE all-gather of the fixed-size per-rank feature blocks (descriptors, keypoint xy, counts), padded to
-  `n_per = ceil(n / world)` images per rank, so the gathered tensor is rank-major: image i sits in global slot
-  `(i mod world) * n_per + i // world`;
+- exchange: ONE all-gather of the fixed-size per-rank feature block (descriptors, keypoint xy, counts packed into one
+  byte buffer), padded to `n_per = ceil(n / world)` images per rank, so the gathered tensors are rank-major: image i
+  sits in global slot `(i mod world) * n_per + i // world`;
 - matching + verification: the lexicographic (i1, i2) pair list cut into `world` contiguous blocks (rank r owns
   pairs [r * per, min((r + 1) * per, P)), per = ceil(P / world)). Consecutive pairs of a block share i1, so its
   descriptors stay in L2, and every pair keeps its global index, which keys the RANSAC sampler: a pair's result
@@ -54,16 +54,18 @@ def rank_pairs(pairs: np.ndarray, world: int, rank: int) -> np.ndarray:
 def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
                        group: Optional[torch.distributed.ProcessGroup] = None,
                        wire: Optional[Sequence[Optional[torch.dtype]]] = None) -> Tuple[torch.Tensor, ...]:
-    """Pads each rank's (n_local, ...) feature tensors to n_per rows and all-gathers them rank-major.
+    """Pads each rank's (n_local, ...) feature tensors to n_per rows and all-gathers them rank-major, in ONE
+    collective: the tensors are packed byte-wise into a single per-rank block (each field 16-byte aligned), gathered
+    with one all_gather_into_tensor, and unpacked as views of the gathered buffer.
 
-    One collective per tensor. wire[i] (optional) is the dtype tensor i travels in; it is cast back afterwards, so
-    the caller must only name a lossless one: SIFT descriptors are integers in [0, 255], so u8 carries them exactly
-    (2048 x 128 B per image instead of 4x that in f32). With world == 1 the inputs are returned unchanged.
+    wire[i] (optional) is the dtype tensor i travels in; it is cast back afterwards, so the caller must only name a
+    lossless one: SIFT descriptors are integers in [0, 255], so u8 carries them exactly (2048 x 128 B per image
+    instead of 4x that in f32). With world == 1 the inputs are returned unchanged.
     """
     world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
     if world == 1:
         return tuple(tensors)
-    out = []
+    fields, layout, off = [], [], 0
     for i, t in enumerate(tensors):
         dtype = t.dtype
         if wire is not None and wire[i] is not None:
@@ -73,10 +75,22 @@ def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
             raise ValueError(f"rank holds {t.shape[0]} images, more than n_per={n_per}")
         if pad:
             t = torch.cat([t, t.new_zeros((pad,) + tuple(t.shape[1:]))])
-        t = t.contiguous()
-        g = torch.empty((world * n_per,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        torch.distributed.all_gather_into_tensor(g, t, group=group)
-        out.append(g if g.dtype == dtype else g.to(dtype))
+        raw = t.contiguous().view(-1).view(torch.uint8)
+        nbytes = raw.numel()
+        layout.append((off, nbytes, t.dtype, tuple(t.shape), dtype))
+        fields.append(raw)
+        off += -(-nbytes // 16) * 16
+    dev = tensors[0].device
+    block = torch.zeros(off, dtype=torch.uint8, device=dev)
+    for raw, (o, nb, _, _, _) in zip(fields, layout):
+        block[o: o + nb] = raw
+    g = torch.empty(world * off, dtype=torch.uint8, device=dev)
+    torch.distributed.all_gather_into_tensor(g, block, group=group)
+    g = g.view(world, off)
+    out = []
+    for o, nb, wdt, shape, dtype in layout:
+        f = g[:, o: o + nb].contiguous().view(wdt).view((world * shape[0],) + shape[1:])
+        out.append(f if f.dtype == dtype else f.to(dtype))
     return tuple(out)
 
 

@@ -78,6 +78,7 @@ def generate_two_view_report(inlier_ratio_est_model: float, v_corr_idxs: np.ndar
 
 
 BA_PAIR_CHUNK = 8192
+GTSAM_LM_DEFAULT_MAX_ITERS = 100  # gtsam.LevenbergMarquardtParams().maxIterations
 
 
 class TwoViewEstimator:
@@ -107,8 +108,11 @@ class TwoViewEstimator:
         # (bundle_adjustment.py:396-419)
         thr = self._ba_reproj_error_thresholds[-1] if self._ba_reproj_error_thresholds else None
         min_inl = self.processor._min_num_inliers_est_model if self.processor is not None else 0
-        return (min_inl, int(self._bundle_adjust_2view_maxiters or 0) or 1000000,
-                1e300 if thr is None else float(thr), 1e300 if tri is None or math.isinf(tri) else float(tri))
+        # setMaxIterations only when maxiters is truthy (bundle_adjustment.py:273-274): else GTSAM's default of 100
+        max_iters = int(self._bundle_adjust_2view_maxiters or 0) or GTSAM_LM_DEFAULT_MAX_ITERS
+        # reproj_error_thresh None: no landmark filter (bundle_adjustment.py:346-355) -> an infinite threshold
+        return (min_inl, max_iters, math.inf if thr is None else float(thr),
+                1e300 if tri is None or math.isinf(tri) else float(tri))
 
     def bundle_adjust_batch(self, keypoints_list: Sequence[Keypoints],
                             jobs: Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]], camera_intrinsics: Sequence

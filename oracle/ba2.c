@@ -648,7 +648,8 @@ int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, co
     int n_valid = 0;
     for (int j = 0; j < m; ++j) {
         int good = 1;
-        for (int c = 0; c < 2 && good; ++c) {
+        /* reproj_error_thresh None (infinite): no filter, every track valid (bundle_adjustment.py:346-355) */
+        for (int c = 0; c < 2 && good && isfinite(reproj_thresh); ++c) {
             double pc[3], pr[2];
             const double* uv = c ? u2 + 2 * j : u1 + 2 * j;
             if (!project(&X[c], c ? K2 : K1, P + 3 * j, pc, pr)) { good = 0; break; }

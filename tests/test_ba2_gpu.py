@@ -98,3 +98,29 @@ def test_ba2_batch_vs_oracle(oracle_mod):
     assert ba2_scenes.angle_deg(R5, s["R"]) <= 1.0 and ba2_scenes.dir_deg(t5, s["t"]) <= 1.0
     o_st, o_R, o_t, o_valid, o_it, _ = oracle_mod.ba2(s["x1"], s["x2"], s["K"], s["K"], R0[2], t0[2])
     assert o_st == 0 and o_valid.all() and ba2_scenes.angle_deg(R5, o_R) < 1e-4
+
+
+def test_ba2_no_reprojection_threshold_vs_oracle(oracle_mod):
+    """ba_reproj_error_thresholds=[None] (an infinite threshold on the ABI): every triangulated track is valid, as
+    the reference's run_ba_stage_with_filtering without filter_landmarks (bundle_adjustment.py:346-355)."""
+    from gtsfm_amd import device, native
+
+    native.require_gpu()
+    rng = np.random.default_rng(22)
+    s = ba2_scenes.make_pair(rng, 400, noise_px=0.25, n_out=50, init_err_deg=0.4)
+    n = len(s["x1"])
+    dev = torch.device("cuda")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    kp = np.stack([s["x1"], s["x2"]]).astype(np.float32)
+    idx = np.stack([np.arange(n), np.arange(n)], 1)[None].astype(np.int32)
+    res = device.bundle_adjust_2view(t(kp), t(np.stack([s["K"], s["K"]])), t(np.array([[0, 1]], np.int32)), t(idx),
+                                     t(np.array([n], np.int32)),
+                                     _Verified(t(np.ones((1, n), np.uint8)), t(s["R0"][None]), t(s["t0"][None]),
+                                               t(np.zeros(1, np.int32))),
+                                     min_inliers=0, reproj_thresh=float("inf"), tri_thresh=float("inf"))
+    o_st, o_R, o_t, o_valid, o_it, _ = oracle_mod.ba2(kp[0].astype(np.float64), kp[1].astype(np.float64), s["K"],
+                                                      s["K"], s["R0"], s["t0"], reproj_thresh=np.inf,
+                                                      tri_thresh=np.inf)
+    assert o_st == 0 and int(res.ba_status[0]) == 0 and int(res.iters[0]) == o_it
+    np.testing.assert_array_equal(res.mask[0].cpu().numpy().astype(bool), o_valid.astype(bool))
+    assert ba2_scenes.angle_deg(res.R[0].cpu().numpy(), o_R) < 1e-4

@@ -1,10 +1,10 @@
-"""Multi-rank launch path on CPU (gloo): gtsfm_amd/launch.py and the AllPairsFrontEnd host logic at world size 2.
+"""Multi-rank launch path on CPU (gloo): gtsfm_amd/launch.py and the AllPairsFrontEnd host logic at world sizes 2 and 3.
 
 - spawn_ranks starts fresh ranks that each see WORLD_SIZE 2 and join one process group (the path `bench.py --gpus N`
   takes before anything touches a GPU); bench.py's own launch is probed the same way;
 - a failing rank ends the job with its status instead of leaving its peer blocked;
-- AllPairsFrontEnd, sharded over 2 gloo ranks with the oracle standing in for the HIP kernels, reproduces the
-  single-rank run pair for pair (R, t, inlier counts, ISP verdicts, verified rows, keypoints): the all-gather is the
+- AllPairsFrontEnd, sharded over 2 and 3 gloo ranks (7 images over 3: a ragged split) with the oracle standing in
+  for the HIP kernels, reproduces the single-rank run pair for pair (R, t, inlier counts, ISP verdicts, verified rows, keypoints): the all-gather is the
   only exchange and every pair keeps its global RANSAC key.
 """
 import json
@@ -13,6 +13,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 import torch
 
 from gtsfm_amd import launch
@@ -52,9 +53,9 @@ def _load(path):
         return {k: z[k] for k in z.files}
 
 
-def test_frontend_gloo_world2_equals_single_rank(tmp_path):
-    n_img = 5
-    rc = launch.spawn_ranks(2, RANK_SCRIPT, ["frontend", str(tmp_path), str(n_img)])
+@pytest.mark.parametrize("world,n_img", [(2, 5), (3, 7)])  # 7 over 3 ranks: ragged (3, 2, 2 images)
+def test_frontend_gloo_sharded_equals_single_rank(tmp_path, world, n_img):
+    rc = launch.spawn_ranks(world, RANK_SCRIPT, ["frontend", str(tmp_path), str(n_img)])
     assert rc == 0
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import frontend_rank  # noqa: E402
@@ -63,7 +64,7 @@ def test_frontend_gloo_world2_equals_single_rank(tmp_path):
 
     torch.set_num_threads(1)
     _, ref = frontend_rank.run_frontend(n_img, launch.RankInfo(0, 1, 0, torch.device("cpu")))
-    parts = [_load(tmp_path / f"results_2_{r}.npz") for r in range(2)]
+    parts = [_load(tmp_path / f"results_{world}_{r}.npz") for r in range(world)]
     got_pairs = np.concatenate([p["pairs"] for p in parts])
     assert np.array_equal(got_pairs, ref.pairs) and len(ref.pairs) == n_img * (n_img - 1) // 2
     for key in ("status", "n_inliers", "n_matches", "isp_ok"):
@@ -78,7 +79,7 @@ def test_frontend_gloo_world2_equals_single_rank(tmp_path):
             q += 1
     # keypoints: each rank holds its own images, identical to the single-rank extraction of the same image
     for r, part in enumerate(parts):
-        for j, i in enumerate(sharding.local_images(n_img, 2, r)):
+        for j, i in enumerate(sharding.local_images(n_img, world, r)):
             n = part["kp_count"][j]
             assert n == ref.kp_count[i]
             assert np.array_equal(part["kp_xy"][j, :n], ref.kp_xy[i, :n])

@@ -10,7 +10,7 @@ from tests.conftest import REPO
 def _declared_functions():
     text = open(os.path.join(REPO, "include", "gtsfm_hip.h")).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(gtsfm_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(gtsfm_[A-Za-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_entry_points():

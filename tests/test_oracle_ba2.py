@@ -40,3 +40,31 @@ def test_nothing_triangulates(oracle_mod):
         assert valid.sum() >= 1
     else:
         assert st in (1, 2) and not valid.any() and np.allclose(R, s["R"])
+
+
+def test_no_reprojection_threshold_keeps_every_track(oracle_mod):
+    """ba_reproj_error_thresholds=[None]: run_ba_stage_with_filtering skips filter_landmarks and marks every track
+    valid (bundle_adjustment.py:346-355); the 0.5 px filter drops the planted outliers."""
+    rng = np.random.default_rng(8)
+    s = ba2_scenes.make_pair(rng, 300, noise_px=0.2, n_out=40, init_err_deg=0.3)
+    st, R, t, valid, it, err = oracle_mod.ba2(s["x1"], s["x2"], s["K"], s["K"], s["R0"], s["t0"],
+                                              reproj_thresh=np.inf, tri_thresh=np.inf)
+    st5, _, _, valid5, it5, _ = oracle_mod.ba2(s["x1"], s["x2"], s["K"], s["K"], s["R0"], s["t0"],
+                                               reproj_thresh=0.5, tri_thresh=np.inf)
+    assert st == 0 and st5 == 0 and it == it5
+    # with no filter, every triangulated correspondence stays (the triangulation keeps the ones in front)
+    assert valid.sum() > valid5.sum() and np.all(valid5 <= valid)
+
+
+def test_falsy_maxiters_maps_to_gtsam_default():
+    """bundle_adjust_2view_maxiters None / 0: the reference does not call setMaxIterations
+    (bundle_adjustment.py:273-274), so GTSAM's LevenbergMarquardtParams default of 100 applies."""
+    from gtsfm_amd.frontend.inlier_support_processor import InlierSupportProcessor
+    from gtsfm_amd.two_view_estimator import TwoViewEstimator
+
+    isp = InlierSupportProcessor(min_num_inliers_est_model=15, min_inlier_ratio_est_model=0.1)
+    for falsy in (None, 0):
+        tve = TwoViewEstimator(None, isp, True, 4.0, bundle_adjust_2view_maxiters=falsy,
+                               ba_reproj_error_thresholds=[None])
+        _, max_iters, thr, _ = tve._ba_params()
+        assert max_iters == 100 and np.isinf(thr)
