@@ -14,9 +14,12 @@ steps from pinned host images to host results (SURVEY.md §8(d)'s PCIe-inclusive
 as `value_host_to_host`.
 
 Workloads:
-  --config c2 (default; configs[1] of BASELINE.json): 100 rendered 1920x1080 images, all 4950 pairs, at N=1. For
-      N GPUs the scene grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work constant:
-      "scaling": "weak").
+  --config c2 (default; configs[1] of BASELINE.json): 100 rendered 1920x1080 images, all 4950 pairs. N GPUs share
+      that same scene (images round-robin, pairs in N blocks: "scaling": "strong").
+  --config c2-weak: the scene grows to the smallest n with n(n-1)/2 >= 4950*N images (per-GPU pair work constant,
+      per-GPU extraction falls as 100/sqrt(N): not a constant-work curve, kept for comparison).
+  --config c1 (configs[0]): the reference's 12 Lund Door images (1296x1936, tests/golden/lund_door), all 66 pairs,
+      sift_front_end.yaml's 5000 keypoints; cpu_baseline is the oracle on the whole workload, nothing extrapolated.
   --config c4 (configs[3]): 1000 rendered 1080p images, all 499,500 pairs, split over the N ranks ("strong").
   --config c3-match: configs[2]'s matcher on SURVEY.md §8(d)'s synthetic descriptors -- 200 images x 4096
       SuperPoint-like 256-D unit vectors, all 19900 pairs through the fp16 MFMA shortlist + certified exact re-rank.
@@ -26,7 +29,7 @@ Workloads:
       of 32 rendered images (configs[4]'s 2000 images x 8 GPUs is ~2M SuperGlue pairs; --images sets the slice).
 Pairs are cut into one contiguous block per rank, images dealt round-robin for extraction.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c4|c3-match|c3|c5] [--images n]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2-weak|c4|c3-match|c3|c5] [--images n]
                     [--no-cpu-baseline]
 
 --gpus N > 1 without a launcher starts N fresh rank processes first (gtsfm_amd/launch.py), before anything touches
@@ -79,45 +82,65 @@ def pmc_traffic():
     return float(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
 
 
-def cpu_baseline(images, K: np.ndarray, n_img: int, kpts: int, threads: int = 16, n_sift: int = 16,
-                 n_pairs: int = 64) -> dict:
+def cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, threads: int = 16, n_sift: int = 16,
+                 n_pairs: int = 120) -> dict:
     """Oracle restatement (oracle/*.c through ctypes, which drops the GIL) timed on `threads` host threads -- the
-    box's CPU share for one GPU -- over a bounded sample: SIFT of n_sift images, then match + verify of n_pairs pairs
-    among them, each stage wall-clocked across the thread pool and scaled to n_img images / all their pairs."""
+    box's CPU share for one GPU -- over a bounded sample: SIFT of n_sift images spread evenly over the scene's n_img
+    (so the pairs among them span the same range of baselines as all pairs of the scene), then match + verify of up to
+    n_pairs of the pairs among them (a seeded choice when there are more), each stage wall-clocked across the pool and
+    scaled to n_img images / all their pairs. When the sample is the whole workload (C1) nothing is scaled.
+    `images` holds the sampled images' pixels: (n_sift, H, W, 3) in the order of sample_images(n_img, n_sift)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import oracle
 
-    n_sift = min(n_sift, images.shape[0])
-    imgs = np.asarray(images[:n_sift])
+    sample = sample_images(n_img, n_sift)
+    imgs = np.asarray(images)
+    assert imgs.shape[0] == len(sample)
     rng = np.random.default_rng(0)
     oracle.ransac_E(rng.normal(size=(8, 2)), rng.normal(size=(8, 2)), 1e-3)  # one-time solver tables, untimed
-    pairs = [(i1, i2) for i1 in range(n_sift) for i2 in range(i1 + 1, n_sift)][:n_pairs]
+    pairs = [(a, b) for a in range(len(sample)) for b in range(a + 1, len(sample))]
+    if len(pairs) > n_pairs:
+        pairs = [pairs[i] for i in sorted(rng.choice(len(pairs), n_pairs, replace=False))]
+    K = np.asarray(intrinsics, dtype=np.float64)
 
     def sift_one(im):
         return oracle.sift(oracle.rgb_to_gray(im), kpts)
 
     def pair_one(p):
         f1, f2 = feats[p[0]], feats[p[1]]
+        k1, k2 = K[sample[p[0]]], K[sample[p[1]]]
         m = oracle.twoway_match(f1[1], f2[1], RATIO)
         if len(m) >= 6:
-            x1 = ((f1[0][m[:, 0], :2] - K[:2, 2]) / K[0, 0]).astype(np.float64)
-            x2 = ((f2[0][m[:, 1], :2] - K[:2, 2]) / K[0, 0]).astype(np.float64)
-            oracle.ransac_E(x1, x2, THRESH_PX / K[0, 0])
+            x1 = ((f1[0][m[:, 0], :2] - k1[1:3]) / k1[0]).astype(np.float64)
+            x2 = ((f2[0][m[:, 1], :2] - k2[1:3]) / k2[0]).astype(np.float64)
+            oracle.ransac_E(x1, x2, THRESH_PX / max(k1[0], k2[0]))
 
     with ThreadPoolExecutor(threads) as pool:
         t0 = time.time()
         feats = list(pool.map(sift_one, imgs))
-        t_sift = (time.time() - t0) / n_sift
+        t_sift_wall = time.time() - t0
         t0 = time.time()
         list(pool.map(pair_one, pairs))
-        t_pair = (time.time() - t0) / len(pairs)
+        t_pair_wall = time.time() - t0
     P = n_img * (n_img - 1) // 2
-    total = n_img * t_sift + P * t_pair
-    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port",
-            "sample": f"oracle (oracle/*.c, {threads} threads): SIFT of {n_sift} of the {n_img} images "
-                      f"({t_sift * 1e3:.0f} ms/img wall) + match+verify of {len(pairs)} pairs among them "
-                      f"({t_pair * 1e3:.0f} ms/pair wall), scaled to {n_img} images / {P} pairs"}
+    whole = len(sample) == n_img and len(pairs) == P
+    total = t_sift_wall + t_pair_wall if whole else (n_img * t_sift_wall / len(sample) + P * t_pair_wall / len(pairs))
+    if whole:
+        what = (f"oracle (oracle/*.c, {threads} threads): the whole workload, SIFT of all {n_img} images "
+                f"({t_sift_wall:.2f} s wall) + match+verify of all {P} pairs ({t_pair_wall:.2f} s wall), no scaling")
+    else:
+        what = (f"oracle (oracle/*.c, {threads} threads): SIFT of {len(sample)} of the {n_img} images, evenly spaced "
+                f"({t_sift_wall / len(sample) * 1e3:.0f} ms/img wall) + match+verify of {len(pairs)} pairs among them "
+                f"({t_pair_wall / len(pairs) * 1e3:.0f} ms/pair wall), scaled to {n_img} images / {P} pairs")
+    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port", "sample": what}
+
+
+def sample_images(n_img: int, n_sift: int) -> np.ndarray:
+    """n_sift image indices spread evenly over [0, n_img) (all of them when n_img <= n_sift)."""
+    if n_img <= n_sift:
+        return np.arange(n_img)
+    return np.unique(np.round(np.linspace(0, n_img - 1, n_sift)).astype(np.int64))
 
 
 def c3_descriptors(n_img: int, k: int, d: int, dev) -> torch.Tensor:
@@ -365,25 +388,55 @@ def sift_bytes_per_image(H: int, W: int, kpts: int) -> float:
     return 84.0 * (4.0 * H * W * 4.0 / 3.0) + H * W + kpts * (128 * 4 + 16)
 
 
+def lund_door_c1():
+    """configs[0] (C1): the reference's 12 Lund Door images (tests/data/set1_lund_door, committed byte for byte under
+    tests/golden/lund_door/ with their data.mat intrinsics in gt.json), decoded with PIL as the reference loader
+    does. 1296 x 1936: max_resolution 1296, the reference CI benchmark's setting, needs no resize."""
+    from PIL import Image as PILImage
+
+    root = os.path.join(REPO, "tests", "golden", "lund_door")
+    gt = json.load(open(os.path.join(root, "gt.json")))
+    imgs = np.stack([np.asarray(PILImage.open(os.path.join(root, n)).convert("RGB")) for n in gt["images"]])
+    intr = np.tile(np.asarray(gt["fx_u0_v0"], dtype=np.float64), (len(imgs), 1))
+    return torch.from_numpy(imgs), intr
+
+
 def main_frontend(args, info, config: str):
-    """configs[1] (C2, weak scaling) / configs[3] (C4, strong scaling): the SIFT all-pairs front-end."""
+    """configs[0] (C1: Lund Door, 12 images, 5000 kpts), configs[1] (C2: 100 rendered 1080p images; N > 1 GPUs share
+    the same scene, "strong"; c2-weak grows the scene instead) and configs[3] (C4: 1000 images, "strong"): the SIFT
+    all-pairs front-end."""
     from gtsfm_amd import native, synthetic
     from gtsfm_amd.frontend import sharding
     from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig
 
     rank, world, dev = info.rank, info.world, info.device
     native.lib()
-    if config == "c4":
-        n_img, scaling = args.images or 1000, "strong"
+    if config == "c1":
+        all_imgs, intrinsics = lund_door_c1()
+        n_img, scaling = len(all_imgs), "strong"
+        H, W = all_imgs.shape[1], all_imgs.shape[2]
+        kpts = args.kpts if args.kpts != 2048 else 5000  # sift_front_end.yaml max_keypoints
+        mine = sharding.local_images(n_img, world, rank)
+        host_images = all_imgs[torch.from_numpy(mine)].contiguous().pin_memory()
+        baseline_images = all_imgs.numpy()[sample_images(n_img, 16)]
     else:
-        n_img, scaling = args.images or images_for(world), "weak"
-    H, W, kpts = args.height, args.width, args.kpts
-    mine = sharding.local_images(n_img, world, rank)
-    # every rank renders (seeded, identical cameras) only the images it extracts; rendering is data generation
-    scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine)
-    host_images = scene.images.cpu().pin_memory()
-    del scene.images
-    torch.cuda.empty_cache()
+        if config == "c4":
+            n_img, scaling = args.images or 1000, "strong"
+        elif config == "c2-weak":
+            n_img, scaling = args.images or images_for(world), "weak"
+        else:  # c2: the 100-image scene of configs[1] at every N (the pairs of the same scene split over the ranks)
+            n_img, scaling = args.images or 100, "strong"
+        H, W, kpts = args.height, args.width, args.kpts
+        mine = sharding.local_images(n_img, world, rank)
+        # every rank renders (seeded, identical cameras) only the images it extracts; rendering is data generation
+        scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine)
+        host_images = scene.images.cpu().pin_memory()
+        intrinsics = scene.intrinsics
+        del scene.images
+        torch.cuda.empty_cache()
+        baseline_images = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            baseline_images = host_images.numpy()[sample_images(n_img, 16)]
     cfg = FrontEndConfig(kpts=kpts, ratio=RATIO, thresh_px=THRESH_PX, min_inliers=MIN_INLIERS,
                          min_inlier_ratio=MIN_INLIER_RATIO)
     if args.extract_chunk:
@@ -395,7 +448,7 @@ def main_frontend(args, info, config: str):
     if args.pair_chunk:
         cfg.pair_chunk = args.pair_chunk
     cfg.bundle_adjust = args.ba
-    fe = AllPairsFrontEnd(host_images, scene.intrinsics, n_img, rank, world, dev, cfg)
+    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg)
 
     for _ in range(args.warmup):
         res = fe.step()
@@ -487,7 +540,7 @@ def main_frontend(args, info, config: str):
         roof["traffic_note"] = ("L2-miss bytes, Infinity-Cache hits included: the A operand (image i2) of each pair is "
                                 "re-read past the 4 MiB XCD L2, from a %.0f MB operand set that fits the 256 MiB "
                                 "Infinity Cache" % (2 * n_launch_img * kpad * 144 * 2 / 1e6))
-    wl = "C4" if config == "c4" else "C2"
+    wl = {"c1": "C1", "c4": "C4"}.get(config, "C2")
     out = {
         "metric": "verified image-pairs/sec (all-pairs front-end), N images @ 2048 kpts/img",
         "value": round(value, 2),
@@ -500,8 +553,10 @@ def main_frontend(args, info, config: str):
         "scaling": scaling,
         "vs_baseline": None,
         "dtype": "u8 image / fp32 pyramid / fp16-MFMA exact-int distances / fp64 RANSAC solver",
-        "data": "synthetic (rendered textured room, seeds 0/1/2)",
-        "config": {"workload": f"{wl}: {n_img} synthetic {W}x{H} images, all {fe.total_pairs} pairs, SIFT {kpts} "
+        "data": ("the reference's Lund Door images (tests/data/set1_lund_door)" if config == "c1" else
+                 "synthetic (rendered textured room, seeds 0/1/2)"),
+        "config": {"workload": f"{wl}: {n_img} {'Lund Door' if config == 'c1' else 'synthetic'} {W}x{H} images, "
+                               f"all {fe.total_pairs} pairs, SIFT {kpts} "
                                f"kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px"
                                + (" + two-view BA" if args.ba else "") + " + inlier support",
                    "images": n_img, "pairs": fe.total_pairs, "kpts": kpts, "parallelism": f"pair blocks x{world}",
@@ -515,7 +570,7 @@ def main_frontend(args, info, config: str):
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(host_images, scene.K, n_img, kpts)
+        out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts)
     if rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -536,7 +591,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba", action="store_true",
                     help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
-    ap.add_argument("--config", default="c2", choices=["c2", "c4", "c3-match", "c3", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2-weak", "c4", "c3-match", "c3", "c5"])
     ap.add_argument("--launch-probe", action="store_true",
                     help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")
     args = ap.parse_args()
