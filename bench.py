@@ -266,103 +266,6 @@ def timed_loop(step, steps: int, world: int, dev) -> float:
     return float(el.item())
 
 
-def _random_weight_nets(dev, superglue: bool):
-    """Seeded random SuperPoint (and SuperGlue) weights in the ABI's packed layout: the pretrained .pth files are not
-    available offline (tests/superpoint_weights.py builds state dicts of the reference architectures)."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    from superpoint_weights import superglue_state_dict, superpoint_state_dict
-
-    from gtsfm_amd.frontend.detector_descriptor.superpoint import pack_superpoint_weights
-
-    sp = torch.from_numpy(pack_superpoint_weights(superpoint_state_dict(0))).to(dev)
-    if not superglue:
-        return sp, None
-    from gtsfm_amd.frontend.matcher.superglue_matcher import pack_superglue_weights
-
-    return sp, torch.from_numpy(pack_superglue_weights(superglue_state_dict(0))).to(dev)
-
-
-def main_dl(args, world, rank, dev, config: str):
-    """configs[2] end to end (c3: SuperPoint 4096 kpts + F16_RERANK mutual NN + ratio 0.8 over all pairs) and a
-    per-GPU slice of configs[4] (c5: SuperPoint 2048 kpts + SuperGlue + 5-point RANSAC (MSAC) over all pairs of a
-    smaller scene). Rendered 1080p images resident in HBM, seeded random network weights."""
-    from gtsfm_amd import device as hip
-    from gtsfm_amd import native, synthetic
-    from gtsfm_amd.frontend import sharding
-
-    c5 = config == "c5"
-    n_img = args.images or (32 if c5 else 200)
-    k = args.kpts if args.kpts != 2048 or c5 else 4096
-    scene = synthetic.render_scene(n_img, args.height, args.width, device=str(dev))
-    mine_img = sharding.local_images(n_img, world, rank)
-    sp_w, sg_w = _random_weight_nets(dev, c5)
-    all_pairs = sharding.all_pairs(n_img)
-    mine = all_pairs[sharding.rank_pairs(all_pairs, world, rank)]
-    pairs = torch.from_numpy(mine.astype(np.int32)).to(dev)
-    imgs = scene.images[torch.from_numpy(np.asarray(mine_img)).to(dev)].contiguous() if world > 1 else scene.images
-    intr = torch.from_numpy(scene.intrinsics).to(dev)
-    hw = torch.tensor([[args.height, args.width]] * n_img, dtype=torch.int32, device=dev)
-    st = {}
-
-    def gather(x):
-        if world == 1:
-            return x
-        return sharding.allgather_features([x], sharding.images_per_rank(n_img, world))[0]
-
-    def step():
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-        ev[0].record()
-        f = hip.superpoint_extract(imgs, sp_w, k)
-        ev[1].record()
-        xy, sc, de, cn = (gather(t) for t in (f.xy, f.scores, f.desc, f.count))
-        if world > 1:  # rank-major rows -> image order
-            slot = torch.from_numpy(sharding.global_slots(n_img, world)).to(dev)
-            xy, sc, de, cn = xy[slot], sc[slot], de[slot], cn[slot]
-        if c5:
-            idx, cnt, _ = hip.superglue_match(xy.contiguous(), sc.contiguous(), de.contiguous(), cn.contiguous(), hw,
-                                              pairs, sg_w)
-            ev[2].record()
-            res = hip.ransac_essential(xy.contiguous(), intr, pairs, idx.contiguous(), cnt, THRESH_PX)
-            ev[3].record()
-            st["res"] = res
-        else:
-            idx, cnt = hip.match_pairs(de.contiguous(), cn.contiguous(), pairs, RATIO, native.GTSFM_MATCH_F16_RERANK)
-            ev[2].record()
-            ev[3].record()
-        st["ev"], st["cnt"] = ev, cnt
-
-    for _ in range(args.warmup):
-        step()
-    elapsed = timed_loop(step, args.steps, world, dev)
-    ev = st["ev"]
-    torch.cuda.synchronize()
-    stage = {"extract": ev[0].elapsed_time(ev[1]), "match": ev[1].elapsed_time(ev[2]),
-             "verify": ev[2].elapsed_time(ev[3])}
-    total_pairs = len(all_pairs)
-    out = {
-        "metric": ("verified image-pairs/sec (SuperPoint + SuperGlue + RANSAC, configs[4] per-GPU slice)" if c5 else
-                   "matched image-pairs/sec (SuperPoint + fp16 MFMA mutual-NN matcher, configs[2] end to end)"),
-        "value": round(total_pairs / (elapsed / args.steps), 2), "unit": "image-pairs/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-        "higher_is_better": True, "scaling": "weak" if world > 1 else "strong", "vs_baseline": None,
-        "dtype": ("fp32 MFMA convs / fp32 MFMA attention + Sinkhorn / fp64 RANSAC" if c5 else
-                  "fp32 MFMA convs / fp16 MFMA shortlist + fp32 exact re-rank"),
-        "data": "synthetic (rendered textured room), seeded random network weights",
-        "config": {"workload": (f"C5 slice: {n_img} 1080p images, all {total_pairs} pairs, SuperPoint {k} kpts, "
-                                f"SuperGlue 18 layers / 20 Sinkhorn iterations, 5-pt RANSAC {THRESH_PX}px" if c5 else
-                                f"C3: {n_img} 1080p images, SuperPoint {k} kpts, all {total_pairs} pairs, F16_RERANK "
-                                f"mutual NN + ratio {RATIO}"),
-                   "images": n_img, "pairs": total_pairs, "kpts": k, "parallelism": f"pair blocks x{world}",
-                   "world_size": world},
-        "stage_ms_last_step": {a: round(b, 3) for a, b in stage.items()},
-        "mean_matches": round(float(st["cnt"].float().mean().item()), 1),
-    }
-    if c5:
-        out["pairs_verified"] = int((st["res"].status == 0).sum().item())
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-
-
 def timed_steps(fe, steps: int, resident: bool, world: int, dev) -> float:
     """Seconds for `steps` steps: barrier + synchronize on both sides, max over ranks."""
     torch.cuda.synchronize()
@@ -401,16 +304,101 @@ def lund_door_c1():
     return torch.from_numpy(imgs), intr
 
 
+SP_FLOP_PER_PIXEL = 169600.0   # SuperPoint convs ~169,600 FLOP per input pixel (352 GF at 1080p)
+SG_FLOP_PER_PAIR_2048 = 254e9   # SuperGlue ~254 GFLOP per pair at K = 2048
+MFMA_F32_PEAK_TFLOPS = 157.3    # dense fp32 MFMA, MI355X_MICROARCH.md
+
+
+def superglue_flop(k1: np.ndarray, k2: np.ndarray) -> np.ndarray:
+    """SURVEY.md 8(d)'s per-pair count 18 * 2 * (20 K d^2 + 4 K^2 d) + 2 K^2 d at K1, K2 keypoints (d = 256), per side
+    summed: the projections / MLPs scale with each side's K, the attention and the score matrix with K1 K2."""
+    d = 256.0
+    lin = 18 * 2 * 20 * d * d * (k1 + k2) / 2.0
+    quad = 18 * 2 * 4 * d * k1 * k2 + 2 * d * k1 * k2
+    return lin + quad
+
+
+def deep_weights(dev, superglue: bool):
+    """Seeded random SuperPoint / SuperGlue weights in the ABI's packed layout (the pretrained .pth files are not
+    available offline; tests/superpoint_weights.py builds state dicts of the reference architectures). SuperPoint's
+    1x1 descriptor layer is the whitening of its seeded encoder's activations over the benchmark scene
+    (tests/golden/make_superpoint_whitening.py), so descriptors of the scene behave like trained ones (unrelated
+    keypoints near-orthogonal, repeated points similar); SuperGlue's final projection gain is 24 (see
+    superglue_state_dict), which gives ~1000 matches on adjacent views. Weights change what is matched, never how
+    much work a step does."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from superpoint_weights import superglue_state_dict, superpoint_state_dict
+
+    from gtsfm_amd.frontend.detector_descriptor.superpoint import pack_superpoint_weights
+
+    sd = superpoint_state_dict(0, whitened=True)
+    sp = torch.from_numpy(pack_superpoint_weights(sd)).to(dev)
+    if not superglue:
+        return sd, sp, None, None
+    from gtsfm_amd.frontend.matcher.superglue_matcher import pack_superglue_weights
+
+    sgd = superglue_state_dict(0, final_scale=24.0)
+    return sd, sp, sgd, torch.from_numpy(pack_superglue_weights(sgd)).to(dev)
+
+
+def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_sd, sg_sd, threads: int = 16,
+                      n_img_sample: int = 3) -> dict:
+    """CPU restatement of the deep front-end timed on `threads` host threads over a bounded sample, scaled to n_img
+    images / all their pairs: oracle/deep.py's SuperPoint (torch fp32 on the host, `threads` intra-op threads, as the
+    reference's torch modules run on a CPU) on n_img_sample images spread over the scene, then for every pair among
+    them the matcher (oracle/deep.py SuperGlue, or the oracle TwoWayMatcher in C on the float descriptors) and the
+    oracle 5-point RANSAC."""
+    from oracle import deep, oracle
+
+    sample = sample_images(n_img, n_img_sample)
+    imgs = np.asarray(images)
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    oracle.ransac_E(rng.normal(size=(8, 2)), rng.normal(size=(8, 2)), 1e-3)
+    t0 = time.time()
+    feats = [deep.superpoint(oracle.rgb_to_gray(im), sp_sd, max_keypoints=kpts) for im in imgs]
+    t_img = (time.time() - t0) / len(imgs)
+    pairs = [(a, b) for a in range(len(sample)) for b in range(a + 1, len(sample))]
+    K = np.asarray(intrinsics, dtype=np.float64)
+    t0 = time.time()
+    for a, b in pairs:
+        (k1, s1, d1), (k2, s2, d2) = feats[a], feats[b]
+        if sg_sd is not None:
+            hw = imgs[a].shape[:2]
+            m0, _ = deep.superglue(k1, k2, d1, d2, s1, s2, hw, hw, sg_sd)
+            v = m0 >= 0
+            m = np.stack([np.flatnonzero(v), m0[v]], 1)
+        else:
+            m = oracle.twoway_match(d1, d2, RATIO).reshape(-1, 2).astype(np.int64)
+        if len(m) >= 6:
+            f1, f2 = K[sample[a]], K[sample[b]]
+            x1 = (k1[m[:, 0]].astype(np.float64) - f1[1:3]) / f1[0]
+            x2 = (k2[m[:, 1]].astype(np.float64) - f2[1:3]) / f2[0]
+            oracle.ransac_E(x1, x2, THRESH_PX / max(f1[0], f2[0]))
+    t_pair = (time.time() - t0) / len(pairs)
+    P = n_img * (n_img - 1) // 2
+    total = n_img * t_img + P * t_pair
+    what = ("SuperGlue (oracle/deep.py)" if sg_sd is not None else "TwoWayMatcher (oracle/twoway.c)")
+    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port",
+            "sample": f"CPU restatement on {threads} threads: SuperPoint (oracle/deep.py, torch fp32) of "
+                      f"{len(sample)} of the {n_img} images ({t_img:.2f} s/img), {what} + oracle RANSAC on the "
+                      f"{len(pairs)} pairs among them ({t_pair:.2f} s/pair), scaled to {n_img} images / {P} pairs"}
+
+
 def main_frontend(args, info, config: str):
-    """configs[0] (C1: Lund Door, 12 images, 5000 kpts), configs[1] (C2: 100 rendered 1080p images; N > 1 GPUs share
-    the same scene, "strong"; c2-weak grows the scene instead) and configs[3] (C4: 1000 images, "strong"): the SIFT
-    all-pairs front-end."""
+    """The all-pairs front-end engine (gtsfm_amd/frontend/all_pairs.py) on one BASELINE config:
+    c1 (configs[0]: Lund Door, 12 images, 5000 SIFT kpts), c2 (configs[1]: 100 rendered 1080p images, 2048 SIFT kpts;
+    N > 1 GPUs share the same scene, "strong"; c2-weak grows the scene instead), c4 (configs[3]: 1000 images,
+    "strong"), c3 (configs[2]: 200 images, SuperPoint 4096 kpts + TwoWayMatcher F16_RERANK) and c5 (a slice of
+    configs[4]: 32 images, SuperPoint 2048 kpts + SuperGlue), each followed by 5-point RANSAC + inlier support."""
     from gtsfm_amd import native, synthetic
     from gtsfm_amd.frontend import sharding
-    from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig
+    from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig, HipSuperPointKernels
 
     rank, world, dev = info.rank, info.world, info.device
     native.lib()
+    deep = config in ("c3", "c5")
+    want_baseline = rank == 0 and world == 1 and not args.no_cpu_baseline
     if config == "c1":
         all_imgs, intrinsics = lund_door_c1()
         n_img, scaling = len(all_imgs), "strong"
@@ -424,9 +412,14 @@ def main_frontend(args, info, config: str):
             n_img, scaling = args.images or 1000, "strong"
         elif config == "c2-weak":
             n_img, scaling = args.images or images_for(world), "weak"
+        elif config == "c3":
+            n_img, scaling = args.images or 200, "strong"
+        elif config == "c5":
+            n_img, scaling = args.images or 32, "strong"
         else:  # c2: the 100-image scene of configs[1] at every N (the pairs of the same scene split over the ranks)
             n_img, scaling = args.images or 100, "strong"
-        H, W, kpts = args.height, args.width, args.kpts
+        H, W = args.height, args.width
+        kpts = args.kpts if not (config == "c3" and args.kpts == 2048) else 4096
         mine = sharding.local_images(n_img, world, rank)
         # every rank renders (seeded, identical cameras) only the images it extracts; rendering is data generation
         scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine)
@@ -435,10 +428,12 @@ def main_frontend(args, info, config: str):
         del scene.images
         torch.cuda.empty_cache()
         baseline_images = None
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            baseline_images = host_images.numpy()[sample_images(n_img, 16)]
+        if want_baseline:
+            baseline_images = host_images.numpy()[sample_images(n_img, 3 if deep else 16)]
     cfg = FrontEndConfig(kpts=kpts, ratio=RATIO, thresh_px=THRESH_PX, min_inliers=MIN_INLIERS,
                          min_inlier_ratio=MIN_INLIER_RATIO)
+    if deep:
+        cfg.extract_chunk, cfg.extract_first, cfg.resident_chunk = 8, 4, 16  # ~0.75 GB SuperPoint workspace / image
     if args.extract_chunk:
         cfg.extract_chunk = args.extract_chunk
     if args.extract_first:
@@ -448,7 +443,11 @@ def main_frontend(args, info, config: str):
     if args.pair_chunk:
         cfg.pair_chunk = args.pair_chunk
     cfg.bundle_adjust = args.ba
-    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg)
+    kernels = sp_sd = sg_sd = None
+    if deep:
+        sp_sd, sp_w, sg_sd, sg_w = deep_weights(dev, config == "c5")
+        kernels = HipSuperPointKernels(sp_w, "superglue" if config == "c5" else "twoway", sg_w)
+    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg, kernels=kernels)
 
     for _ in range(args.warmup):
         res = fe.step()
@@ -459,12 +458,12 @@ def main_frontend(args, info, config: str):
     ms_per_step = elapsed_res / args.steps * 1e3
     value = fe.total_pairs / (elapsed_res / args.steps)
 
-    # instrumented steps: per-phase HIP events on the compute / copy streams; the distance-GEMM kernel's own events
-    # through gtsfm_match_set_kernel_events (one pair chunk per launch at C2)
+    # instrumented steps: per-phase HIP events on the compute / copy streams; the matcher kernel's own events
+    # (the distance GEMM, or F16_RERANK's shortlist GEMM) through gtsfm_match_set_kernel_events
     lib = native.lib()
     stage_host, stage_res, kernel_ms = [], [], []
     fe.instrument = True
-    for _ in range(3):
+    for _ in range(3 if not deep else 2):
         res = fe.step(resident=False)
         torch.cuda.synchronize()
         stage_host.append(fe.stage_ms())
@@ -494,53 +493,96 @@ def main_frontend(args, info, config: str):
         t = torch.from_numpy(kc).to(dev)
         torch.distributed.all_reduce(t)
         kc = t.cpu().numpy()
-    pr = fe.my_pairs
-    # the kernel events bracket each launch and end on the LAST pair chunk's: its pairs are the launch's work
-    a_last, b_last = fe.pchunks[-1]
-    pl = pr[a_last:b_last]
-    match_flop = float((2.0 * kc[pl[:, 0]] * kc[pl[:, 1]] * 128).sum())
-    match_flop_all = float((2.0 * kc[pr[:, 0]] * kc[pr[:, 1]] * 128).sum())
-    H_p, M_p, S_p = stats["n_hyp"], stats["n_matches"], stats["n_models"]
-    verify_flop = float((1.2e4 * H_p + 36.0 * M_p * S_p).sum().item())
-    extract_bytes = fe.n_local * sift_bytes_per_image(H, W, kpts)
-    mnn_ms = float(np.median(kernel_ms))
-    if world > 1:
         torch.distributed.all_reduce(n_ok)
         torch.distributed.all_reduce(n_inl_rows)
-    match_tf = match_flop / (mnn_ms * 1e-3) / 1e12
-    ex_ms, ver_ms = st_res.get("extract", float("nan")), st_res.get("verify", float("nan"))
-    extract_gbs = extract_bytes / (ex_ms * 1e-3) / 1e9
+    pr = fe.my_pairs
+    a_last, b_last = fe.pchunks[-1]
+    pl = pr[a_last:b_last]  # the kernel events end on the LAST pair chunk's launch: its pairs are that launch's work
+    D = fe.desc_dim
+    H_p, M_p, S_p = stats["n_hyp"], stats["n_matches"], stats["n_models"]
+    verify_flop = float((1.2e4 * H_p + 36.0 * M_p * S_p).sum().item())
+    ex_ms, m_ms, ver_ms = (st_res.get(k, float("nan")) for k in ("extract", "match", "verify"))
     verify_tf = verify_flop / (ver_ms * 1e-3) / 1e12
-    kpad = -(-kpts // 256) * 256
-    n_rows = world * fe.n_per
-    # the last launch's operand images (both sides of its pairs) read once, its putatives written once
-    n_launch_img = len(np.unique(pl))
-    algo_bytes = 2 * n_launch_img * kpad * 144 * 2 + 2 * len(pl) * kpts * 8  # two fp16 forms, K = 144
-    traffic = pmc_traffic()
-    roof = {"bound": "mfma", "achieved": round(match_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(match_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
-            "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
-            "kernel": "mnn_pp_kernel (one launch per pair chunk)", "kernel_ms": round(mnn_ms, 3),
-            "work": "2*K1*K2*128 flop per pair, summed over the last launch's %d pairs (GFLOP: %.1f of %.1f per step)"
-                    % (len(pl), match_flop / 1e9, match_flop_all / 1e9)}
-    roof["stages"] = {
-        "extract": {"bound": "hbm", "achieved": round(extract_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(extract_gbs / HBM_PEAK_GBS, 4), "ms": ex_ms,
-                    "work": "SURVEY 8(d): 84*sum_o P_o + H*W + K*528 B/image = %.3f GB x %d images"
-                            % (sift_bytes_per_image(H, W, kpts) / 1e9, fe.n_local)},
-        "match": {"bound": "mfma", "achieved": round(match_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                  "frac": round(match_tf / MFMA_F16_PEAK_TFLOPS, 4), "ms": round(mnn_ms, 3),
-                  "work": "2*K1*K2*128 flop per pair (distance GEMM counted once)"},
-        "verify": {"bound": "valu", "achieved": round(verify_tf, 2), "peak": VALU_F32_PEAK_TFLOPS,
-                   "unit": "TFLOP/s", "frac": round(verify_tf / VALU_F32_PEAK_TFLOPS, 4), "ms": ver_ms,
-                   "work": "SURVEY 8(d): sum_p H_p*1.2e4 + 36*M_p*(models scored)_p; H mean %.1f, models/H %.2f"
-                           % (float(H_p.mean()), float(S_p.sum() / max(float(H_p.sum()), 1.0)))},
-    }
-    if traffic:
-        roof["traffic_note"] = ("L2-miss bytes, Infinity-Cache hits included: the A operand (image i2) of each pair is "
-                                "re-read past the 4 MiB XCD L2, from a %.0f MB operand set that fits the 256 MiB "
-                                "Infinity Cache" % (2 * n_launch_img * kpad * 144 * 2 / 1e6))
-    wl = {"c1": "C1", "c4": "C4"}.get(config, "C2")
+    verify_stage = {"bound": "valu", "achieved": round(verify_tf, 2), "peak": VALU_F32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(verify_tf / VALU_F32_PEAK_TFLOPS, 4), "ms": ver_ms,
+                    "work": "SURVEY 8(d): sum_p H_p*1.2e4 + 36*M_p*(models scored)_p; H mean %.1f, models/H %.2f"
+                            % (float(H_p.mean()), float(S_p.sum() / max(float(H_p.sum()), 1.0)))}
+    gemm_ms = float(np.median(kernel_ms))
+    gemm_flop = float((2.0 * kc[pl[:, 0]] * kc[pl[:, 1]] * D).sum())
+    gemm_flop_all = float((2.0 * kc[pr[:, 0]] * kc[pr[:, 1]] * D).sum())
+    gemm_tf = gemm_flop / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else float("nan")
+    if not deep:
+        extract_bytes = fe.n_local * sift_bytes_per_image(H, W, kpts)
+        extract_gbs = extract_bytes / (ex_ms * 1e-3) / 1e9
+        kpad = -(-kpts // 256) * 256
+        # the last launch's operand images (both sides of its pairs) read once, its putatives written once
+        n_launch_img = len(np.unique(pl))
+        algo_bytes = 2 * n_launch_img * kpad * 144 * 2 + 2 * len(pl) * kpts * 8  # two fp16 forms, K = 144
+        traffic = pmc_traffic()
+        roof = {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(gemm_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
+                "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
+                "kernel": "mnn_pp_kernel (one launch per pair chunk)", "kernel_ms": round(gemm_ms, 3),
+                "work": "2*K1*K2*128 flop per pair, summed over the last launch's %d pairs (GFLOP: %.1f of %.1f per "
+                        "step)" % (len(pl), gemm_flop / 1e9, gemm_flop_all / 1e9)}
+        roof["stages"] = {
+            "extract": {"bound": "hbm", "achieved": round(extract_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(extract_gbs / HBM_PEAK_GBS, 4), "ms": ex_ms,
+                        "work": "SURVEY 8(d): 84*sum_o P_o + H*W + K*528 B/image = %.3f GB x %d images"
+                                % (sift_bytes_per_image(H, W, kpts) / 1e9, fe.n_local)},
+            "match": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(gemm_tf / MFMA_F16_PEAK_TFLOPS, 4), "ms": round(gemm_ms, 3),
+                      "work": "2*K1*K2*128 flop per pair (distance GEMM counted once)"},
+            "verify": verify_stage,
+        }
+        if traffic:
+            roof["traffic_note"] = ("L2-miss bytes, Infinity-Cache hits included: the A operand (image i2) of each "
+                                    "pair is re-read past the 4 MiB XCD L2, from a %.0f MB operand set that fits the "
+                                    "256 MiB Infinity Cache" % (2 * n_launch_img * kpad * 144 * 2 / 1e6))
+    else:
+        sp_flop = fe.n_local * SP_FLOP_PER_PIXEL * H * W
+        sp_tf = sp_flop / (ex_ms * 1e-3) / 1e12
+        ex_stage = {"bound": "mfma", "achieved": round(sp_tf, 1), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(sp_tf / MFMA_F32_PEAK_TFLOPS, 4), "ms": ex_ms,
+                    "work": "SURVEY 8(d): SuperPoint ~169,600 FLOP per pixel (fp32 MFMA convs) x %d images"
+                            % fe.n_local}
+        if config == "c5":
+            sg_flop = float(superglue_flop(kc[pr[:, 0]], kc[pr[:, 1]]).sum())
+            sg_tf = sg_flop / (m_ms * 1e-3) / 1e12
+            match_stage = {"bound": "mfma", "achieved": round(sg_tf, 1), "peak": MFMA_F32_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(sg_tf / MFMA_F32_PEAK_TFLOPS, 4), "ms": m_ms,
+                           "work": "SURVEY 8(d): SuperGlue 18*2*(20*K*d^2 + 4*K1*K2*d) + 2*K1*K2*d per pair "
+                                   "(d = 256; ~254 GFLOP at K = 2048) over %d pairs, all SuperGlue kernels of the "
+                                   "stage (GEMMs, attention, Sinkhorn) timed together" % len(pr)}
+            roof = dict(match_stage)
+            roof["kernel"] = "SuperGlue stage (sg_gemm / sg_attention / Sinkhorn kernels), HIP events on its stream"
+            roof["traffic"] = None
+        else:
+            match_stage = {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+                           "unit": "TFLOP/s", "frac": round(gemm_tf / MFMA_F16_PEAK_TFLOPS, 4),
+                           "ms": round(gemm_ms, 3), "stage_ms": m_ms,
+                           "work": "2*K1*K2*256 flop per pair over the last launch's %d pairs (the shortlist kernel "
+                                   "computes the matrix once per side: 2x this)" % len(pl)}
+            roof = dict(match_stage)
+            roof["kernel"] = "fl_shortlist_kernel (F16_RERANK fp16 MFMA shortlist; one launch per pair chunk)"
+            roof["traffic"] = None
+        roof["stages"] = {"extract": ex_stage, "match": match_stage, "verify": verify_stage}
+    wl = {"c1": "C1", "c4": "C4", "c3": "C3", "c5": "C5 slice"}.get(config, "C2")
+    if deep:
+        desc = (f"{wl}: {n_img} synthetic {W}x{H} images, all {fe.total_pairs} pairs, SuperPoint {kpts} kpts/img + "
+                + ("SuperGlue 18 layers / 20 Sinkhorn iterations" if config == "c5" else
+                   f"TwoWayMatcher ratio {RATIO} (F16_RERANK)") + f", 5-pt RANSAC {THRESH_PX}px + inlier support")
+        dtype = ("u8 image / fp32-MFMA SuperPoint / " + ("fp32-MFMA SuperGlue" if config == "c5" else
+                 "fp16-MFMA shortlist + fp32 exact re-rank") + " / fp64 RANSAC solver")
+        data = ("synthetic (rendered textured room, seeds 0/1/2); seeded random network weights with a whitened "
+                "SuperPoint descriptor head (tests/golden/make_superpoint_whitening.py)")
+    else:
+        desc = (f"{wl}: {n_img} {'Lund Door' if config == 'c1' else 'synthetic'} {W}x{H} images, all "
+                f"{fe.total_pairs} pairs, SIFT {kpts} kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px"
+                + (" + two-view BA" if args.ba else "") + " + inlier support")
+        dtype = "u8 image / fp32 pyramid / fp16-MFMA exact-int distances / fp64 RANSAC solver"
+        data = ("the reference's Lund Door images (tests/data/set1_lund_door)" if config == "c1" else
+                "synthetic (rendered textured room, seeds 0/1/2)")
     out = {
         "metric": "verified image-pairs/sec (all-pairs front-end), N images @ 2048 kpts/img",
         "value": round(value, 2),
@@ -552,25 +594,25 @@ def main_frontend(args, info, config: str):
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "u8 image / fp32 pyramid / fp16-MFMA exact-int distances / fp64 RANSAC solver",
-        "data": ("the reference's Lund Door images (tests/data/set1_lund_door)" if config == "c1" else
-                 "synthetic (rendered textured room, seeds 0/1/2)"),
-        "config": {"workload": f"{wl}: {n_img} {'Lund Door' if config == 'c1' else 'synthetic'} {W}x{H} images, "
-                               f"all {fe.total_pairs} pairs, SIFT {kpts} "
-                               f"kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px"
-                               + (" + two-view BA" if args.ba else "") + " + inlier support",
-                   "images": n_img, "pairs": fe.total_pairs, "kpts": kpts, "parallelism": f"pair blocks x{world}",
+        "dtype": dtype,
+        "data": data,
+        "config": {"workload": desc, "images": n_img, "pairs": fe.total_pairs, "kpts": kpts,
+                   "parallelism": f"pair blocks x{world}",
                    "world_size": torch.distributed.get_world_size() if torch.distributed.is_initialized() else 1},
         "value_host_to_host": round(fe.total_pairs / (elapsed / args.steps), 2),
         "ms_per_step_host_to_host": round(elapsed / args.steps * 1e3, 3),
         "pairs_passing_isp": int(n_ok.item()),
         "verified_rows": int(n_inl_rows.item()),
+        "mean_putatives": round(float(M_p.mean()), 1) if len(M_p) else 0.0,
         "stage_ms": st_res,
         "stage_ms_host_to_host": st_host,
         "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts)
+    if want_baseline:
+        if deep:
+            out["cpu_baseline"] = deep_cpu_baseline(baseline_images, intrinsics, n_img, kpts, sp_sd, sg_sd)
+        else:
+            out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts)
     if rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -612,8 +654,6 @@ def main():
     try:
         if args.config == "c3-match":
             main_c3(args, info.world, info.rank, info.device)
-        elif args.config in ("c3", "c5"):
-            main_dl(args, info.world, info.rank, info.device, args.config)
         else:
             main_frontend(args, info, args.config)
     finally:

@@ -324,10 +324,13 @@ class SuperPointResult:
 
 def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: int, keypoint_threshold: float = 0.005,
                        nms_radius: int = 4, remove_borders: int = 4,
-                       stream: Optional[torch.cuda.Stream] = None) -> SuperPointResult:
+                       stream: Optional[torch.cuda.Stream] = None, out: Optional[SuperPointResult] = None,
+                       workspace: Optional[torch.Tensor] = None) -> SuperPointResult:
     """SuperPoint on a batch of same-sized uint8 images (n, H, W) gray or (n, H, W, 3) RGB (gtsfm_superpoint_batched).
 
     weights: the packed fp32 blob (gtsfm_amd.frontend.detector_descriptor.superpoint.pack_superpoint_weights).
+    out: optional preallocated outputs (xy (n,k,2), scores (n,k), desc (n,k,256), count, n_detected; rows past a
+    count are unspecified); workspace: optional device buffer of at least gtsfm_superpoint_workspace_bytes.
     """
     assert images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous()
     assert weights.is_cuda and weights.dtype == torch.float32 and weights.is_contiguous()
@@ -336,14 +339,18 @@ def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: in
     n, H, W = images.shape[0], images.shape[1], images.shape[2]
     C = 1 if images.dim() == 3 else images.shape[3]
     dev = images.device
-    out = SuperPointResult(torch.zeros((n, max_kpts, 2), dtype=torch.float32, device=dev),
-                           torch.zeros((n, max_kpts), dtype=torch.float32, device=dev),
-                           torch.empty((n, max_kpts, 256), dtype=torch.float32, device=dev),
-                           torch.zeros((n,), dtype=torch.int32, device=dev),
-                           torch.zeros((n,), dtype=torch.int32, device=dev))
+    if out is None:
+        out = SuperPointResult(torch.zeros((n, max_kpts, 2), dtype=torch.float32, device=dev),
+                               torch.zeros((n, max_kpts), dtype=torch.float32, device=dev),
+                               torch.empty((n, max_kpts, 256), dtype=torch.float32, device=dev),
+                               torch.zeros((n,), dtype=torch.int32, device=dev),
+                               torch.zeros((n,), dtype=torch.int32, device=dev))
+    for t, shape in ((out.xy, (n, max_kpts, 2)), (out.scores, (n, max_kpts)), (out.desc, (n, max_kpts, 256))):
+        assert t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and tuple(t.shape) == shape
     if n == 0:
         return out
-    ws = _workspace(L.gtsfm_superpoint_workspace_bytes(n, H, W, max_kpts), dev)
+    need = L.gtsfm_superpoint_workspace_bytes(n, H, W, max_kpts)
+    ws = workspace if workspace is not None and workspace.numel() >= need else _workspace(need, dev)
     if stream is not None:
         ws.record_stream(stream)
     rc = L.gtsfm_superpoint_batched(_ptr(images), n, H, W, C, _ptr(weights), max_kpts, float(keypoint_threshold),

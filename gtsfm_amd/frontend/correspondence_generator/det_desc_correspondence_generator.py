@@ -6,14 +6,18 @@ Drop-in for gtsfm/frontend/correspondence_generator/det_desc_correspondence_gene
 dict (i1, i2) -> (M, 2) uint32 putative correspondences (np.array([]) for a pair without matches,
 twoway_matcher.py:71-72,80-81).
 
-The reference submits one Dask task per image and one per pair (:64-80). Here, when the plugins are the HIP SIFT
-and the HIP TwoWayMatcher, images of one size go through ONE batched SIFT launch sequence, their features stay in
-HBM as one padded (n, k, 128) block, and all pairs go through ONE batched matcher launch per chunk of pairs. Other
-plugin combinations run their own per-call methods in the reference's order.
+The reference submits one Dask task per image and one per pair (:64-80). Here the HIP plugin combinations of the
+BASELINE configs run batched on the device: images of one size go through ONE batched extraction launch sequence
+(per workspace-bounded group), their features stay in HBM as one padded (n, k, D) block, and the pairs go through one
+batched matcher launch per chunk of pairs:
+- SIFTDetectorDescriptor + TwoWayMatcher (configs C1, C2, C4): the exact-integer fp16 MFMA distance GEMM;
+- SuperPointDetectorDescriptor + TwoWayMatcher (config C3): the F16_RERANK matcher on the float descriptors;
+- SuperPointDetectorDescriptor + SuperGlueMatcher (config C5): batched SuperGlue (superglue.hip).
+Any other combination (e.g. cacher-wrapped plugins) runs its own per-call methods in the reference's order.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -25,6 +29,8 @@ from gtsfm_amd.frontend.correspondence_generator.correspondence_generator_base i
 from gtsfm_amd.frontend.detector_descriptor.detector_descriptor_base import DetectorDescriptorBase
 from gtsfm_amd.frontend.detector_descriptor.sift import SIFTDetectorDescriptor, extract_group, sift_groups
 from gtsfm_amd.frontend.matcher.matcher_base import MatcherBase
+from gtsfm_amd.frontend.detector_descriptor.superpoint import SuperPointDetectorDescriptor
+from gtsfm_amd.frontend.matcher.superglue_matcher import MATCH_THRESHOLD, SuperGlueMatcher
 from gtsfm_amd.frontend.matcher.twoway_matcher import MatchingDistanceType, TwoWayMatcher
 
 PAIR_CHUNK = 8192  # pairs per matcher launch: (chunk, k, 2) int32 indices = 128 MiB at k = 2048
@@ -84,6 +90,82 @@ def match_pairs_batched(feats: DeviceFeatures, image_pairs: Sequence[Tuple[int, 
     return out
 
 
+SP_GROUP_BYTES = 16 << 30  # SuperPoint workspace per launch (~0.75 GB per 1080p image)
+
+
+def extract_superpoint_batched(detector: SuperPointDetectorDescriptor, images: Sequence[Image]) -> DeviceFeatures:
+    """gtsfm_superpoint_batched per image size in workspace-bounded groups; features gathered into one padded block
+    (scores kept for SuperGlue). Masks are not supported on the device path (the per-call plugin raises too)."""
+    native.require_gpu()
+    n, k = len(images), detector.max_keypoints
+    dev = torch.device("cuda")
+    xy = torch.zeros((n, k, 2), dtype=torch.float32, device=dev)
+    sc = torch.zeros((n, k), dtype=torch.float32, device=dev)
+    desc = torch.zeros((n, k, 256), dtype=torch.float32, device=dev)
+    count = torch.zeros((n,), dtype=torch.int32, device=dev)
+    by_shape: Dict[tuple, List[int]] = {}
+    for i, im in enumerate(images):
+        if im.mask is not None:
+            raise NotImplementedError("image masks are not supported on the MI355X SuperPoint path yet")
+        by_shape.setdefault(tuple(im.value_array.shape), []).append(i)
+    L = native.lib()
+    for shape, idx in by_shape.items():
+        per = max(1, int(L.gtsfm_superpoint_workspace_bytes(1, shape[0], shape[1], k)))
+        g = max(1, SP_GROUP_BYTES // per)
+        for s0 in range(0, len(idx), g):
+            part = idx[s0: s0 + g]
+            res = detector.extract_batch([images[i].value_array for i in part], k)
+            sel = torch.tensor(part, dtype=torch.long, device=dev)
+            xy[sel], sc[sel], desc[sel], count[sel] = res.xy, res.scores, res.desc, res.count
+    cnt = count.cpu().numpy()
+    xy_h, sc_h = xy.cpu().numpy(), sc.cpu().numpy()
+    kps = [Keypoints(coordinates=xy_h[i, : cnt[i]], scales=None, responses=sc_h[i, : cnt[i]]) for i in range(n)]
+    out = DeviceFeatures(xy, desc, count, kps)
+    out.scores = sc
+    return out
+
+
+def superglue_pairs_batched(matcher: SuperGlueMatcher, feats: DeviceFeatures, image_shapes: Sequence[tuple],
+                            image_pairs: Sequence[Tuple[int, int]], chunk: int = 1024
+                            ) -> Dict[Tuple[int, int], np.ndarray]:
+    """All pairs through gtsfm_superglue_batched on the resident features, `chunk` pairs per launch sequence (the
+    workspace is ~59 MB per pair at 2048 keypoints); host dict in SuperGlueMatcher.match's format."""
+    out: Dict[Tuple[int, int], np.ndarray] = {}
+    pairs = np.asarray(image_pairs, dtype=np.int64).reshape(-1, 2)
+    dev = feats.desc.device
+    kmax = feats.desc.shape[1]
+    kpad = (kmax + 63) // 64 * 64
+    xy, sc, desc = feats.xy, feats.scores, feats.desc
+    if kpad != kmax:
+        pad = kpad - kmax
+        xy = torch.nn.functional.pad(xy, (0, 0, 0, pad))
+        sc = torch.nn.functional.pad(sc, (0, pad))
+        desc = torch.nn.functional.pad(desc, (0, 0, 0, pad))
+    hw = torch.tensor([[int(s[0]), int(s[1])] for s in image_shapes], dtype=torch.int32, device=dev)
+    cnt_h = feats.count.cpu().numpy()
+    ws = None
+    for s in range(0, len(pairs), chunk):
+        blk = pairs[s: s + chunk]
+        run = blk[(cnt_h[blk[:, 0]] > 0) & (cnt_h[blk[:, 1]] > 0)] if len(blk) else blk
+        for i1, i2 in blk:
+            out[(int(i1), int(i2))] = np.zeros((0, 2), np.uint32)
+        if not len(run):
+            continue
+        need = int(native.lib().gtsfm_superglue_workspace_bytes(len(run), kpad))
+        if ws is None or ws.numel() < need:
+            ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        idx, c, _ = device.superglue_match(xy.contiguous(), sc.contiguous(), desc.contiguous(), feats.count, hw,
+                                           torch.from_numpy(run.astype(np.int32)).to(dev), matcher.weights(),
+                                           matcher._n_layers, matcher._config["sinkhorn_iterations"],
+                                           MATCH_THRESHOLD, workspace=ws)
+        c = c.cpu().numpy()
+        w = int(c.max()) if len(c) else 0
+        idx_h = idx[:, :w].cpu().numpy().view(np.uint32)
+        for j, (i1, i2) in enumerate(run):
+            out[(int(i1), int(i2))] = idx_h[j, : c[j]].copy()
+    return out
+
+
 class DetDescCorrespondenceGenerator(CorrespondenceGeneratorBase):
     """Traditional detect -> describe -> match, batched on the device when the plugins are the HIP ones."""
 
@@ -95,21 +177,41 @@ class DetDescCorrespondenceGenerator(CorrespondenceGeneratorBase):
     def __repr__(self) -> str:
         return f"DetDescCorrespondenceGenerator:\n   {self._detector_descriptor}\n   {self._matcher}\n"
 
-    def _batched(self) -> bool:
-        m = self._matcher
-        return (isinstance(self._detector_descriptor, SIFTDetectorDescriptor) and isinstance(m, TwoWayMatcher)
-                and m._distance_type is MatchingDistanceType.EUCLIDEAN)
+    def _batched(self) -> Optional[str]:
+        """Which batched device path serves this plugin pair: 'sift', 'superpoint_twoway', 'superpoint_superglue',
+        or None (per-call)."""
+        d, m = self._detector_descriptor, self._matcher
+        twoway_l2 = type(m) is TwoWayMatcher and m._distance_type is MatchingDistanceType.EUCLIDEAN
+        if type(d) is SIFTDetectorDescriptor and twoway_l2:
+            return "sift"
+        if type(d) is SuperPointDetectorDescriptor and twoway_l2:
+            return "superpoint_twoway"
+        if type(d) is SuperPointDetectorDescriptor and type(m) is SuperGlueMatcher:
+            return "superpoint_superglue"
+        return None
 
     def generate_correspondences(
         self, client, images: List, image_pairs: List[Tuple[int, int]]
     ) -> Tuple[List[Keypoints], Dict[Tuple[int, int], np.ndarray]]:
         imgs = [resolve(im) for im in images]
-        if self._batched():
+        path = self._batched()
+        if path == "sift":
             feats = extract_sift_batched(self._detector_descriptor, imgs)
             self.device_features = feats
             # SIFT descriptors are integers in [0, 255] with |d|^2 < 2^19: the exact fp16 MFMA path applies
             corr = match_pairs_batched(feats, image_pairs, self._matcher._ratio_test_threshold,
                                        native.GTSFM_MATCH_INT_F16)
+            return feats.keypoints, corr
+        if path is not None:
+            feats = extract_superpoint_batched(self._detector_descriptor, imgs)
+            self.device_features = feats
+            if path == "superpoint_twoway":
+                # 256-D float descriptors: fp16 MFMA shortlist + certified exact re-rank (same matches as EXACT_F32)
+                corr = match_pairs_batched(feats, image_pairs, self._matcher._ratio_test_threshold,
+                                           native.GTSFM_MATCH_F16_RERANK)
+            else:
+                corr = superglue_pairs_batched(self._matcher, feats, [im.value_array.shape for im in imgs],
+                                               image_pairs)
             return feats.keypoints, corr
         features = [self._detector_descriptor.detect_and_describe(im) for im in imgs]
         corr = {}

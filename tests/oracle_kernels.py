@@ -1,4 +1,4 @@
-"""Test stand-in for gtsfm_amd.frontend.all_pairs.HipKernels: the same five calls computed by the CPU oracle on CPU
+"""Test stand-in for gtsfm_amd.frontend.all_pairs.HipKernels: the same kernel-set calls computed by the CPU oracle on CPU
 tensors, so AllPairsFrontEnd's host logic (chunking, sharding, all-gather, compaction, D2H assembly) runs under gloo
 without a GPU. Test infrastructure only -- never imported by the product package."""
 from __future__ import annotations
@@ -22,10 +22,14 @@ class OracleRansacResult:
 
 
 class OracleKernels:
-    def sift_workspace_bytes(self, n, H, W, kpts):
+    attr_dim, desc_dim = 3, 128
+    gather = (("xy", None), ("desc", torch.uint8), ("count", None))
+    max_pair_chunk = None
+
+    def extract_workspace_bytes(self, n, H, W, kpts):
         return 0
 
-    def sift(self, images, kpts, out, workspace):
+    def extract(self, images, kpts, out, workspace):
         for i in range(images.shape[0]):
             img = images[i].numpy()
             gray = oracle.rgb_to_gray(img) if img.ndim == 3 else img
@@ -39,7 +43,8 @@ class OracleKernels:
             out.count[i] = n
             out.n_detected[i] = nd
 
-    def match(self, desc, counts, pairs, ratio, groups=None):  # groups only lay out GPU work
+    def match(self, f, pairs, ratio, groups=None, image_hw=None):  # groups only lay out GPU work
+        desc, counts = f.desc, f.count
         P, kmax = pairs.shape[0], desc.shape[1]
         idx = torch.zeros((P, kmax, 2), dtype=torch.int32)
         cnt = torch.zeros(P, dtype=torch.int32)

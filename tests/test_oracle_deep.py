@@ -1,0 +1,44 @@
+"""oracle/deep.py (the CPU restatement of SuperPoint / SuperGlue used as checker and CPU baseline) against the reference
+modules' own outputs on seeded random weights (tests/golden/superpoint_random_w0.npz, superglue_random_w0.npz, written
+in this container by tests/golden/make_superpoint_golden.py / make_superglue_golden.py from
+/root/reference/thirdparty/SuperGluePretrainedNetwork/models/*.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from superpoint_weights import superglue_state_dict, superpoint_state_dict
+from tests.conftest import GOLDEN
+
+
+@pytest.fixture(scope="module")
+def sp_golden():
+    return np.load(os.path.join(GOLDEN, "superpoint_random_w0.npz"))
+
+
+@pytest.mark.parametrize("case", ["lund_250x333", "synthetic_240x320", "lund_480x640"])
+def test_superpoint_restatement_matches_reference(sp_golden, case):
+    from oracle import deep
+
+    g = sp_golden
+    kp, sc, desc = deep.superpoint(g[f"{case}__image"], superpoint_state_dict(0))
+    np.testing.assert_array_equal(kp, g[f"{case}__keypoints"])
+    np.testing.assert_allclose(sc, g[f"{case}__scores"], rtol=1e-5, atol=1e-7)
+    rows = g[f"{case}__desc_rows"]
+    np.testing.assert_allclose(desc[rows], g[f"{case}__desc"], atol=2e-6)
+
+
+@pytest.mark.parametrize("case", ["small_150x170", "mid_700x650"])
+def test_superglue_restatement_matches_reference(case):
+    from oracle import deep
+
+    g = np.load(os.path.join(GOLDEN, "superglue_random_w0.npz"))
+    k = lambda n: g[f"{case}__{n}"]  # noqa: E731
+    hw = tuple(int(v) for v in k("hw"))
+    m0, ms0 = deep.superglue(k("kp0"), k("kp1"), k("d0"), k("d1"), k("s0"), k("s1"), hw, hw, superglue_state_dict(0))
+    ref = k("matches0")
+    assert (m0 >= 0).sum() > 10
+    # float32 on both sides, different accumulation order inside the einsums: allow the rare near-threshold flip
+    assert (m0 != ref).sum() <= max(1, 0.005 * len(ref)), ((m0 != ref).sum(), len(ref))
+    both = (m0 >= 0) & (ref >= 0)
+    np.testing.assert_allclose(ms0[both], k("mscores0")[both], atol=1e-4)
