@@ -20,6 +20,25 @@
 
 #include "common.hpp"
 
+// Development instrumentation (off in the product build): -DGTSFM_RANSAC_PROF accumulates per-phase shader-clock
+// cycles of every wave into g_rprof (vector global atomics from lane 0), read back with gtsfm_ransac_prof_read.
+#ifdef GTSFM_RANSAC_PROF
+__device__ unsigned long long g_rprof[32];
+#define RPROF_DECL unsigned long long rprof_t = clock64();
+#define RPROF(k)                                                              \
+    do {                                                                      \
+        const unsigned long long rprof_n = clock64();                         \
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_rprof[k], rprof_n - rprof_t); \
+        rprof_t = rprof_n;                                                    \
+    } while (0)
+#define RPROF_COUNT(k, v) \
+    do { if ((threadIdx.x & 63) == 0) atomicAdd(&g_rprof[k], (unsigned long long)(v)); } while (0)
+#else
+#define RPROF_DECL
+#define RPROF(k) do { } while (0)
+#define RPROF_COUNT(k, v) do { } while (0)
+#endif
+
 namespace {
 
 constexpr int kBatch = 64;      // hypotheses per chunk: the iteration bound is re-evaluated after each chunk
@@ -194,6 +213,7 @@ __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
 // isolation step.
 template <typename RootFn>
 __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_root) {
+    RPROF_DECL
     LaneArr<double> S = m.u;  // chain row k in slot k % 3 (11 doubles each) while it is still needed by prem
     LaneArr<double> t = m.u.at(33);
     LaneArr<uint8_t> sdeg = m.b.at(2 * kStack);
@@ -226,6 +246,7 @@ __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_roo
             }
         n++;
     }
+    RPROF(7);
     // root bound (== oracle root_bound_pow2): exact exponent arithmetic, a power of two
     double bound;
     {
@@ -270,6 +291,8 @@ __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_roo
             st_a[ns] = a; st_b[ns] = mid; st_va[ns] = (uint8_t)va; st_vb[ns] = (uint8_t)vm; ++ns;
         }
     }
+    RPROF(8);
+    RPROF_COUNT(20, guard);
     double lo[kMaxSol], hi[kMaxSol], flo[kMaxSol];
 #pragma unroll
     for (int k = 0; k < kMaxSol; ++k) {
@@ -298,6 +321,7 @@ __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_roo
             hi[k] = go && !left ? mid : hi[k];
         }
     }
+    RPROF(9);
     double xr[kMaxSol];
 #pragma unroll
     for (int k = 0; k < kMaxSol; ++k) xr[k] = 0.5 * (lo[k] + hi[k]);
@@ -318,11 +342,14 @@ __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_roo
             xr[k] = go ? xs : xr[k];
         }
     }
+    RPROF(10);
     LaneArr<double> roots = iv_a;
 #pragma unroll
     for (int k = 0; k < kMaxSol; ++k)
         if (k < nr) roots[k] = xr[k];
     for (int k = 0; k < nr; ++k) on_root(roots[k]);
+    RPROF(11);
+    RPROF_COUNT(21, nr);
     return nr;
 }
 
@@ -399,7 +426,9 @@ constexpr int kStageVals = 6 * 10 + 4 * 9;  // doubles handed from stage 1 to st
 
 __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem m, int part, double N[4][9],
                                   double Rt[6][10]) {
+    RPROF_DECL
     if (!nullspace_5x9(x1, x2, m, N)) return false;
+    RPROF(1);
     double E[9][4];
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
@@ -456,6 +485,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
             addmul_ql(tr, E[3 * i + j], -1.0, row);
             store_row(1 + 3 * i + j, row);
         }
+    RPROF(2);
     // Gauss-Jordan with partial pivoting on the lane's half rows; every row is moved through registers whole
 #pragma unroll
     for (int c = 0; c < 10; ++c) {
@@ -499,6 +529,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
     for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int j = 0; j < 10; ++j) Rt[r][j] = A[10 * (4 + r) + j];
+    RPROF(3);
     return true;
 }
 
@@ -506,6 +537,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
 // 10 unit-norm E; on_sol(s, E) is called for each solution in root order.
 template <typename SolFn>
 __device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], RootMem m, SolFn&& on_sol) {
+    RPROF_DECL
     double B[3][3][5];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -545,6 +577,7 @@ __device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], R
         }
     }
     int nsol = 0;
+    RPROF(6);
     real_roots(n, 10, m, [&](double z) {
         double Bz[3][3];
 #pragma unroll
@@ -1081,6 +1114,8 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
     const double2* x1 = x1n_all + (size_t)p * mcap;
     const double2* x2 = x2n_all + (size_t)p * mcap;
     const SolverMem mem = solver_mem(smem, lane);
+    RPROF_DECL
+    RPROF_COUNT(16, 1);
     int ok = 0;
     int idx[5];
     if (sample5(seed, pair_ids ? pair_ids[p] : pair_id_base + p, done + hyp, M, idx)) {
@@ -1092,6 +1127,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
             s2[2 * k] = b.x; s2[2 * k + 1] = b.y;
         }
         double N[4][9], Rt[6][10];
+        RPROF(0);
         if (five_point_stage1(s1, s2, mem, part, N, Rt)) {
             ok = 1;
             double* out = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
@@ -1109,6 +1145,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
         }
     }
     if (!part) nsol[(size_t)p * kMaxHyp + hyp] = ok;
+    RPROF(4);
 }
 
 // Stage 2, one 64-lane workgroup per chunk of an active pair (blockIdx.y = chunk): lane l turns stage 1's output into
@@ -1126,6 +1163,8 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
     int* ns_out = nsol + (size_t)p * kMaxHyp + hyp;
     if (*ns_out == 0) return;  // degenerate sample: stays 0
     const RootMem mem = root_mem(smem, lane);
+    RPROF_DECL
+    RPROF_COUNT(17, 1);
     double N[4][9], Rt[6][10];
     const double* in = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
 #pragma unroll
@@ -1137,11 +1176,13 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
 #pragma unroll
         for (int j = 0; j < 9; ++j) N[k][j] = in[(60 + 9 * k + j) * kMaxHyp];
     double* cout = cand + ((size_t)p * kMaxHyp + hyp) * (kMaxSol * 9);
+    RPROF(5);
     const int ns = five_point_stage2(N, Rt, mem, [&](int s, const double* E) {
 #pragma unroll
         for (int e = 0; e < 9; ++e) cout[9 * s + e] = E[e];
     });
     *ns_out = ns;
+    RPROF(12);
 }
 
 // One kScoreWaves-wave workgroup per active pair: the pair's putatives are staged in LDS once, then the launch's chunks are
@@ -1197,6 +1238,8 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
         for (int i = tid; i < M; i += 64 * kScoreWaves) spts[i] = pts[i];
     const float4* sp = kLds ? (const float4*)spts : pts;
     long best_off = -1;  // cand offset of a winner found by this launch
+    RPROF_DECL
+    RPROF_COUNT(18, 1);
 #pragma unroll 1
     for (int g = 0; g < n_chunks && done < niters; ++g) {
         const size_t hbase = (size_t)p * kMaxHyp + (size_t)g * kBatch;  // the chunk's first hypothesis slot
@@ -1215,6 +1258,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
             }
         }
         __syncthreads();
+        RPROF(14);
         const int total = flat_off[kBatch];
         // candidate ci's E (fp64 in HBM); the next one of this wave is fetched while the current one is counted
         auto fetch = [&](int ci, double (&e)[9]) {
@@ -1281,6 +1325,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
             }
             if (alive && lane == 0) atomicMax(&best_key, ((unsigned long long)(uint32_t)(c + 1) << 32) | my_low);
         }
+        RPROF(13);
         __syncthreads();
         if (tid == 0) {
             const unsigned long long bk = best_key;
@@ -1351,6 +1396,7 @@ __global__ __launch_bounds__(64, GTSFM_REFINE_OCC) void ransac_refine_kernel(con
         for (int i = lane; i < M; i += 64) mask[i] = 0;
         return;
     }
+    RPROF_DECL
     const PairState ps = st[p];
     if (ps.best <= 0) {
         if (lane == 0) {
@@ -1475,6 +1521,7 @@ __global__ __launch_bounds__(64, GTSFM_REFINE_OCC) void ransac_refine_kernel(con
         if (out.n_hyp) out.n_hyp[p] = done;
         if (out.n_models) out.n_models[p] = ps.n_models;
     }
+    RPROF(15);
 }
 
 }  // namespace
@@ -1501,6 +1548,18 @@ static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_p
     o += gtsfm_align_up((size_t)n_pairs * (mcap + 1) * sizeof(int), 256);  // bound table (last)
     return o;
 }
+
+#ifdef GTSFM_RANSAC_PROF
+int gtsfm_ransac_prof_read(unsigned long long* out, int reset) {
+    GTSFM_CHECK_HIP(hipDeviceSynchronize());
+    GTSFM_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rprof), sizeof(unsigned long long) * 32));
+    if (reset) {
+        static const unsigned long long zeros[32] = {};
+        GTSFM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_rprof), zeros, sizeof(zeros)));
+    }
+    return GTSFM_OK;
+}
+#endif
 
 size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap) {
     if (n_pairs <= 0 || mcap <= 0) return 0;

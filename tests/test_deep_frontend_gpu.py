@@ -58,13 +58,16 @@ def test_detdesc_superpoint_batched_equals_per_call(views):
         for i, (k, _) in enumerate(per):
             np.testing.assert_array_equal(kps[i].coordinates, k.coordinates)
             np.testing.assert_array_equal(kps[i].responses, k.responses)
-        n_matches = 0
+        n_matches, n_pairs_matched = 0, 0
         for i1, i2 in pairs:
             ref = matcher.match(per[i1][0], per[i2][0], per[i1][1], per[i2][1], arr[i1].shape, arr[i2].shape)
             got = corr[(i1, i2)]
             np.testing.assert_array_equal(np.asarray(got).reshape(-1, 2), np.asarray(ref).reshape(-1, 2))
             n_matches += len(np.asarray(got).reshape(-1, 2))
-        assert n_matches > 100, type(matcher).__name__
+            n_pairs_matched += len(np.asarray(got).reshape(-1, 2)) > 0
+        # ratio 0.8 in 256-D is selective; SuperGlue at gain 24 returns hundreds per adjacent pair
+        assert n_pairs_matched >= 3 and n_matches >= (100 if matcher is sg else 10), (type(matcher).__name__,
+                                                                                       n_matches, n_pairs_matched)
 
 
 @pytest.mark.parametrize("matcher", ["superglue", "twoway"])
