@@ -20,6 +20,8 @@
 // 1e-5 prior (GeneralSFMFactor2Cal3Bundler + PriorFactorCal3Bundler, bundle_adjustment.py:106-136,180-200). Holding
 // K at its prior value with k1 = k2 = 0 is the limit of that prior; the host refuses non-zero k1 / k2
 // (geometry.calibration_params), so the approximation is the prior's 1e-5 freedom in f only.
+// Relative-pose priors (optional, per pair): the prior's i2Ti1 initialises the second camera and a BetweenFactorPose3
+// joins the LM (two_view_estimator.py:165,192; bundle_adjustment.py:136-152), as oracle/ba2.c.
 // Outputs per pair: status (0 BA ok, 1 no track triangulated, 2 no track valid, 3 not run: verification failed or
 // fewer than min_inliers verified rows -- the reference's guard at :312), R / unit t (the verifier's for statuses 1-3),
 // the post-BA mask over the putatives (the pre-BA mask when not run), its count and the LM iterations.
@@ -143,6 +145,94 @@ __device__ void pose_log(const Pose& T, double* xi) {
     mv3(W, Wt, WWt);
     const double tn = tan(0.5 * th);
     for (int k = 0; k < 3; ++k) xi[3 + k] = T.t[k] - (0.5 * th) * Wt[k] + (1.0 - th / (2.0 * tn)) * WWt[k];
+}
+
+// ------------------------------------------------------------------ relative-pose prior (oracle/ba2.c between_t)
+// BetweenFactorPose3(X0, X1, m = i2Ti1_prior^-1, Diagonal.Sigmas) (bundle_adjustment.py:136-152): whitened
+// e = Logmap(m^-1 X0^-1 X1) / sigma; d e / d X1 = Jr^-1(e), d e / d X0 = -Jr^-1(e) Ad(hx^-1), hx = X0^-1 X1, with
+// Jr^-1(e) = I + ad(e) / 2 + ad(e)^2 / 12. Same operations as the oracle; computed redundantly by every lane.
+struct Between {
+    bool on;
+    Pose minv;       // the prior's value i2Ti1 (= m^-1)
+    double isig[6];  // 1 / sigma, rotation first
+};
+
+__device__ void pose_mul(const Pose& A, const Pose& B, Pose& C) {
+    Pose o;
+    mm3(A.R, B.R, o.R);
+    mv3(A.R, B.t, o.t);
+    for (int k = 0; k < 3; ++k) o.t[k] += A.t[k];
+    C = o;
+}
+
+__device__ void pose_inv(const Pose& A, Pose& C) {
+    Pose o;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) o.R[3 * i + j] = A.R[3 * j + i];
+    mtv3(A.R, A.t, o.t);
+    for (int k = 0; k < 3; ++k) o.t[k] = -o.t[k];
+    C = o;
+}
+
+__device__ void between_residual(const Between& f, const Pose* X, double* e, Pose& hx) {
+    Pose x0i, E0;
+    pose_inv(X[0], x0i);
+    pose_mul(x0i, X[1], hx);
+    pose_mul(f.minv, hx, E0);
+    pose_log(E0, e);
+}
+
+__device__ double between_error(const Between& f, const Pose* X) {
+    if (!f.on) return 0.0;
+    double e[6];
+    Pose hx;
+    between_residual(f, X, e, hx);
+    double s = 0;
+    for (int k = 0; k < 6; ++k) s += (e[k] * f.isig[k]) * (e[k] * f.isig[k]);
+    return 0.5 * s;
+}
+
+__device__ void between_linearize(const Between& f, const Pose* X, double* r, double* J) {
+    double e[6];
+    Pose hx, hi;
+    between_residual(f, X, e, hx);
+    double ad[36], Ji[36], Ad[36];
+    for (int k = 0; k < 36; ++k) ad[k] = 0.0;
+    double Ws[9], Vs[9];
+    skew3(e, Ws);
+    skew3(e + 3, Vs);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            ad[6 * i + j] = Ws[3 * i + j];
+            ad[6 * (3 + i) + j] = Vs[3 * i + j];
+            ad[6 * (3 + i) + 3 + j] = Ws[3 * i + j];
+        }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double a = 0;
+            for (int k = 0; k < 6; ++k) a += ad[6 * i + k] * ad[6 * k + j];
+            Ji[6 * i + j] = (i == j ? 1.0 : 0.0) + 0.5 * ad[6 * i + j] + a / 12.0;
+        }
+    pose_inv(hx, hi);
+    for (int k = 0; k < 36; ++k) Ad[k] = 0.0;
+    double T[9], TR[9];
+    skew3(hi.t, T);
+    mm3(T, hi.R, TR);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Ad[6 * i + j] = hi.R[3 * i + j];
+            Ad[6 * (3 + i) + 3 + j] = hi.R[3 * i + j];
+            Ad[6 * (3 + i) + j] = TR[3 * i + j];
+        }
+    for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 6; ++j) {
+            double a = 0;
+            for (int k = 0; k < 6; ++k) a += Ji[6 * i + k] * Ad[6 * k + j];
+            J[12 * i + j] = -a * f.isig[i];
+            J[12 * i + 6 + j] = Ji[6 * i + j] * f.isig[i];
+        }
+        r[i] = e[i] * f.isig[i];
+    }
 }
 
 __device__ __forceinline__ bool project(const Pose& X, const double* K, const double* p, double* pc, double* uv) {
@@ -476,6 +566,8 @@ struct Ba2Args {
     const double* R_in;
     const double* t_in;
     const int* status_in;
+    const double* prior_Rt;   // [pair][12] i2Ti1_prior (R row-major, t) or null
+    const double* prior_sig;  // [pair][6] its sigmas; sigma[0] <= 0: no prior for the pair
     int min_inliers, max_iters;
     double reproj_thresh, tri_thresh;
     double* P;    // [pair][mcap][3]
@@ -520,6 +612,16 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
     const double K2[3] = {a.intr[3 * i2], a.intr[3 * i2 + 1], a.intr[3 * i2 + 2]};
     const double* Rin = a.R_in + 9 * p;
     const double* tin = a.t_in + 3 * p;
+    // a relative-pose prior initialises the second camera (two_view_estimator.py:165-171) and adds the between factor
+    Between bf;
+    bf.on = a.prior_Rt != nullptr && a.prior_sig != nullptr && a.prior_sig[6 * p] > 0.0;
+    if (bf.on) {
+        for (int k = 0; k < 9; ++k) bf.minv.R[k] = a.prior_Rt[12 * p + k];
+        for (int k = 0; k < 3; ++k) bf.minv.t[k] = a.prior_Rt[12 * p + 9 + k];
+        for (int k = 0; k < 6; ++k) bf.isig[k] = 1.0 / a.prior_sig[6 * p + k];
+        Rin = a.prior_Rt + 12 * p;
+        tin = a.prior_Rt + 12 * p + 9;
+    }
     Pose X[2];
     for (int k = 0; k < 9; ++k) X[0].R[k] = (k % 4 == 0) ? 1.0 : 0.0;
     X[0].t[0] = X[0].t[1] = X[0].t[2] = 0.0;
@@ -557,10 +659,11 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
         m += __popcll(bal);
     }
     for (int j = lane; j < M; j += 64) out_mask[j] = 0;
-    if (m == 0) {
+    if (m == 0) {  // the initial pose: the prior's when given (two_view_estimator.py:186-187), unit translation
         if (lane == 0) {
+            const double nt = sqrt(tin[0] * tin[0] + tin[1] * tin[1] + tin[2] * tin[2]);
             for (int k = 0; k < 9; ++k) a.R_out[9 * p + k] = Rin[k];
-            for (int k = 0; k < 3; ++k) a.t_out[3 * p + k] = tin[k];
+            for (int k = 0; k < 3; ++k) a.t_out[3 * p + k] = tin[k] / nt;
             a.n_out[p] = 0;
             a.status_out[p] = 1;
             if (a.iters_out) a.iters_out[p] = 0;
@@ -574,7 +677,7 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
     {
         double e = 0;
         for (int j = lane; j < m; j += 64) e += track_error(X, K1, K2, P + 3 * j, UV + 4 * j);
-        err = wave_sum(e) + pose_prior_error(X[0]);  // the point prior is 0 at the start
+        err = wave_sum(e) + pose_prior_error(X[0]) + between_error(bf, X);  // the point prior is 0 at the start
     }
     double lambda = 1e-5;
     int iters = 0;
@@ -583,6 +686,8 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
             const double cur = err;
             double xi0[6];
             pose_log(X[0], xi0);
+            double br[6] = {0, 0, 0, 0, 0, 0}, bJ[72];
+            if (bf.on) between_linearize(bf, X, br, bJ);
             bool accepted = false;
             for (int inner = 0; inner < kInnerMax; ++inner) {
                 // pass 1: reduced camera system, lane-private LDS columns
@@ -628,9 +733,12 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
                         acc[(78 + r) * 64 + lane] += v;
                     }
                 }
+                double brr = 0.0;
+                for (int k = 0; k < 6; ++k) brr += br[k] * br[k];
                 const double oldLin = 0.5 * (wave_sum(oldLin_l) + 100.0 * (xi0[0] * xi0[0] + xi0[1] * xi0[1] +
                                                                          xi0[2] * xi0[2] + xi0[3] * xi0[3] +
-                                                                         xi0[4] * xi0[4] + xi0[5] * xi0[5]));
+                                                                         xi0[4] * xi0[4] + xi0[5] * xi0[5]) +
+                                             brr);
                 const bool any_bad = __ballot(bad) != 0ull;
                 __syncthreads();
                 for (int e = lane; e < kAcc; e += 64) {
@@ -656,6 +764,17 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
                         S[13 * k] += 100.0;
                         s[k] += -xi0[k] * 100.0;
                     }
+                    if (bf.on)  // between factor: A = J, b = -r
+                        for (int a2 = 0; a2 < 12; ++a2) {
+                            for (int b2 = 0; b2 < 12; ++b2) {
+                                double v = 0;
+                                for (int k = 0; k < 6; ++k) v += bJ[12 * k + a2] * bJ[12 * k + b2];
+                                S[12 * a2 + b2] += v;
+                            }
+                            double v = 0;
+                            for (int k = 0; k < 6; ++k) v += bJ[12 * k + a2] * br[k];
+                            s[a2] -= v;
+                        }
                     int ok = any_bad ? 0 : 1;
                     for (int j = 0; j < 12 && ok; ++j) {  // Cholesky
                         double v = S[13 * j];
@@ -735,10 +854,16 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
                         const double v = (dc[k] + xi0[k]) * 10.0;
                         newLin += v * v;
                     }
+                    if (bf.on)
+                        for (int k = 0; k < 6; ++k) {
+                            double v = br[k];
+                            for (int c = 0; c < 12; ++c) v += bJ[12 * k + c] * dc[c];
+                            newLin += v * v;
+                        }
                     newLin *= 0.5;
                     const double linChange = oldLin - newLin;
                     if (linChange >= 0) {
-                        newErr = wave_sum(ne) + pose_prior_error(Xn[0]);
+                        newErr = wave_sum(ne) + pose_prior_error(Xn[0]) + between_error(bf, Xn);
                         const double costChange = err - newErr;
                         if (linChange > kDblEps * oldLin) success = costChange / linChange > kMinFidelity;
                         else success = true;
@@ -790,9 +915,9 @@ __global__ __launch_bounds__(64) void ba2_kernel(Ba2Args a) {
     if (lane == 0) {
         a.n_out[p] = n_valid;
         if (a.iters_out) a.iters_out[p] = iters;
-        if (n_valid == 0) {
-            for (int k = 0; k < 9; ++k) a.R_out[9 * p + k] = Rin[k];
-            for (int k = 0; k < 3; ++k) a.t_out[3 * p + k] = tin[k];
+        if (n_valid == 0) {  // no camera keeps a landmark: the verifier's pose (two_view_estimator.py:199-202)
+            for (int k = 0; k < 9; ++k) a.R_out[9 * p + k] = a.R_in[9 * p + k];
+            for (int k = 0; k < 3; ++k) a.t_out[3 * p + k] = a.t_in[3 * p + k];
             a.status_out[p] = 2;
         } else {
             double R[9], t[3];
@@ -832,7 +957,8 @@ size_t gtsfm_ba2_workspace_bytes(int n_pairs, int mcap) {
 int gtsfm_ba2_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
                       int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
                       const uint8_t* d_in_mask, const double* d_R_in, const double* d_t_in, const int* d_status_in,
-                      int min_inliers, int max_iters, double reproj_thresh, double tri_thresh, void* d_workspace,
+                      const double* d_prior_Rt, const double* d_prior_sigmas, int min_inliers, int max_iters,
+                      double reproj_thresh, double tri_thresh, void* d_workspace,
                       size_t workspace_bytes, double* d_R_out, double* d_t_out, uint8_t* d_out_mask, int* d_n_out,
                       int* d_status_out, int* d_iters, void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
@@ -857,6 +983,8 @@ int gtsfm_ba2_batched(const float* d_kp_xy, const double* d_intrinsics, int n_im
     a.R_in = d_R_in;
     a.t_in = d_t_in;
     a.status_in = d_status_in;
+    a.prior_Rt = d_prior_Rt;
+    a.prior_sig = d_prior_sigmas;
     a.min_inliers = min_inliers;
     a.max_iters = max_iters;
     a.reproj_thresh = reproj_thresh;

@@ -4,7 +4,8 @@
 extern "C" {
 
 // 2.00: gtsfm_ransac_E_batched gained d_n_models; gtsfm_compact_verified added
-int gtsfm_hip_abi_version(void) { return 300; }
+// 3.01: gtsfm_ba2_batched gained the relative-pose prior inputs d_prior_Rt / d_prior_sigmas
+int gtsfm_hip_abi_version(void) { return 301; }
 
 const char* gtsfm_hip_target(void) { return "gfx950"; }
 

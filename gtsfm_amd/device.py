@@ -187,11 +187,18 @@ class BA2Result:
 def bundle_adjust_2view(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch.Tensor, match_idx: torch.Tensor,
                         match_count: torch.Tensor, res: "RansacResult", min_inliers: int = 15, max_iters: int = 100,
                         reproj_thresh: float = 0.5, tri_thresh: float = 100.0,
-                        stream: Optional[torch.cuda.Stream] = None) -> BA2Result:
+                        stream: Optional[torch.cuda.Stream] = None, prior_Rt: Optional[torch.Tensor] = None,
+                        prior_sigmas: Optional[torch.Tensor] = None) -> BA2Result:
     """Two-view triangulation + bundle adjustment of every verified pair (gtsfm_ba2_batched) on the verifier's
-    outputs `res` (same tensors as ransac_essential took)."""
+    outputs `res` (same tensors as ransac_essential took). prior_Rt (P, 12) float64 (i2Ti1 R row-major, t) and
+    prior_sigmas (P, 6) float64: optional relative-pose priors (a row with sigma[0] <= 0 has none)."""
     assert kp_xy.is_cuda and kp_xy.dtype == torch.float32 and kp_xy.is_contiguous()
     assert intrinsics.dtype == torch.float64 and match_idx.dtype == torch.int32 and match_idx.is_contiguous()
+    assert (prior_Rt is None) == (prior_sigmas is None)
+    if prior_Rt is not None:
+        assert prior_Rt.dtype == torch.float64 and prior_Rt.is_contiguous() and prior_Rt.is_cuda
+        assert prior_sigmas.dtype == torch.float64 and prior_sigmas.is_contiguous() and prior_sigmas.is_cuda
+        assert tuple(prior_Rt.shape) == (match_idx.shape[0], 12) and tuple(prior_sigmas.shape) == (match_idx.shape[0], 6)
     n_img, kmax = kp_xy.shape[0], kp_xy.shape[1]
     P, mcap = match_idx.shape[0], match_idx.shape[1]
     dev = kp_xy.device
@@ -208,7 +215,8 @@ def bundle_adjust_2view(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: to
             ws.record_stream(stream)
         rc = L.gtsfm_ba2_batched(_ptr(kp_xy), _ptr(intrinsics), n_img, kmax, _ptr(pairs), P, _ptr(match_idx),
                                  _ptr(match_count), mcap, _ptr(res.mask), _ptr(res.R.contiguous()),
-                                 _ptr(res.t.contiguous()), _ptr(res.status), int(min_inliers), int(max_iters),
+                                 _ptr(res.t.contiguous()), _ptr(res.status), _ptr(prior_Rt), _ptr(prior_sigmas),
+                                 int(min_inliers), int(max_iters),
                                  float(reproj_thresh), float(tri_thresh), _ptr(ws), ws.numel(), _ptr(R), _ptr(t),
                                  _ptr(mask), _ptr(n_out), _ptr(st), _ptr(iters), native.stream_handle(stream))
         native.check(rc, "gtsfm_ba2_batched")

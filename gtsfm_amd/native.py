@@ -106,8 +106,8 @@ SIGNATURES = {
     "gtsfm_ba2_batched": (
         c_int,
         [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p,
-         c_void_p, c_int, c_int, c_double, c_double, c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p,
-         c_void_p, c_void_p, c_void_p],
+         c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_double, c_void_p, c_size_t, c_void_p, c_void_p,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     "gtsfm_sampson_sq_batched": (
         c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

@@ -9,7 +9,8 @@ goes through ONE batched RANSAC launch sequence (Ransac.verify_batch), then -- w
 every shipped configuration -- ONE batched two-view triangulation + bundle adjustment launch
 (gtsfm_ba2_batched: `bundle_adjust`, :136-208, on the pairs with >= min_num_inliers verified rows, :311), and only
 the cheap report / ISP logic runs per pair on the host. After BA the report keeps the pre-BA inlier ratio, as the
-reference does (:325-327). Relative-pose priors on the BA path are not supported (the runner passes none).
+reference does (:325-327). Relative-pose priors (PosePrior, :165,192) go to the BA kernel per pair: the prior
+initialises the second camera and adds a between factor (gtsfm_ba2_batched's d_prior_Rt / d_prior_sigmas).
 """
 from __future__ import annotations
 
@@ -115,20 +116,26 @@ class TwoViewEstimator:
                 1e300 if tri is None or math.isinf(tri) else float(tri))
 
     def bundle_adjust_batch(self, keypoints_list: Sequence[Keypoints],
-                            jobs: Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]], camera_intrinsics: Sequence
+                            jobs: Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]], camera_intrinsics: Sequence,
+                            priors: Optional[Dict[Tuple[int, int], Any]] = None
                             ) -> Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]]:
         """bundle_adjust (:136-208) of every (i1, i2) -> (i2Ri1, i2Ui1, verified_corr_idxs) job in batched
         gtsfm_ba2_batched launches; returns (i2Ri1, i2Ui1, valid_corr_idxs) per job, as the reference returns them:
-        the initial pose and an empty (0, 2) int32 array when nothing triangulates, the initial pose and the (empty)
-        valid rows when BA leaves no valid track."""
+        the initial pose (the prior's when the job has one) and an empty (0, 2) int32 array when nothing
+        triangulates, the verifier's pose and the (empty) valid rows when BA leaves no valid track. priors: optional
+        (i1, i2) -> PosePrior (i2Ti1_prior)."""
         import torch
 
         from gtsfm_amd import device, native
 
         native.require_gpu()
         _, max_iters, thr, tri = self._ba_params()
+        from gtsfm_amd.common.pose_prior import prior_arrays
+
+        priors = {k: v for k, v in (priors or {}).items() if v is not None}
         out: Dict[Tuple[int, int], Tuple[Any, Any, np.ndarray]] = {}
-        keys = [k for k, (R, U, _) in jobs.items() if R is not None and U is not None]
+        # the initial pose is the prior's when given, else the verifier's (:165-171); neither: nothing to adjust
+        keys = [k for k, (R, U, _) in jobs.items() if (R is not None and U is not None) or k in priors]
         for k in jobs:
             if k not in keys:
                 out[k] = (None, None, jobs[k][2])
@@ -158,23 +165,36 @@ class TwoViewEstimator:
             mask = np.zeros((len(blk), mcap), np.uint8)
             R0 = np.zeros((len(blk), 3, 3))
             t0 = np.zeros((len(blk), 3))
+            pRt = np.zeros((len(blk), 12))
+            psg = np.zeros((len(blk), 6))
             for j, (k, r) in enumerate(zip(blk, rows)):
                 idx[j, : len(r)] = r.astype(np.int64)
                 cnt[j] = len(r)
                 mask[j, : len(r)] = 1
-                R0[j] = geometry.rotation_matrix(jobs[k][0])
-                t0[j] = geometry.unit_vector(jobs[k][1])
+                if k in priors:
+                    Rp, tp, sp = prior_arrays(priors[k])
+                    pRt[j, :9], pRt[j, 9:], psg[j] = Rp.ravel(), tp, sp
+                if jobs[k][0] is not None and jobs[k][1] is not None:
+                    R0[j] = geometry.rotation_matrix(jobs[k][0])
+                    t0[j] = geometry.unit_vector(jobs[k][1])
+                else:  # prior only: the kernel initialises from the prior
+                    R0[j] = pRt[j, :9].reshape(3, 3)
+                    t0[j] = pRt[j, 9:] / np.linalg.norm(pRt[j, 9:])
             v = _Verified()
             v.mask, v.R, v.t = (torch.from_numpy(x).to(dev) for x in (mask, R0, t0))
             v.status = torch.zeros(len(blk), dtype=torch.int32, device=dev)
+            has_prior = bool(psg[:, 0].any())
             res = device.bundle_adjust_2view(kp_d, intr_d, torch.tensor(blk, dtype=torch.int32, device=dev),
                                              torch.from_numpy(idx).to(dev), torch.from_numpy(cnt).to(dev), v,
-                                             min_inliers=0, max_iters=max_iters, reproj_thresh=thr, tri_thresh=tri)
+                                             min_inliers=0, max_iters=max_iters, reproj_thresh=thr, tri_thresh=tri,
+                                             prior_Rt=torch.from_numpy(pRt).to(dev) if has_prior else None,
+                                             prior_sigmas=torch.from_numpy(psg).to(dev) if has_prior else None)
             st = res.ba_status.cpu().numpy()
             R, t, m = res.R.cpu().numpy(), res.t.cpu().numpy(), res.mask.cpu().numpy().astype(bool)
             for j, (k, r) in enumerate(zip(blk, rows)):
-                if st[j] == native.BA2_STATUS_NO_TRACKS:
-                    out[k] = (jobs[k][0], jobs[k][1], np.zeros((0, 2), dtype=np.int32))
+                if st[j] == native.BA2_STATUS_NO_TRACKS:  # the initial pose (:186-187): the prior's when given
+                    init = (geometry.Rot3(R[j]), geometry.Unit3(t[j])) if k in priors else (jobs[k][0], jobs[k][1])
+                    out[k] = (init[0], init[1], np.zeros((0, 2), dtype=np.int32))
                 elif st[j] == native.BA2_STATUS_NONE_VALID:
                     out[k] = (jobs[k][0], jobs[k][1], np.asarray(jobs[k][2]).reshape(-1, 2)[:0])
                 else:
@@ -185,13 +205,12 @@ class TwoViewEstimator:
     def bundle_adjust(self, keypoints_i1: Keypoints, keypoints_i2: Keypoints, verified_corr_idxs: np.ndarray,
                       camera_intrinsics_i1, camera_intrinsics_i2, i2Ri1_initial, i2Ui1_initial, i2Ti1_prior=None):
         """Drop-in for TwoViewEstimator.bundle_adjust (:136-208): one pair through the batched kernel."""
-        if i2Ti1_prior is not None:
-            raise NotImplementedError("relative pose priors are not supported on the MI355X two-view BA path")
-        if i2Ri1_initial is None or i2Ui1_initial is None:
+        if i2Ti1_prior is None and (i2Ri1_initial is None or i2Ui1_initial is None):
             return None, None, verified_corr_idxs
         return self.bundle_adjust_batch([keypoints_i1, keypoints_i2],
                                         {(0, 1): (i2Ri1_initial, i2Ui1_initial, verified_corr_idxs)},
-                                        [camera_intrinsics_i1, camera_intrinsics_i2])[(0, 1)]
+                                        [camera_intrinsics_i1, camera_intrinsics_i2],
+                                        priors={(0, 1): i2Ti1_prior})[(0, 1)]
 
     def _wants_ba(self, v_corr) -> bool:
         return self._bundle_adjust_2view and len(v_corr) >= self.processor._min_num_inliers_est_model
@@ -276,9 +295,9 @@ def run_two_view_estimator_as_futures(
     post_ba: Dict[Tuple[int, int], Any] = {}
     ba_jobs = {k: verified[k][:3] for k in todo if two_view_estimator._wants_ba(verified[k][2])}
     if ba_jobs:
-        if any((relative_pose_priors or {}).get(k) is not None for k in ba_jobs):
-            raise NotImplementedError("relative pose priors are not supported on the MI355X two-view BA path")
-        post_ba = two_view_estimator.bundle_adjust_batch(keypoints_list, ba_jobs, camera_intrinsics)
+        post_ba = two_view_estimator.bundle_adjust_batch(keypoints_list, ba_jobs, camera_intrinsics,
+                                                         priors={k: (relative_pose_priors or {}).get(k)
+                                                                 for k in ba_jobs})
     for (i1, i2), m in todo.items():
         results[(i1, i2)] = two_view_estimator._finish(verified[(i1, i2)], keypoints_list[i1], keypoints_list[i2],
                                                        gt[i1], gt[i2], gt_scene_mesh, post_ba.get((i1, i2)))

@@ -152,7 +152,11 @@ int gtsfm_ransac_F_batched(const float* d_kp_xy, const double* d_intrinsics, int
  * oracle/ba2.c (calibrations held fixed; the reference's sigma 1e-5 prior pins them).
  * Inputs: the verifier's keypoints / intrinsics / pairs / putatives exactly as gtsfm_ransac_E_batched takes them,
  * its inlier mask d_in_mask[n_pairs][mcap] (the pre-BA verified rows), i2Ri1 d_R_in[n_pairs][9], unit i2ti1
- * d_t_in[n_pairs][3] and status d_status_in (0 = verified). Per pair with status 0 and >= min_inliers verified rows:
+ * d_t_in[n_pairs][3] and status d_status_in (0 = verified). Optional relative-pose priors (two_view_estimator.py:165,
+ * 192: bundle_adjust's i2Ti1_prior): d_prior_Rt[n_pairs][12] = the prior's i2Ti1 (R row-major, then t) and
+ * d_prior_sigmas[n_pairs][6] its sigmas (PosePrior.covariance, rotation first); a pair with sigma[0] <= 0 has none,
+ * both NULL = no priors. A prior initialises the second camera and adds BetweenFactorPose3(X0, X1, prior^-1)
+ * (bundle_adjustment.py:136-152). Per pair with status 0 and >= min_inliers verified rows:
  * every verified row is triangulated (DLT + LM point refinement, cheirality, reprojection < tri_thresh px), the
  * 2-view BA runs (Huber 1.345 on 1 px, X0 prior 0.1, first-point prior 0.1, Levenberg-Marquardt <= max_iters
  * iterations), and rows whose two reprojections stay < reproj_thresh px survive (filter_landmarks).
@@ -166,7 +170,8 @@ size_t gtsfm_ba2_workspace_bytes(int n_pairs, int mcap);
 int gtsfm_ba2_batched(const float* d_kp_xy, const double* d_intrinsics, int n_img, int kmax, const int* d_pairs,
                       int n_pairs, const uint32_t* d_match_idx, const int* d_match_count, int mcap,
                       const uint8_t* d_in_mask, const double* d_R_in, const double* d_t_in, const int* d_status_in,
-                      int min_inliers, int max_iters, double reproj_thresh, double tri_thresh, void* d_workspace,
+                      const double* d_prior_Rt, const double* d_prior_sigmas, int min_inliers, int max_iters,
+                      double reproj_thresh, double tri_thresh, void* d_workspace,
                       size_t workspace_bytes, double* d_R_out, double* d_t_out, uint8_t* d_out_mask, int* d_n_out,
                       int* d_status_out, int* d_iters, void* stream);
 

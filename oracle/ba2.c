@@ -152,6 +152,99 @@ static void pose_log(const pose_t* T, double* xi) {
     for (int k = 0; k < 3; ++k) xi[3 + k] = T->t[k] - (0.5 * th) * Wt[k] + (1.0 - th / (2.0 * tn)) * WWt[k];
 }
 
+/* ------------------------------------------------------------------ relative-pose prior
+ * BetweenFactorPose3(X0, X1, m, Diagonal.Sigmas(sigmas)) with m = i2Ti1_prior.value.inverse()
+ * (bundle_adjustment.py:136-152; two_view_estimator.py:165,192 passes the prior). GTSAM's error is
+ * e = Pose3::Logmap(m^-1 * X0^-1 * X1) (Local of the Expmap chart), whitened by 1 / sigma. With X_c <- X_c Exp(d_c):
+ * de/dd1 = Jr^-1(e), de/dd0 = -Jr^-1(e) Ad(hx^-1), hx = X0^-1 X1; Jr^-1(e) is taken to second order,
+ * I + ad(e) / 2 + ad(e)^2 / 12 (exact to O(|e|^4)); ad((w, v)) = [[w^, 0], [v^, w^]], Ad((R, t)) = [[R, 0], [t^ R, R]]. */
+typedef struct {
+    int on;
+    pose_t minv;    /* m^-1 = i2Ti1_prior (the prior's value itself) */
+    double isig[6]; /* 1 / sigma, GTSAM tangent order (rotation, translation) */
+} between_t;
+
+static void pose_mul(const pose_t* A, const pose_t* B, pose_t* C) {
+    pose_t o;
+    mm3(A->R, B->R, o.R);
+    mv3(A->R, B->t, o.t);
+    for (int k = 0; k < 3; ++k) o.t[k] += A->t[k];
+    *C = o;
+}
+
+static void pose_inv(const pose_t* A, pose_t* C) {
+    pose_t o;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) o.R[3 * i + j] = A->R[3 * j + i];
+    mtv3(A->R, A->t, o.t);
+    for (int k = 0; k < 3; ++k) o.t[k] = -o.t[k];
+    *C = o;
+}
+
+/* unwhitened residual e (6) and hx = X0^-1 X1 */
+static void between_residual(const between_t* f, const pose_t* X, double* e, pose_t* hx) {
+    pose_t x0i, E0;
+    pose_inv(&X[0], &x0i);
+    pose_mul(&x0i, &X[1], hx);
+    pose_mul(&f->minv, hx, &E0);
+    pose_log(&E0, e);
+}
+
+static double between_error(const between_t* f, const pose_t* X) {
+    if (!f->on) return 0.0;
+    double e[6];
+    pose_t hx;
+    between_residual(f, X, e, &hx);
+    double s = 0;
+    for (int k = 0; k < 6; ++k) s += (e[k] * f->isig[k]) * (e[k] * f->isig[k]);
+    return 0.5 * s;
+}
+
+/* whitened residual r (6) and Jacobian J (6 x 12, columns: X0 then X1) at X */
+static void between_linearize(const between_t* f, const pose_t* X, double* r, double* J) {
+    double e[6];
+    pose_t hx, hi;
+    between_residual(f, X, e, &hx);
+    double ad[36], ad2[36], Ji[36], Ad[36];
+    memset(ad, 0, sizeof(ad));
+    double Ws[9], Vs[9];
+    skew3(e, Ws);
+    skew3(e + 3, Vs);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            ad[6 * i + j] = Ws[3 * i + j];
+            ad[6 * (3 + i) + j] = Vs[3 * i + j];
+            ad[6 * (3 + i) + 3 + j] = Ws[3 * i + j];
+        }
+    for (int i = 0; i < 6; ++i)
+        for (int j = 0; j < 6; ++j) {
+            double a = 0;
+            for (int k = 0; k < 6; ++k) a += ad[6 * i + k] * ad[6 * k + j];
+            ad2[6 * i + j] = a;
+        }
+    for (int k = 0; k < 36; ++k) Ji[k] = (k % 7 == 0 ? 1.0 : 0.0) + 0.5 * ad[k] + ad2[k] / 12.0;
+    pose_inv(&hx, &hi);
+    memset(Ad, 0, sizeof(Ad));
+    double T[9], TR[9];
+    skew3(hi.t, T);
+    mm3(T, hi.R, TR);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Ad[6 * i + j] = hi.R[3 * i + j];
+            Ad[6 * (3 + i) + 3 + j] = hi.R[3 * i + j];
+            Ad[6 * (3 + i) + j] = TR[3 * i + j];
+        }
+    for (int i = 0; i < 6; ++i) {
+        for (int j = 0; j < 6; ++j) {
+            double a = 0;
+            for (int k = 0; k < 6; ++k) a += Ji[6 * i + k] * Ad[6 * k + j];
+            J[12 * i + j] = -a * f->isig[i];
+            J[12 * i + 6 + j] = Ji[6 * i + j] * f->isig[i];
+        }
+        r[i] = e[i] * f->isig[i];
+    }
+}
+
 /* camera (pose X, calibration f,u0,v0, k1 = k2 = 0) projection; 0 on cheirality failure (z <= 0) */
 static int project(const pose_t* X, const double* K, const double* p, double* pc, double* uv) {
     const double d[3] = {p[0] - X->t[0], p[1] - X->t[1], p[2] - X->t[2]};
@@ -396,7 +489,7 @@ int oracle_triangulate2(const pose_t* X0, const pose_t* X1, const double* K1, co
 
 /* total nonlinear error: Huber reprojection losses + X0 prior + P0 prior */
 static double ba_error(const pose_t* X, const double* K1, const double* K2, const double* P, const double* uv1,
-                       const double* uv2, int n, const double* P0_prior) {
+                       const double* uv2, int n, const double* P0_prior, const between_t* bf) {
     const double* K[2] = {K1, K2};
     double err = 0;
     for (int j = 0; j < n; ++j) {
@@ -416,7 +509,7 @@ static double ba_error(const pose_t* X, const double* K1, const double* K2, cons
     s = 0;
     for (int k = 0; k < 3; ++k) s += (P[k] - P0_prior[k]) * (P[k] - P0_prior[k]);
     err += 0.5 * s / 0.01;
-    return err;
+    return err + between_error(bf, X);
 }
 
 /* one point's whitened, Huber-reweighted factor blocks at the current values */
@@ -454,19 +547,38 @@ static void linearize_point(const pose_t* X, const double* K1, const double* K2,
  * R_in / t_in: i2Ri1 and the unit i2ti1 of the verifier. R_out / t_out: i2Ri1 and unit i2ti1 after BA (the input
  * pose for statuses 1 and 2). valid[j]: correspondence j survives triangulation + BA + filtering. */
 int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, const double* K2, const double* R_in,
-               const double* t_in, int max_iters, double reproj_thresh, double tri_thresh, double* R_out,
-               double* t_out, uint8_t* valid, int* iters_out, double* error_out) {
+               const double* t_in, int max_iters, double reproj_thresh, double tri_thresh, const double* prior_Rt,
+               const double* prior_sigmas, double* R_out, double* t_out, uint8_t* valid, int* iters_out,
+               double* error_out) {
     memcpy(R_out, R_in, 9 * sizeof(double));
     memcpy(t_out, t_in, 3 * sizeof(double));
     memset(valid, 0, (size_t)n);
     if (iters_out) *iters_out = 0;
+    /* relative-pose prior i2Ti1_prior = (R, t) (prior_Rt: R row-major then t; NULL = none): it initialises the
+     * second camera instead of the verifier's pose (two_view_estimator.py:165-171) and adds the between factor */
+    between_t bf;
+    memset(&bf, 0, sizeof(bf));
+    const double* Ri = R_in;
+    const double* ti = t_in;
+    if (prior_Rt && prior_sigmas) {
+        bf.on = 1;
+        memcpy(bf.minv.R, prior_Rt, 9 * sizeof(double));
+        memcpy(bf.minv.t, prior_Rt + 9, 3 * sizeof(double));
+        for (int k = 0; k < 6; ++k) bf.isig[k] = 1.0 / prior_sigmas[k];
+        Ri = prior_Rt;
+        ti = prior_Rt + 9;
+        /* no track: the reference returns the initial pose, i.e. the prior's (two_view_estimator.py:186-187) */
+        memcpy(R_out, Ri, 9 * sizeof(double));
+        const double nt = sqrt(ti[0] * ti[0] + ti[1] * ti[1] + ti[2] * ti[2]);
+        for (int k = 0; k < 3; ++k) t_out[k] = ti[k] / nt;
+    }
     pose_t X[2];
     memset(&X[0], 0, sizeof(pose_t));
     X[0].R[0] = X[0].R[4] = X[0].R[8] = 1.0;
     /* X1 = i2Ti1^-1: R^T, -R^T t */
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) X[1].R[3 * i + j] = R_in[3 * j + i];
-    mtv3(R_in, t_in, X[1].t);
+        for (int j = 0; j < 3; ++j) X[1].R[3 * i + j] = Ri[3 * j + i];
+    mtv3(Ri, ti, X[1].t);
     for (int i = 0; i < 3; ++i) X[1].t[i] = -X[1].t[i];
     /* triangulate every correspondence */
     int* tri = (int*)malloc(sizeof(int) * (size_t)(n > 0 ? n : 1));
@@ -489,7 +601,7 @@ int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, co
     const double P0_prior[3] = {P[0], P[1], P[2]};
     double* Pn = (double*)malloc(sizeof(double) * 3 * (size_t)m);
     pt_lin_t* lin = (pt_lin_t*)malloc(sizeof(pt_lin_t) * (size_t)m);
-    double err = ba_error(X, K1, K2, P, u1, u2, m, P0_prior);
+    double err = ba_error(X, K1, K2, P, u1, u2, m, P0_prior, &bf);
     double lambda = 1e-5;
     int iters = 0;
     if (err > 0.0) {
@@ -504,6 +616,11 @@ int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, co
                 for (int c = 0; c < 2; ++c) oldLin += lin[j].b[c][0] * lin[j].b[c][0] + lin[j].b[c][1] * lin[j].b[c][1];
             for (int k = 0; k < 6; ++k) oldLin += xi0[k] * xi0[k] / 0.01;
             for (int k = 0; k < 3; ++k) oldLin += (P[k] - P0_prior[k]) * (P[k] - P0_prior[k]) / 0.01;
+            double br[6] = {0, 0, 0, 0, 0, 0}, bJ[72];
+            if (bf.on) {
+                between_linearize(&bf, X, br, bJ);
+                for (int k = 0; k < 6; ++k) oldLin += br[k] * br[k];
+            }
             oldLin *= 0.5;
             for (;;) {
                 /* reduced camera system S dc = s (Schur complement on the points) */
@@ -515,6 +632,17 @@ int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, co
                     S[13 * k] += 100.0;
                     s[k] += -xi0[k] * 100.0;
                 }
+                if (bf.on) /* between factor: A = J, b = -r */
+                    for (int a = 0; a < 12; ++a) {
+                        for (int b2 = 0; b2 < 12; ++b2) {
+                            double v = 0;
+                            for (int k = 0; k < 6; ++k) v += bJ[12 * k + a] * bJ[12 * k + b2];
+                            S[12 * a + b2] += v;
+                        }
+                        double v = 0;
+                        for (int k = 0; k < 6; ++k) v += bJ[12 * k + a] * br[k];
+                        s[a] -= v;
+                    }
                 int ok = 1;
                 for (int j = 0; j < m && ok; ++j) {
                     const pt_lin_t* L = &lin[j];
@@ -613,12 +741,18 @@ int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, co
                         const double a = (s[k] + xi0[k]) * 10.0;
                         newLin += a * a;
                     }
+                    if (bf.on)
+                        for (int k = 0; k < 6; ++k) {
+                            double a = br[k];
+                            for (int c = 0; c < 12; ++c) a += bJ[12 * k + c] * s[c];
+                            newLin += a * a;
+                        }
                     newLin *= 0.5;
                     const double linChange = oldLin - newLin;
                     if (linChange >= 0) {
                         pose_retract(&X[0], s, &Xn[0]);
                         pose_retract(&X[1], s + 6, &Xn[1]);
-                        newErr = ba_error(Xn, K1, K2, Pn, u1, u2, m, P0_prior);
+                        newErr = ba_error(Xn, K1, K2, Pn, u1, u2, m, P0_prior, &bf);
                         const double costChange = err - newErr;
                         if (linChange > DBL_EPSILON * oldLin) success = costChange / linChange > LM_MIN_FIDELITY;
                         else success = 1;
@@ -662,7 +796,11 @@ int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, co
         }
     }
     free(tri); free(P); free(u1); free(u2); free(Pn); free(lin);
-    if (n_valid == 0) return 2;
+    if (n_valid == 0) { /* no camera keeps a landmark: the verifier's pose (two_view_estimator.py:199-202) */
+        memcpy(R_out, R_in, 9 * sizeof(double));
+        memcpy(t_out, t_in, 3 * sizeof(double));
+        return 2;
+    }
     /* i2Ti1 = wTi2^-1 wTi1 */
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j)

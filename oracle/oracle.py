@@ -65,8 +65,8 @@ def _register_optional(l: ctypes.CDLL) -> None:
     if hasattr(l, "oracle_ba2"):
         l.oracle_ba2.restype = ctypes.c_int
         l.oracle_ba2.argtypes = [_f64p, _f64p, ctypes.c_int, _f64p, _f64p, _f64p, _f64p, ctypes.c_int, ctypes.c_double,
-                                 ctypes.c_double, _f64p, _f64p, _u8p, ctypes.POINTER(ctypes.c_int),
-                                 ctypes.POINTER(ctypes.c_double)]
+                                 ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, _f64p, _f64p, _u8p,
+                                 ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
     if hasattr(l, "oracle_ransac_F"):
         l.oracle_ransac_F.restype = ctypes.c_int
         l.oracle_ransac_F.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
@@ -221,18 +221,26 @@ def recover_pose(E: np.ndarray, x1n: np.ndarray, x2n: np.ndarray):
 
 
 def ba2(uv1: np.ndarray, uv2: np.ndarray, K1, K2, R: np.ndarray, t: np.ndarray, max_iters: int = 100,
-        reproj_thresh: float = 0.5, tri_thresh: float = 100.0):
+        reproj_thresh: float = 0.5, tri_thresh: float = 100.0, prior_R: Optional[np.ndarray] = None,
+        prior_t: Optional[np.ndarray] = None, prior_sigmas: Optional[np.ndarray] = None):
     """Two-view triangulation + bundle adjustment (oracle/ba2.c). K = (f, u0, v0). Returns
-    (status, R_out, t_out, valid (n,) bool, LM iterations, final error); status 0 ok / 1 no track / 2 none valid."""
+    (status, R_out, t_out, valid (n,) bool, LM iterations, final error); status 0 ok / 1 no track / 2 none valid.
+    prior_R / prior_t / prior_sigmas: an i2Ti1 relative-pose prior (PosePrior value and sigmas, rotation first)."""
     uv1 = np.ascontiguousarray(uv1, np.float64).reshape(-1, 2)
     uv2 = np.ascontiguousarray(uv2, np.float64).reshape(-1, 2)
     n = len(uv1)
     Ro, to = np.zeros(9), np.zeros(3)
     valid = np.zeros(max(n, 1), np.uint8)
     it, err = ctypes.c_int(0), ctypes.c_double(0)
+    prt = psg = None
+    if prior_R is not None:
+        prt = np.concatenate([np.asarray(prior_R, np.float64).ravel(), np.asarray(prior_t, np.float64).ravel()])
+        psg = np.ascontiguousarray(prior_sigmas, np.float64).ravel()
     st = lib().oracle_ba2(uv1.ravel(), uv2.ravel(), n, np.asarray(K1, np.float64), np.asarray(K2, np.float64),
                           np.ascontiguousarray(R, np.float64).ravel(), np.ascontiguousarray(t, np.float64).ravel(),
-                          max_iters, reproj_thresh, tri_thresh, Ro, to, valid, ctypes.byref(it), ctypes.byref(err))
+                          max_iters, reproj_thresh, tri_thresh, None if prt is None else prt.ctypes.data,
+                          None if psg is None else psg.ctypes.data, Ro, to, valid, ctypes.byref(it),
+                          ctypes.byref(err))
     return st, Ro.reshape(3, 3), to, valid[:n].astype(bool), it.value, err.value
 
 

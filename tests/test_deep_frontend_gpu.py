@@ -89,6 +89,8 @@ def test_engine_deep_kernels_vs_plugins_and_oracle(views, oracle_mod, matcher):
     m_plugin = sg if matcher == "superglue" else TwoWayMatcher(ratio_test_threshold=0.8)
     views_idx = [0, 1, 2, 3, 5, 8]
     verified_adjacent = 0
+    diag = [(views_idx[int(a)], views_idx[int(b)], int(res.n_matches[q]), int(res.status[q]), int(res.n_inliers[q]),
+             bool(res.isp_ok[q])) for q, (a, b) in enumerate(res.pairs)]
     for p, (i1, i2) in enumerate(res.pairs):
         i1, i2 = int(i1), int(i2)
         m = np.asarray(m_plugin.match(per[i1][0], per[i2][0], per[i1][1], per[i2][1], arr[i1].shape,
@@ -119,4 +121,4 @@ def test_engine_deep_kernels_vs_plugins_and_oracle(views, oracle_mod, matcher):
             R_gt, t_gt = sc.relative_pose(views_idx[i1], views_idx[i2])
             assert scenes.rotation_angle_deg(res.R[p], R_gt) < 2.0, p
     # the C5 / C3 slice carries real matches into RANSAC: adjacent views (11.25 degrees apart) verify
-    assert verified_adjacent >= 2, verified_adjacent
+    assert verified_adjacent >= 2, (verified_adjacent, diag)

@@ -68,3 +68,46 @@ def test_falsy_maxiters_maps_to_gtsam_default():
                                ba_reproj_error_thresholds=[None])
         _, max_iters, thr, _ = tve._ba_params()
         assert max_iters == 100 and np.isinf(thr)
+
+
+def _rotated(R, deg, axis=(0.0, 0.0, 1.0)):
+    from scipy.spatial.transform import Rotation
+
+    a = np.asarray(axis) / np.linalg.norm(axis)
+    return Rotation.from_rotvec(np.deg2rad(deg) * a).as_matrix() @ R
+
+
+def test_relative_pose_prior_moves_the_solution(oracle_mod):
+    """bundle_adjust with i2Ti1_prior (two_view_estimator.py:165,192): the prior initialises the second camera and a
+    BetweenFactorPose3 (sigmas, rotation first) pulls the estimate toward it. A tight prior 2 degrees off the truth
+    drags the result most of the way to the prior; a loose one leaves the no-prior result; a prior at the truth does
+    no harm."""
+    rng = np.random.default_rng(9)
+    s = ba2_scenes.make_pair(rng, 200, noise_px=0.5, init_err_deg=0.0)
+    args = (s["x1"], s["x2"], s["K"], s["K"], s["R0"], s["t0"])
+    st0, R0, t0, v0, it0, _ = oracle_mod.ba2(*args)
+    assert st0 == 0
+    Rp = _rotated(s["R"], 2.0)
+    tight = np.array([1e-4, 1e-4, 1e-4, 1e-2, 1e-2, 1e-2])
+    st1, R1, t1, v1, it1, _ = oracle_mod.ba2(*args, prior_R=Rp, prior_t=s["t"], prior_sigmas=tight)
+    assert st1 == 0
+    assert ba2_scenes.angle_deg(R1, Rp) < 0.2 < ba2_scenes.angle_deg(R0, Rp)
+    loose = np.full(6, 1e3)
+    st2, R2, t2, v2, _, _ = oracle_mod.ba2(*args, prior_R=Rp, prior_t=s["t"], prior_sigmas=loose)
+    assert st2 == 0 and ba2_scenes.angle_deg(R2, R0) < 0.05 and ba2_scenes.dir_deg(t2, t0) < 0.1
+    st3, R3, t3, _, _, _ = oracle_mod.ba2(*args, prior_R=s["R"], prior_t=s["t"], prior_sigmas=np.full(6, 0.01))
+    assert st3 == 0 and ba2_scenes.angle_deg(R3, s["R"]) <= ba2_scenes.angle_deg(R0, s["R"]) + 1e-3
+
+
+def test_relative_pose_prior_returned_when_nothing_triangulates(oracle_mod):
+    """No track: the reference returns the initial pose, which is the prior's when one is given
+    (two_view_estimator.py:165-187)."""
+    rng = np.random.default_rng(10)
+    s = ba2_scenes.make_pair(rng, 40, noise_px=0.0)
+    Rp = _rotated(s["R"], 1.0)
+    # the prior points the baseline backwards: every point falls behind a camera
+    st, R, t, valid, _, _ = oracle_mod.ba2(s["x1"], s["x2"], s["K"], s["K"], s["R"], s["t"], prior_R=Rp,
+                                           prior_t=-s["t"] * 50.0, prior_sigmas=np.full(6, 0.1))
+    if st == 1:
+        np.testing.assert_allclose(R, Rp)
+        np.testing.assert_allclose(t, -s["t"] / np.linalg.norm(s["t"]))
