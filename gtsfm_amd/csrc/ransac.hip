@@ -169,6 +169,10 @@ __device__ __forceinline__ RootMem root_mem(unsigned char* smem, int lane) {
 // the padded row equals Horner from the row's true degree bit for bit (leading zeros contribute exact zeros), and
 // rows past the chain length evaluate to 0 and are skipped exactly like the oracle's loop bound.
 constexpr int kChain = 66;
+#ifndef GTSFM_ROOT_GROUP
+#define GTSFM_ROOT_GROUP 4  // root slots bisected / polished together (independent Horner chains)
+#endif
+constexpr int kRootGroup = GTSFM_ROOT_GROUP;
 __device__ __forceinline__ constexpr int row_off(int k) { return 11 * k - k * (k - 1) / 2; }
 
 __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], double x) {
@@ -212,16 +216,31 @@ __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
 // bisected together (10 independent chains), so a wave never serialises one lane's bisection behind another's
 // isolation step.
 template <typename RootFn>
-__device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_root) {
+__device__ int real_roots(const double (&pin)[11], int deg, RootMem m, RootFn&& on_root) {
     RPROF_DECL
     LaneArr<double> S = m.u;  // chain row k in slot k % 3 (11 doubles each) while it is still needed by prem
     LaneArr<double> t = m.u.at(33);
     LaneArr<uint8_t> sdeg = m.b.at(2 * kStack);
-    while (deg > 0 && fabs(pin[deg]) <= 1e-300) --deg;
+    // the coefficients stay in registers: every index below is static (the degree only selects)
+    double lead = pin[0];
+#pragma unroll
+    for (int i = 1; i < 11; ++i) lead = i == deg ? pin[i] : lead;
+#pragma unroll
+    for (int i = 10; i >= 1; --i) {
+        if (i > deg) continue;
+        if (i == deg && fabs(lead) <= 1e-300) {
+            --deg;
+            lead = pin[i - 1];
+        }
+    }
     if (deg <= 0) return 0;
-    for (int i = 0; i <= deg; ++i) S[i] = pin[i] / pin[deg];
+#pragma unroll
+    for (int i = 0; i < 11; ++i)
+        if (i <= deg) S[i] = pin[i] / lead;
     sdeg[0] = (uint8_t)deg;
-    for (int i = 1; i <= deg; ++i) S[11 + i - 1] = (double)i * S[i];
+#pragma unroll
+    for (int i = 1; i < 11; ++i)
+        if (i <= deg) S[11 + i - 1] = (double)i * S[i];
     sdeg[1] = (uint8_t)(deg - 1);
     // register chain: rows 0 and 1 now, row n as soon as prem produces it (rows past the chain stay 0)
     double R[kChain];
@@ -306,19 +325,26 @@ __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_roo
 #pragma unroll
     for (int k = 0; k < kMaxSol; ++k) live |= (k < nr ? 1u : 0u) << k;
     const unsigned all_roots = live;
+    // Slots are visited in groups of kRootGroup: a group is skipped only when no lane has a live root in it, and
+    // inside a group every slot is evaluated unconditionally (results kept by `go`), so the group's Horner chains
+    // are independent instructions the scheduler interleaves. Per slot the arithmetic is unchanged.
     for (int it = 0; it < 80; ++it) {
         if (!__any(live != 0)) break;
 #pragma unroll
-        for (int k = 0; k < kMaxSol; ++k) {
-            if (!__any((live >> k) & 1u)) continue;
-            const bool go = ((live >> k) & 1u) && hi[k] - lo[k] > 0x1p-20 * fmax(1.0, fmax(fabs(lo[k]), fabs(hi[k])));
-            if (!go) live &= ~(1u << k);
-            const double mid = 0.5 * (lo[k] + hi[k]);
-            const double fm = peval0(R, mid);
-            const bool left = (fm < 0.0) == (flo[k] < 0.0) && fm != 0.0;
-            lo[k] = go && left ? mid : lo[k];
-            flo[k] = go && left ? fm : flo[k];
-            hi[k] = go && !left ? mid : hi[k];
+        for (int g = 0; g < kMaxSol; g += kRootGroup) {
+            if (!__any((live >> g) & ((1u << kRootGroup) - 1u))) continue;
+#pragma unroll
+            for (int k = g; k < g + kRootGroup && k < kMaxSol; ++k) {
+                const bool go =
+                    ((live >> k) & 1u) && hi[k] - lo[k] > 0x1p-20 * fmax(1.0, fmax(fabs(lo[k]), fabs(hi[k])));
+                if (!go) live &= ~(1u << k);
+                const double mid = 0.5 * (lo[k] + hi[k]);
+                const double fm = peval0(R, mid);
+                const bool left = (fm < 0.0) == (flo[k] < 0.0) && fm != 0.0;
+                lo[k] = go && left ? mid : lo[k];
+                flo[k] = go && left ? fm : flo[k];
+                hi[k] = go && !left ? mid : hi[k];
+            }
         }
     }
     RPROF(9);
@@ -328,18 +354,21 @@ __device__ int real_roots(const double* pin, int deg, RootMem m, RootFn&& on_roo
     live = all_roots;
     for (int it = 0; it < 4; ++it) {
 #pragma unroll
-        for (int k = 0; k < kMaxSol; ++k) {
-            if (!__any((live >> k) & 1u)) continue;
-            const double fx = peval0(R, xr[k]), dfx = peval1(R, xr[k]);
-            const bool go = ((live >> k) & 1u) && fx != 0.0;
-            if (!go) live &= ~(1u << k);
-            const bool left = (fx < 0.0) == (flo[k] < 0.0);
-            lo[k] = go && left ? xr[k] : lo[k];
-            flo[k] = go && left ? fx : flo[k];
-            hi[k] = go && !left ? xr[k] : hi[k];
-            const double xn = xr[k] - fx / dfx;
-            const double xs = (xn > lo[k] && xn < hi[k]) ? xn : 0.5 * (lo[k] + hi[k]);
-            xr[k] = go ? xs : xr[k];
+        for (int g = 0; g < kMaxSol; g += kRootGroup) {
+            if (!__any((live >> g) & ((1u << kRootGroup) - 1u))) continue;
+#pragma unroll
+            for (int k = g; k < g + kRootGroup && k < kMaxSol; ++k) {
+                const double fx = peval0(R, xr[k]), dfx = peval1(R, xr[k]);
+                const bool go = ((live >> k) & 1u) && fx != 0.0;
+                if (!go) live &= ~(1u << k);
+                const bool left = (fx < 0.0) == (flo[k] < 0.0);
+                lo[k] = go && left ? xr[k] : lo[k];
+                flo[k] = go && left ? fx : flo[k];
+                hi[k] = go && !left ? xr[k] : hi[k];
+                const double xn = xr[k] - fx / dfx;
+                const double xs = (xn > lo[k] && xn < hi[k]) ? xn : 0.5 * (lo[k] + hi[k]);
+                xr[k] = go ? xs : xr[k];
+            }
         }
     }
     RPROF(10);

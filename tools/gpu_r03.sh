@@ -11,8 +11,9 @@ for cfg in c1 c5 c3; do
   timeout -k 10 400 python -u bench.py --config $cfg --steps $steps --warmup 1 > gpurun_out/bench_${TAG}_$cfg.json 2> gpurun_out/bench_${TAG}_$cfg.err
   rc=$?; echo "$cfg rc=$rc"; cat gpurun_out/bench_${TAG}_$cfg.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_${TAG}_$cfg.err; exit $rc; }
 done
-if [ -f build_var/libgtsfm_hip_prof.so ]; then
-  GTSFM_HIP_LIB=build_var/libgtsfm_hip_prof.so timeout -k 10 300 python -u tools/ransac_prof.py 100 > gpurun_out/ransac_prof_${TAG}.txt 2>&1
-  rc=$?; echo "ransac_prof rc=$rc"; cat gpurun_out/ransac_prof_${TAG}.txt | tail -25
-fi
+for v in prof prof1; do
+  [ -f build_var/libgtsfm_hip_$v.so ] || continue
+  GTSFM_HIP_LIB=build_var/libgtsfm_hip_$v.so timeout -k 10 300 python -u tools/ransac_prof.py 100 > gpurun_out/ransac_${v}_${TAG}.txt 2>&1
+  rc=$?; echo "ransac $v rc=$rc"; tail -25 gpurun_out/ransac_${v}_${TAG}.txt; [ $rc -eq 0 ] || exit $rc
+done
 exit 0
