@@ -173,6 +173,9 @@ constexpr int kChain = 66;
 #define GTSFM_ROOT_GROUP 4  // root slots bisected / polished together (independent Horner chains)
 #endif
 constexpr int kRootGroup = GTSFM_ROOT_GROUP;
+#ifndef GTSFM_GJ_UNROLL
+#define GTSFM_GJ_UNROLL 0  // unroll the 10 row updates of each Gauss-Jordan column (rows' LDS loads batched)
+#endif
 __device__ __forceinline__ constexpr int row_off(int k) { return 11 * k - k * (k - 1) / 2; }
 
 __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], double x) {
@@ -542,6 +545,9 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         for (int j = 0; j < 10; ++j) prow[j] *= inv;
 #pragma unroll
         for (int j = 0; j < 10; ++j) A[10 * c + j] = prow[j];
+#if GTSFM_GJ_UNROLL
+#pragma unroll
+#endif
         for (int r = 0; r < 10; ++r) {
             if (r == c) continue;
             double row[10];

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${1:-r02}
 shift
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest tests -m gpu --maxfail=5 -v --timeout 240 --timeout-method thread \
     > gpurun_out/pytest_${TAG}.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_${TAG}.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|error" gpurun_out/pytest_${TAG}.log | head -20; exit $rc; }
 timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/smoke_${TAG}.log 2>&1

@@ -11,6 +11,13 @@ for cfg in c1 c5 c3; do
   timeout -k 10 400 python -u bench.py --config $cfg --steps $steps --warmup 1 > gpurun_out/bench_${TAG}_$cfg.json 2> gpurun_out/bench_${TAG}_$cfg.err
   rc=$?; echo "$cfg rc=$rc"; cat gpurun_out/bench_${TAG}_$cfg.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_${TAG}_$cfg.err; exit $rc; }
 done
+# verifier A/B: the product library first (its results are the reference), then every variant in build_var/
+timeout -k 10 300 python -u tools/verify_bench.py > gpurun_out/vb_${TAG}.jsonl 2>&1 || { tail -5 gpurun_out/vb_${TAG}.jsonl; exit 1; }
+for so in build_var/libgtsfm_hip_*.so; do
+  case $so in *prof*) continue;; esac
+  GTSFM_HIP_LIB=$so timeout -k 10 300 python -u tools/verify_bench.py >> gpurun_out/vb_${TAG}.jsonl 2>&1 || { tail -5 gpurun_out/vb_${TAG}.jsonl; exit 1; }
+done
+cat gpurun_out/vb_${TAG}.jsonl
 for v in prof prof1; do
   [ -f build_var/libgtsfm_hip_$v.so ] || continue
   GTSFM_HIP_LIB=build_var/libgtsfm_hip_$v.so timeout -k 10 300 python -u tools/ransac_prof.py 100 > gpurun_out/ransac_${v}_${TAG}.txt 2>&1
