@@ -1362,28 +1362,30 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
         }
         RPROF(13);
         __syncthreads();
-        if (tid == 0) {
+        if (wave == 0) {
             const unsigned long long bk = best_key;
             const uint32_t low = (uint32_t)bk;
-            if (low != 0xFFFFFFFFu) {  // a candidate of this chunk beat the previous best
-                const int ci = (int)(0xFFFFFFFEu - low);
-                int hl = 0;
-                while (flat_off[hl + 1] <= ci) ++hl;
-                const int sI = ci - flat_off[hl];
-                if (kMsac) {
-                    best = cand_cnt[ci];
-                    best_score = ~(uint32_t)(bk >> 32);
-                } else {
-                    best = (int)(bk >> 32) - 1;
+            // the winner's hypothesis: the first one whose running candidate count passes it (one ballot)
+            const int ci = (int)(0xFFFFFFFEu - low);
+            const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
+            if (lane == 0) {
+                if (low != 0xFFFFFFFFu) {  // a candidate of this chunk beat the previous best
+                    const int sI = ci - flat_off[hl];
+                    if (kMsac) {
+                        best = cand_cnt[ci];
+                        best_score = ~(uint32_t)(bk >> 32);
+                    } else {
+                        best = (int)(bk >> 32) - 1;
+                    }
+                    best_h = done + hl;
+                    best_s = sI;
+                    best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
                 }
-                best_h = done + hl;
-                best_s = sI;
-                best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
+                if (best > 0) niters = min(niters, bound_tab[(size_t)p * (mcap + 1) + best]);
+                n_models += total;
+                sh_bound[0] = best;
+                sh_bound[1] = niters;
             }
-            if (best > 0) niters = min(niters, bound_tab[(size_t)p * (mcap + 1) + best]);
-            n_models += total;
-            sh_bound[0] = best;
-            sh_bound[1] = niters;
         }
         __syncthreads();  // flat_off / best_key are rewritten by the next chunk
         best = sh_bound[0];
