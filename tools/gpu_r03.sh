@@ -12,8 +12,10 @@ for cfg in c1 c5 c3; do
   rc=$?; echo "$cfg rc=$rc"; cat gpurun_out/bench_${TAG}_$cfg.json; [ $rc -eq 0 ] || { tail -20 gpurun_out/bench_${TAG}_$cfg.err; exit $rc; }
 done
 # verifier A/B: the product library first (its results are the reference), then every variant in build_var/
+[ -d build_var ] || exit 0
 timeout -k 10 300 python -u tools/verify_bench.py > gpurun_out/vb_${TAG}.jsonl 2>&1 || { tail -5 gpurun_out/vb_${TAG}.jsonl; exit 1; }
 for so in build_var/libgtsfm_hip_*.so; do
+  [ -f "$so" ] || continue
   case $so in *prof*) continue;; esac
   GTSFM_HIP_LIB=$so timeout -k 10 300 python -u tools/verify_bench.py >> gpurun_out/vb_${TAG}.jsonl 2>&1 || { tail -5 gpurun_out/vb_${TAG}.jsonl; exit 1; }
 done
