@@ -18,6 +18,8 @@
 //     normal matrix is reduced through LDS in a fixed order) and the cheirality vote of recoverPose.
 #include <math.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 
 // Development instrumentation (off in the product build): -DGTSFM_RANSAC_PROF accumulates per-phase shader-clock
@@ -100,16 +102,19 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 // consecutive words, so every access is bank-conflict free, and nothing spills to scratch. The solver runs in two
 // kernels so each one's workgroup holds only its own phase's arrays:
 //   stage 1 (sample, 5x9 nullspace, 10x20 Gauss-Jordan), two lanes per hypothesis: Q (45) + column permutation
-//       (9 ints) | this lane's half of A (10 x 10) = 51 KB per 64-lane workgroup (three per CU);
-//   stage 2 (det B(z), Sturm chain, isolation, bisection, E): a rolling window of three Sturm rows (3 x 11) + prem
-//       scratch (11) | isolation stack (2 x 24) + intervals (2 x 10) doubles, stack counts and chain degrees as
-//       bytes = 38 KB per workgroup (four per CU). Finished chain rows go straight to the register chain R.
+//       (9 ints) | rows 2..9 of this lane's half of A (8 x 10; rows 0, 1 in registers) = 40 KB per 64-lane
+//       workgroup (four per CU);
+//   stage 2 (det B(z), Sturm chain, isolation, bisection, E): the chain is built in registers (generic degrees;
+//       a private-memory fallback for degree drops), the isolating intervals are selected into registers, and LDS
+//       holds only the isolation stack as left ends (24 doubles + 24 count bytes) = 13.5 KB per workgroup, so
+//       with <= 256 registers two waves share a SIMD.
 constexpr int kLanes = 64;
-constexpr int kUnion = 100;   // stage-1 doubles per lane: Q (45) + V (9) + permutation ints (at slot 64) | half of A
+constexpr int kRegRows = 2;   // rows of the lane's half of A kept in registers (the rest in LDS)
+constexpr int kUnion = 10 * (10 - kRegRows);  // stage-1 doubles per lane: Q (45) + V (9) + perm ints (slot 64) | A rows 2..9
 constexpr int kPermSlot = 64; // double slot where the nullspace's column permutation (9 ints) starts
 constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
-constexpr int kRootDbl = 68;  // stage-2 doubles per lane: 3 Sturm rows (33) + t (11) | stack (48) + intervals (20)
-constexpr int kRootB = 64;    // stage-2 bytes per lane: stack va/vb (2 x 24) + chain degrees (11), padded
+constexpr int kRootDbl = kStack;  // stage-2 doubles per lane: the isolation stack's left ends
+constexpr int kRootB = kStack;    // stage-2 bytes per lane: the stack's Sturm sign-variation counts
 constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double);
 static_assert(kPermSlot >= 54 && kPermSlot * 8 + 9 * 4 <= kUnion * 8, "permutation ints overlap Q/V or overflow");
 constexpr size_t kRootLds = (size_t)kRootDbl * kLanes * sizeof(double) + (size_t)kRootB * kLanes;
@@ -173,9 +178,6 @@ constexpr int kChain = 66;
 #define GTSFM_ROOT_GROUP 4  // root slots bisected / polished together (independent Horner chains)
 #endif
 constexpr int kRootGroup = GTSFM_ROOT_GROUP;
-#ifndef GTSFM_GJ_UNROLL
-#define GTSFM_GJ_UNROLL 0  // unroll the 10 row updates of each Gauss-Jordan column (rows' LDS loads batched)
-#endif
 __device__ __forceinline__ constexpr int row_off(int k) { return 11 * k - k * (k - 1) / 2; }
 
 __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], double x) {
@@ -214,16 +216,54 @@ __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
     return a;
 }
 
-// Real roots (ascending) of a degree <= 10 polynomial: Sturm isolation + 80-step bisection, arithmetic identical to
+// Sturm chain of p (degree <= 10), the rows of oracle/ransac.c real_roots, into the register chain R (row k
+// zero-padded to 11 - k; rows past the chain's end 0). Generic case: p of degree 10 and every pseudo-remainder of
+// degree exactly one less than its divisor, so every row's degree and every loop bound is a compile-time constant
+// and the whole chain lives in registers. A lane whose polynomial leaves that pattern (a degree drop, a zero
+// remainder) rebuilds the chain with run-time degrees in private memory, the oracle's loop verbatim. Both paths do
+// the oracle's operations in the oracle's order.
+__device__ __forceinline__ void sturm_chain_fallback(const double (&row0)[11], int deg, double (&R)[kChain]) {
+    double S[11][11];
+    int sd[11];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) S[0][i] = row0[i];
+    sd[0] = deg;
+    for (int i = 1; i <= deg; ++i) S[1][i - 1] = (double)i * row0[i];
+    sd[1] = deg - 1;
+    int n = 2;
+    while (n < 11 && sd[n - 1] > 0) {
+        const double* a = S[n - 2];
+        const double* b = S[n - 1];
+        const int da = sd[n - 2], db = sd[n - 1];
+        double t[11];
+        for (int i = 0; i <= da; ++i) t[i] = a[i];
+        for (int k = da; k >= db; --k) {
+            const double f = t[k] / b[db];
+            for (int i = 0; i <= db; ++i) t[k - db + i] -= f * b[i];
+            t[k] = 0.0;
+        }
+        int dr = db - 1;
+        double scale = 0.0;
+        for (int i = 0; i <= da; ++i) scale = fmax(scale, fabs(a[i]));
+        while (dr >= 0 && fabs(t[dr]) <= 1e-14 * scale) --dr;
+        if (dr < 0) break;
+        for (int i = 0; i <= dr; ++i) S[n][i] = -t[i];
+        sd[n] = dr;
+        n++;
+    }
+#pragma unroll
+    for (int k = 0; k < 11; ++k)
+#pragma unroll
+        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = (k < n && i <= sd[k < n ? k : 0]) ? S[k][i] : 0.0;
+}
+
+// Real roots (ascending) of a degree <= 10 polynomial into xr[0..nr): Sturm isolation, then all isolating intervals
+// bisected together to a relative width of 2^-20 and polished by 4 safeguarded Newton steps, the arithmetic of
 // oracle/ransac.c real_roots. Isolation runs first and records the isolating intervals; all intervals are then
 // bisected together (10 independent chains), so a wave never serialises one lane's bisection behind another's
 // isolation step.
-template <typename RootFn>
-__device__ int real_roots(const double (&pin)[11], int deg, RootMem m, RootFn&& on_root) {
+__device__ int real_roots(const double (&pin)[11], int deg, RootMem m, double (&xr)[kMaxSol]) {
     RPROF_DECL
-    LaneArr<double> S = m.u;  // chain row k in slot k % 3 (11 doubles each) while it is still needed by prem
-    LaneArr<double> t = m.u.at(33);
-    LaneArr<uint8_t> sdeg = m.b.at(2 * kStack);
     // the coefficients stay in registers: every index below is static (the degree only selects)
     double lead = pin[0];
 #pragma unroll
@@ -237,44 +277,51 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, RootFn&& 
         }
     }
     if (deg <= 0) return 0;
-#pragma unroll
-    for (int i = 0; i < 11; ++i)
-        if (i <= deg) S[i] = pin[i] / lead;
-    sdeg[0] = (uint8_t)deg;
-#pragma unroll
-    for (int i = 1; i < 11; ++i)
-        if (i <= deg) S[11 + i - 1] = (double)i * S[i];
-    sdeg[1] = (uint8_t)(deg - 1);
-    // register chain: rows 0 and 1 now, row n as soon as prem produces it (rows past the chain stay 0)
     double R[kChain];
+    double row0[11];
 #pragma unroll
-    for (int k = 0; k < 2; ++k)
+    for (int i = 0; i < 11; ++i) row0[i] = i <= deg ? pin[i] / lead : 0.0;
+    bool generic = deg == 10;
+    {
 #pragma unroll
-        for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= (int)sdeg[k] ? S[11 * k + i] : 0.0;
+        for (int i = 0; i < 11; ++i) R[i] = row0[i];
 #pragma unroll
-    for (int i = row_off(2); i < kChain; ++i) R[i] = 0.0;
-    int n = 2;
-    while (n < 11 && sdeg[n - 1] > 0) {
-        const int so = 11 * (n % 3), sa = 11 * ((n - 2) % 3), sb = 11 * ((n - 1) % 3);
-        const int dr = prem(S.at(sa), sdeg[n - 2], S.at(sb), sdeg[n - 1], S.at(so), t);
-        if (dr < 0) break;
-        for (int i = 0; i <= dr; ++i) S[so + i] = -S[so + i];
-        sdeg[n] = (uint8_t)dr;
+        for (int i = 1; i < 11; ++i) R[row_off(1) + i - 1] = (double)i * row0[i];
+        // rows 2..10: row k = -(row k-2 mod row k-1), degrees 12-k / 11-k -> 10-k
 #pragma unroll
-        for (int k = 2; k < 11; ++k)
-            if (k == n) {
+        for (int k = 2; k < 11; ++k) {
+            const int da = 12 - k, db = 11 - k;
+            const int oa = row_off(k - 2), ob = row_off(k - 1);
+            double t[13];
 #pragma unroll
-                for (int i = 0; i < 11 - k; ++i) R[row_off(k) + i] = i <= dr ? S[so + i] : 0.0;
+            for (int i = 0; i <= da; ++i) t[i] = R[oa + i];
+#pragma unroll
+            for (int kk = da; kk >= db; --kk) {
+                const double f = t[kk] / R[ob + db];
+#pragma unroll
+                for (int i = 0; i <= db; ++i) t[kk - db + i] -= f * R[ob + i];
+                t[kk] = 0.0;
             }
-        n++;
+            double scale = 0.0;
+#pragma unroll
+            for (int i = 0; i <= da; ++i) scale = fmax(scale, fabs(R[oa + i]));
+            generic = generic && fabs(t[db - 1]) > 1e-14 * scale;
+#pragma unroll
+            for (int i = 0; i <= db - 1; ++i) R[row_off(k) + i] = -t[i];
+        }
     }
+    if (!generic) sturm_chain_fallback(row0, deg, R);
     RPROF(7);
     // root bound (== oracle root_bound_pow2): exact exponent arithmetic, a power of two
     double bound;
     {
         int emax = -2000;
-        for (int k = 1; k <= deg; ++k) {
-            double mk = fabs(S[deg - k]);
+#pragma unroll
+        for (int k = 1; k <= 10; ++k) {
+            if (k > deg) continue;
+            double mk = 0.0;
+#pragma unroll
+            for (int i = 0; i < 11; ++i) mk = i == deg - k ? fabs(R[i]) : mk;
             if (k == deg) mk *= 0.5;
             if (mk == 0.0) continue;
             int x;
@@ -285,43 +332,48 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, RootFn&& 
         if (emax == -2000) emax = 0;
         bound = ldexp(1.0, emax + 1);
     }
-    // isolation (stack and the interval list reuse the chain's LDS)
-    LaneArr<double> st_a = m.u, st_b = m.u.at(kStack), iv_a = m.u.at(2 * kStack), iv_b = m.u.at(2 * kStack + kMaxSol);
-    LaneArr<uint8_t> st_va = m.b, st_vb = m.b.at(kStack);
+    // isolation (depth-first, left interval first). The stack always partitions [left end of the top, bound] into
+    // adjacent intervals, so an entry's right end (and its Sturm count) is the left end of the entry below it: only
+    // left ends are stored. The isolating intervals are selected into registers.
+    LaneArr<double> st_a = m.u;
+    LaneArr<uint8_t> st_va = m.b;
+    const int v_bound = sign_changes_reg(R, bound);
+    double lo[kMaxSol], hi[kMaxSol];
+#pragma unroll
+    for (int k = 0; k < kMaxSol; ++k) lo[k] = hi[k] = 0.0;
     int ns = 1, nr = 0, guard = 0;
     st_a[0] = -bound;
-    st_b[0] = bound;
     st_va[0] = (uint8_t)sign_changes_reg(R, -bound);
-    st_vb[0] = (uint8_t)sign_changes_reg(R, bound);
     while (ns > 0 && nr < kMaxSol && guard < 2000) {
         ++guard;
         --ns;
-        const double a = st_a[ns], b = st_b[ns];
-        const int va = st_va[ns], vb = st_vb[ns];
+        const double a = st_a[ns];
+        const int va = st_va[ns];
+        const double b = ns > 0 ? st_a[ns > 0 ? ns - 1 : 0] : bound;
+        const int vb = ns > 0 ? (int)st_va[ns > 0 ? ns - 1 : 0] : v_bound;
         const int cnt = va - vb;
         if (cnt <= 0) continue;
         if (cnt == 1 || b - a < 1e-10 * fmax(1.0, fabs(a))) {
-            iv_a[nr] = a;
-            iv_b[nr] = b;
+#pragma unroll
+            for (int k = 0; k < kMaxSol; ++k) {
+                lo[k] = k == nr ? a : lo[k];
+                hi[k] = k == nr ? b : hi[k];
+            }
             ++nr;
             continue;
         }
         const double mid = 0.5 * (a + b);
         const int vm = sign_changes_reg(R, mid);
-        if (ns + 2 <= kStack) {
-            st_a[ns] = mid; st_b[ns] = b; st_va[ns] = (uint8_t)vm; st_vb[ns] = (uint8_t)vb; ++ns;
-            st_a[ns] = a; st_b[ns] = mid; st_va[ns] = (uint8_t)va; st_vb[ns] = (uint8_t)vm; ++ns;
+        if (ns + 2 <= kStack) {  // (mid, b) below (a, mid): left ends mid, a
+            st_a[ns] = mid; st_va[ns] = (uint8_t)vm; ++ns;
+            st_a[ns] = a; st_va[ns] = (uint8_t)va; ++ns;
         }
     }
     RPROF(8);
     RPROF_COUNT(20, guard);
-    double lo[kMaxSol], hi[kMaxSol], flo[kMaxSol];
+    double flo[kMaxSol];
 #pragma unroll
-    for (int k = 0; k < kMaxSol; ++k) {
-        lo[k] = k < nr ? iv_a[k] : 0.0;
-        hi[k] = k < nr ? iv_b[k] : 0.0;
-        flo[k] = peval0(R, lo[k]);
-    }
+    for (int k = 0; k < kMaxSol; ++k) flo[k] = peval0(R, lo[k]);
     // all isolating intervals refined together (== oracle): bisection down to a relative width of 2^-20, then 4
     // safeguarded Newton steps with p' = Sturm row 1
     unsigned live = 0;
@@ -351,7 +403,6 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, RootFn&& 
         }
     }
     RPROF(9);
-    double xr[kMaxSol];
 #pragma unroll
     for (int k = 0; k < kMaxSol; ++k) xr[k] = 0.5 * (lo[k] + hi[k]);
     live = all_roots;
@@ -375,12 +426,6 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, RootFn&& 
         }
     }
     RPROF(10);
-    LaneArr<double> roots = iv_a;
-#pragma unroll
-    for (int k = 0; k < kMaxSol; ++k)
-        if (k < nr) roots[k] = xr[k];
-    for (int k = 0; k < nr; ++k) on_root(roots[k]);
-    RPROF(11);
     RPROF_COUNT(21, nr);
     return nr;
 }
@@ -469,23 +514,18 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         E[e][2] = N[2][e];
         E[e][3] = N[3][e];
     }
-    LaneArr<double> A = m.u;  // [10][10]: this lane's half; each row is accumulated in registers, then stored once
+    // This lane's half of A: rows 0..kRegRows-1 in registers (G), rows kRegRows..9 in LDS (A), so the workgroup's LDS
+    // is 40 KB (four workgroups per CU instead of three). Each row is accumulated in registers, then stored once.
+    LaneArr<double> A = m.u.at(-10 * kRegRows);  // A[10 * r + j] for r >= kRegRows
+    double G[kRegRows][10];
     auto store_row = [&](int r, const double(&row)[20]) {
 #pragma unroll
-        for (int k = 0; k < 10; ++k) A[10 * r + k] = part ? row[10 + k] : row[k];
+        for (int k = 0; k < 10; ++k) {
+            const double v = part ? row[10 + k] : row[k];
+            if (r < kRegRows) G[r < kRegRows ? r : 0][k] = v;
+            else A[10 * r + k] = v;
+        }
     };
-    {
-        double row[20], q[10];
-#pragma unroll
-        for (int k = 0; k < 20; ++k) row[k] = 0.0;
-        mul_ll(E[4], E[8], q); addmul_ql(q, E[0], 1.0, row);
-        mul_ll(E[5], E[7], q); addmul_ql(q, E[0], -1.0, row);
-        mul_ll(E[3], E[8], q); addmul_ql(q, E[1], -1.0, row);
-        mul_ll(E[5], E[6], q); addmul_ql(q, E[1], 1.0, row);
-        mul_ll(E[3], E[7], q); addmul_ql(q, E[2], 1.0, row);
-        mul_ll(E[4], E[6], q); addmul_ql(q, E[2], -1.0, row);
-        store_row(0, row);
-    }
     double EEt[3][3][10], tr[10], tmp[10];
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -505,61 +545,107 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         }
 #pragma unroll
     for (int mm = 0; mm < 10; ++mm) tr[mm] = EEt[0][0][mm] + EEt[1][1][mm] + EEt[2][2][mm];
+    // rows 9, 8, ..., 1, then the det row 0: the register rows are produced last (short live ranges)
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
+    for (int ij = 8; ij >= 0; --ij) {
+        const int i = ij / 3, j = ij % 3;
+        double row[20];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            double row[20];
+        for (int k = 0; k < 20; ++k) row[k] = 0.0;
 #pragma unroll
-            for (int k = 0; k < 20; ++k) row[k] = 0.0;
+        for (int k = 0; k < 3; ++k) addmul_ql(EEt[i][k], E[3 * k + j], 2.0, row);
+        addmul_ql(tr, E[3 * i + j], -1.0, row);
+        store_row(1 + ij, row);
+    }
+    {
+        double row[20], q[10];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) addmul_ql(EEt[i][k], E[3 * k + j], 2.0, row);
-            addmul_ql(tr, E[3 * i + j], -1.0, row);
-            store_row(1 + 3 * i + j, row);
-        }
+        for (int k = 0; k < 20; ++k) row[k] = 0.0;
+        mul_ll(E[4], E[8], q); addmul_ql(q, E[0], 1.0, row);
+        mul_ll(E[5], E[7], q); addmul_ql(q, E[0], -1.0, row);
+        mul_ll(E[3], E[8], q); addmul_ql(q, E[1], -1.0, row);
+        mul_ll(E[5], E[6], q); addmul_ql(q, E[1], 1.0, row);
+        mul_ll(E[3], E[7], q); addmul_ql(q, E[2], 1.0, row);
+        mul_ll(E[4], E[6], q); addmul_ql(q, E[2], -1.0, row);
+        store_row(0, row);
+    }
     RPROF(2);
-    // Gauss-Jordan with partial pivoting on the lane's half rows; every row is moved through registers whole
-#pragma unroll
-    for (int c = 0; c < 10; ++c) {
+    // Gauss-Jordan with partial pivoting on the lane's half rows; every row is moved through registers whole. Row
+    // indices are static except the pivot row pr, which is read / written through LDS or a register select.
+    auto ld = [&](int r, int j) -> double { return r < kRegRows ? G[r < kRegRows ? r : 0][j] : A[10 * r + j]; };
+    // one column step per call with a compile-time column (no dynamically indexed register rows)
+    auto gj_step = [&](auto cc) -> bool {
+        constexpr int c = decltype(cc)::value;
         int pr = c;
-        double best = fabs(A[10 * c + c]);  // meaningful in the even lane (column c)
+        double best = fabs(ld(c, c));  // meaningful in the even lane (column c)
+#pragma unroll
         for (int r = c + 1; r < 10; ++r) {
-            const double v = fabs(A[10 * r + c]);
+            const double v = fabs(ld(r, c));
             if (v > best) { best = v; pr = r; }
         }
         pr = pair_lo(pr);
         best = pair_lo(best);
         if (best < 1e-14) return false;
         double prow[10];
+        if (c < kRegRows) {  // pr may be a register row
+            const bool in_lds = pr >= kRegRows;
 #pragma unroll
-        for (int j = 0; j < 10; ++j) prow[j] = A[10 * pr + j];
+            for (int j = 0; j < 10; ++j) {
+                double v = in_lds ? A[10 * (in_lds ? pr : kRegRows) + j] : G[0][j];
+#pragma unroll
+                for (int q = 1; q < kRegRows; ++q) v = pr == q ? G[q][j] : v;
+                prow[j] = v;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 10; ++j) prow[j] = A[10 * pr + j];
+        }
         if (pr != c) {
             double crow[10];
 #pragma unroll
-            for (int j = 0; j < 10; ++j) crow[j] = A[10 * c + j];
+            for (int j = 0; j < 10; ++j) crow[j] = ld(c, j);
+            if (pr >= kRegRows) {
 #pragma unroll
-            for (int j = 0; j < 10; ++j) A[10 * pr + j] = crow[j];
+                for (int j = 0; j < 10; ++j) A[10 * pr + j] = crow[j];
+            } else {
+#pragma unroll
+                for (int q = 0; q < kRegRows; ++q)
+#pragma unroll
+                    for (int j = 0; j < 10; ++j) G[q][j] = pr == q ? crow[j] : G[q][j];
+            }
         }
         const double inv = 1.0 / pair_lo(prow[c]);
 #pragma unroll
         for (int j = 0; j < 10; ++j) prow[j] *= inv;
 #pragma unroll
-        for (int j = 0; j < 10; ++j) A[10 * c + j] = prow[j];
-#if GTSFM_GJ_UNROLL
+        for (int j = 0; j < 10; ++j) {
+            if (c < kRegRows) G[c < kRegRows ? c : 0][j] = prow[j];
+            else A[10 * c + j] = prow[j];
+        }
 #pragma unroll
-#endif
         for (int r = 0; r < 10; ++r) {
             if (r == c) continue;
             double row[10];
 #pragma unroll
-            for (int j = 0; j < 10; ++j) row[j] = A[10 * r + j];
+            for (int j = 0; j < 10; ++j) row[j] = ld(r, j);
             const double f = pair_lo(row[c]);
 #pragma unroll
             for (int j = 0; j < 10; ++j) row[j] -= f * prow[j];
 #pragma unroll
-            for (int j = 0; j < 10; ++j) A[10 * r + j] = row[j];
+            for (int j = 0; j < 10; ++j) {
+                if (r < kRegRows) G[r < kRegRows ? r : 0][j] = row[j];
+                else A[10 * r + j] = row[j];
+            }
         }
-    }
+        return true;
+    };
+    using std::integral_constant;
+    if (!gj_step(integral_constant<int, 0>{}) || !gj_step(integral_constant<int, 1>{}) ||
+        !gj_step(integral_constant<int, 2>{}) || !gj_step(integral_constant<int, 3>{}) ||
+        !gj_step(integral_constant<int, 4>{}) || !gj_step(integral_constant<int, 5>{}) ||
+        !gj_step(integral_constant<int, 6>{}) || !gj_step(integral_constant<int, 7>{}) ||
+        !gj_step(integral_constant<int, 8>{}) || !gj_step(integral_constant<int, 9>{}))
+        return false;
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -570,14 +656,21 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
 
 // Stage 2: the 3 x 3 polynomial matrix B(z) from the reduced rows, its degree-10 determinant, real roots, and up to
 // 10 unit-norm E; on_sol(s, E) is called for each solution in root order.
-template <typename SolFn>
-__device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], RootMem m, SolFn&& on_sol) {
-    RPROF_DECL
-    double B[3][3][5];
+// B(z) (3 x 3 polynomial matrix) from stage 1's reduced rows (`in`: this hypothesis' first stage value, stride
+// kMaxHyp). Reads through a pointer the compiler cannot see through, so a second call reloads (from L2) instead of
+// keeping B live across the root finder.
+__device__ __forceinline__ void load_B(const double* in, double (&B)[3][3][5]) {
+    uint64_t a = (uint64_t)in;
+    asm volatile("" : "+v"(a));
+    const double* q = (const double*)a;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-        const double* e = Rt[2 * r];  // e[k] == A[20 * (4 + 2r) + 10 + k]
-        const double* f = Rt[2 * r + 1];
+        double e[10], f[10];  // e[k] == A[4 + 2r][10 + k], f[k] == A[5 + 2r][10 + k]
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+            e[j] = q[(size_t)(10 * (2 * r) + j) * kMaxHyp];
+            f[j] = q[(size_t)(10 * (2 * r + 1) + j) * kMaxHyp];
+        }
         B[r][0][0] = e[2]; B[r][0][1] = e[1] - f[2]; B[r][0][2] = e[0] - f[1];
         B[r][0][3] = -f[0]; B[r][0][4] = 0.0;
         B[r][1][0] = e[5]; B[r][1][1] = e[4] - f[5]; B[r][1][2] = e[3] - f[4];
@@ -585,10 +678,20 @@ __device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], R
         B[r][2][0] = e[9]; B[r][2][1] = e[8] - f[9]; B[r][2][2] = e[7] - f[8];
         B[r][2][3] = e[6] - f[7]; B[r][2][4] = -f[6];
     }
+}
+
+// Stage 2: the 3 x 3 polynomial matrix B(z) from the reduced rows, its degree-10 determinant, real roots, and up to
+// 10 unit-norm E; on_sol(s, E) is called for each solution in root order. B and the null-space basis N are read
+// from stage 1's output (`in`) before and after the root finder, so neither holds registers during it.
+template <typename SolFn>
+__device__ int five_point_stage2(const double* in, RootMem m, SolFn&& on_sol) {
+    RPROF_DECL
     double n[11];
-#pragma unroll
-    for (int i = 0; i < 11; ++i) n[i] = 0.0;
     {
+        double B[3][3][5];
+        load_B(in, B);
+#pragma unroll
+        for (int i = 0; i < 11; ++i) n[i] = 0.0;
         const int deg[3] = {3, 3, 4};
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -611,9 +714,21 @@ __device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], R
                 for (int j = 0; j <= dm; ++j) n[i + j] += B[0][c][i] * mm[j];
         }
     }
-    int nsol = 0;
     RPROF(6);
-    real_roots(n, 10, m, [&](double z) {
+    double xr[kMaxSol];
+    const int nr = real_roots(n, 10, m, xr);
+    double B[3][3][5], N[4][9];
+    load_B(in, B);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 9; ++j) N[k][j] = in[(size_t)(60 + 9 * k + j) * kMaxHyp];
+    int nsol = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxSol; ++k) {
+        if (!__any(k < nr)) break;
+        if (k >= nr) continue;
+        const double z = xr[k];
         double Bz[3][3];
 #pragma unroll
         for (int r = 0; r < 3; ++r)
@@ -635,7 +750,7 @@ __device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], R
             const double nn = cx * cx + cy * cy + cz * cz;
             if (nn > bn) { bn = nn; bx = cx; by = cy; bzz = cz; }
         }
-        if (!(fabs(bzz) > 1e-300)) return;
+        if (!(fabs(bzz) > 1e-300)) continue;
         const double x = bx / bzz, y = by / bzz;
         double Eo[9], nrm = 0.0;
 #pragma unroll
@@ -644,12 +759,13 @@ __device__ int five_point_stage2(const double N[4][9], const double Rt[6][10], R
             nrm += Eo[e] * Eo[e];
         }
         nrm = sqrt(nrm);
-        if (!(nrm > 0.0)) return;
+        if (!(nrm > 0.0)) continue;
 #pragma unroll
         for (int e = 0; e < 9; ++e) Eo[e] /= nrm;
         on_sol(nsol, Eo);
         ++nsol;
-    });
+    }
+    RPROF(11);
     return nsol;
 }
 
@@ -682,6 +798,37 @@ __device__ __forceinline__ uint32_t msac_cost(const float* E, float4 p, float th
     const float r = den > 0.0f ? __fdiv_rn(nn, den) : 0.0f;
     const float q = __fmul_rn(r, scale);
     return q < 65535.0f ? (uint32_t)q : 65535u;
+}
+
+// Two putatives per lane in packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: one instruction for both): the same fused
+// and rounded operations as msac_cost / sampson_inlier, component-wise, so each component is bit-identical to the
+// scalar path. Only the division stays scalar.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <bool kMsac>
+__device__ __forceinline__ void score2(const float (&E)[9], f2 x1, f2 y1, f2 x2, f2 y2, float thr2, float scale,
+                                       uint32_t& bad, int& cnt) {
+    const f2 a0 = pfma((f2)E[1], y1, pfma((f2)E[0], x1, (f2)E[2]));
+    const f2 a1 = pfma((f2)E[4], y1, pfma((f2)E[3], x1, (f2)E[5]));
+    const f2 a2 = pfma((f2)E[7], y1, pfma((f2)E[6], x1, (f2)E[8]));
+    const f2 b0 = pfma((f2)E[3], y2, pfma((f2)E[0], x2, (f2)E[6]));
+    const f2 b1 = pfma((f2)E[4], y2, pfma((f2)E[1], x2, (f2)E[7]));
+    const f2 num = pfma(y2, a1, pfma(x2, a0, a2));
+    const f2 den = pfma(b1, b1, pfma(b0, b0, pfma(a1, a1, a0 * a0)));
+    const f2 nn = num * num;
+    const f2 rhs = (f2)thr2 * den;
+    const bool in0 = nn.x <= rhs.x, in1 = nn.y <= rhs.y;
+    cnt += (in0 ? 1 : 0) + (in1 ? 1 : 0);
+    if constexpr (kMsac) {
+        const f2 r = {den.x > 0.0f ? __fdiv_rn(nn.x, den.x) : 0.0f, den.y > 0.0f ? __fdiv_rn(nn.y, den.y) : 0.0f};
+        const f2 qq = r * (f2)scale;
+        const uint32_t c0 = qq.x < 65535.0f ? (uint32_t)qq.x : 65535u;
+        const uint32_t c1 = qq.y < 65535.0f ? (uint32_t)qq.y : 65535u;
+        bad += (in0 ? c0 : 65536u) + (in1 ? c1 : 65536u);
+    } else {
+        bad += (in0 ? 0u : 1u) + (in1 ? 0u : 1u);
+    }
 }
 
 // Wave-wide sum, uniform result: DPP prefix sum within each row of 16 (row_shr 1, 2, 4, 8), then row_bcast 15 / 31
@@ -1133,7 +1280,7 @@ __global__ void ransac_init_kernel(PairState* __restrict__ st, int n_pairs, int 
 // hypothesis-minor). nsol = 1 marks a non-degenerate sample for stage 2, 0 a finished one. A launch covers
 // gridDim.y / 2 chunks; a chunk that starts at or past the pair's current iteration bound is skipped (the bound only
 // falls, so the score kernel never reaches it).
-__global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restrict__ match_count, int mcap,
+__global__ __launch_bounds__(64, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void ransac_solve1_kernel(const int* __restrict__ match_count, int mcap,
                                                               const double2* __restrict__ x1n_all,
                                                               const double2* __restrict__ x2n_all, uint64_t seed,
                                                               int pair_id_base, const int* __restrict__ pair_ids,
@@ -1185,7 +1332,7 @@ __global__ __launch_bounds__(64, 1) void ransac_solve1_kernel(const int* __restr
 
 // Stage 2, one 64-lane workgroup per chunk of an active pair (blockIdx.y = chunk): lane l turns stage 1's output into
 // the candidate essential matrices of hypothesis done + 64 blockIdx.y + l (fp64) -> cand, nsol.
-__global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restrict__ match_count,
+__global__ __launch_bounds__(64, 2) void ransac_solve2_kernel(const int* __restrict__ match_count,
                                                               const PairState* __restrict__ st,
                                                               const double* __restrict__ stage,
                                                               double* __restrict__ cand, int* __restrict__ nsol) {
@@ -1200,64 +1347,58 @@ __global__ __launch_bounds__(64, 1) void ransac_solve2_kernel(const int* __restr
     const RootMem mem = root_mem(smem, lane);
     RPROF_DECL
     RPROF_COUNT(17, 1);
-    double N[4][9], Rt[6][10];
     const double* in = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int j = 0; j < 10; ++j) Rt[r][j] = in[(10 * r + j) * kMaxHyp];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int j = 0; j < 9; ++j) N[k][j] = in[(60 + 9 * k + j) * kMaxHyp];
-    double* cout = cand + ((size_t)p * kMaxHyp + hyp) * (kMaxSol * 9);
+    // candidates hypothesis-minor, [P][kMaxSol][9][kMaxHyp]: the lanes' stores of one element are contiguous
+    double* cout = cand + (size_t)p * kMaxSol * 9 * kMaxHyp + hyp;
     RPROF(5);
-    const int ns = five_point_stage2(N, Rt, mem, [&](int s, const double* E) {
+    const int ns = five_point_stage2(in, mem, [&](int s, const double* E) {
 #pragma unroll
-        for (int e = 0; e < 9; ++e) cout[9 * s + e] = E[e];
+        for (int e = 0; e < 9; ++e) cout[(size_t)(9 * s + e) * kMaxHyp] = E[e];
     });
     *ns_out = ns;
     RPROF(12);
 }
 
-// One kScoreWaves-wave workgroup per active pair: the pair's putatives are staged in LDS once, then the launch's chunks are
-// scored in order. A chunk's candidates (flattened in (hypothesis, solution) order) are dealt round-robin to the
-// waves, each counted by one wave with an exact early exit against the running best. The best is an LDS atomicMax on
-// the key (count + 1, ~index), so the winner is the FIRST candidate in order with the largest count, as in the
-// sequential scan of oracle/ransac.c: a candidate stops once it can no longer beat the current best count, or only tie
-// it from a later index. The OpenCV iteration bound is applied after every chunk, and the pair stops there once
-// done >= niters, exactly as the oracle's batch loop (oracle/ransac.c:679-706).
-// kMsac: the key is (~score, ~index) with the quantised MSAC score (msac_cost); a candidate stops once its partial
-// score (which only grows) exceeds the best, or equals it from a later index. The winner's inlier count (for the
-// iteration bound and the status) is kept per candidate in LDS.
-#ifndef GTSFM_SCORE_WAVES
-#define GTSFM_SCORE_WAVES 8  // waves per pair (r02: 4 -> 8 took 0.3 ms off verify; 16 was slower)
+// Scoring, one workgroup of kScoreThreads lanes per active pair and launch, LANE PER CANDIDATE: the candidates of the
+// launch's chunks (flattened in (hypothesis, solution) order, the oracle's scan order) are dealt to the lanes, and
+// every lane walks all putatives of its own candidate in index order, reading each putative as one broadcast LDS
+// load. No cross-lane reduction sits on the per-point path. The per-point terms are the oracle's (msac_cost /
+// sampson_inlier), integer sums, so the order of evaluation cannot change a score.
+// Selection is exactly the oracle's sequential scan (oracle/ransac.c:716-740: a candidate replaces the best only with
+// a strictly lower MSAC score / strictly more inliers, so the first in order wins a tie): every candidate carries the
+// 64-bit key (badness << 32 | flat index + 1 << 19 | inlier count) with badness = MSAC score or outlier count, and the
+// winner is the smallest key. A lane drops its candidate as soon as its partial badness (which only grows) shows that
+// it cannot beat the best key among the pre-launch best and the finished candidates of chunks <= its own (`pref`):
+// such a candidate can be neither its chunk's prefix minimum nor the chunk minimum that the walk below needs. After
+// all lanes finish, thread 0 walks the chunks in order exactly like the oracle's batch loop
+// (oracle/ransac.c:679-706): best = min(best, chunk minimum), the iteration bound from the best count, done += 64,
+// stop once done >= niters (chunks past that point were solved speculatively and are discarded).
+#ifndef GTSFM_SCORE_THREADS
+#define GTSFM_SCORE_THREADS 256
 #endif
-constexpr int kScoreWaves = GTSFM_SCORE_WAVES;
-#ifndef GTSFM_MSAC_PPL
-#define GTSFM_MSAC_PPL 2  // points per lane between two MSAC exit tests
-#endif
-constexpr int kMsacPpl = GTSFM_MSAC_PPL;
+constexpr int kScoreThreads = GTSFM_SCORE_THREADS;
+constexpr int kMaxCand = kMaxHyp * kMaxSol;  // candidates one launch may hold per pair (13 bits of the key)
+static_assert(kMaxCand < (1 << 13), "flat candidate index must fit the key's 13 bits");
+constexpr int kKeyCountBits = 19;
 
 template <bool kLds, bool kMsac>
-__global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const int* __restrict__ pairs,
-                                                                        const double* __restrict__ intr,
-                                                                        const int* __restrict__ match_count, int mcap,
-                                                                        const float4* __restrict__ pts_all,
-                                                                        double thr_px, double prob,
-                                                                        const double* __restrict__ cand,
-                                                                        const int* __restrict__ nsol, int n_chunks,
-                                                                        const int* __restrict__ bound_tab,
-                                                                        PairState* __restrict__ st) {
+__global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* __restrict__ pairs,
+                                                                    const double* __restrict__ intr,
+                                                                    const int* __restrict__ match_count, int mcap,
+                                                                    const float4* __restrict__ pts_all,
+                                                                    double thr_px, double prob,
+                                                                    const double* __restrict__ cand,
+                                                                    const int* __restrict__ nsol, int n_chunks,
+                                                                    const int* __restrict__ bound_tab,
+                                                                    PairState* __restrict__ st) {
     extern __shared__ float4 spts[];  // [M]
-    __shared__ unsigned long long best_key;
-    __shared__ int flat_off[kBatch + 1];  // candidates of hypotheses < h
-    __shared__ int sh_bound[2];           // best count, iteration bound after the chunk (from thread 0)
-    __shared__ int cand_cnt[kMsac ? kBatch * kMaxSol : 1];  // kMsac: inlier count of every unbeaten candidate
+    __shared__ int flat_off[kMaxHyp + 1];       // candidates of the launch's hypotheses < h
+    __shared__ uint16_t hyp_of[kMaxCand];       // flat candidate -> hypothesis slot of the launch
+    __shared__ int chunk_tot[kMaxGroups];
+    __shared__ unsigned long long chunk_min[kMaxGroups], pref[kMaxGroups];
     const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int M = match_count[p];
     if (M < 6) return;
-    // thread 0 updates the pair state after each chunk; the others follow best / niters / done
     int best = st[p].best, best_h = st[p].best_h, best_s = st[p].best_s, done = st[p].done, niters = st[p].niters;
     int n_models = st[p].n_models;
     uint32_t best_score = st[p].best_score;
@@ -1268,131 +1409,134 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
     const float thr2 = (float)(thr * thr);
     const float scale = __fdiv_rn(65536.0f, thr2);
     const float4* pts = pts_all + (size_t)p * mcap;
-    // kLds: the putatives are staged in LDS once (M <= 9600); oversize pairs read them from L2/HBM instead
+    // kLds: the putatives are staged in LDS in pair blocks, block j = {x1, y1, x2, y2} of points 2j and 2j + 1 as
+    // (a, b) pairs ({x1a, x1b, y1a, y1b}, {x2a, x2b, y2a, y2b}), so the packed evaluation reads its operand pairs
+    // straight into register pairs
+    float* spf = (float*)spts;
     if (kLds)
-        for (int i = tid; i < M; i += 64 * kScoreWaves) spts[i] = pts[i];
-    const float4* sp = kLds ? (const float4*)spts : pts;
-    long best_off = -1;  // cand offset of a winner found by this launch
+        for (int i = tid; i < M; i += kScoreThreads) {
+            const float4 v = pts[i];
+            float* b = spf + 8 * (i >> 1) + (i & 1);
+            b[0] = v.x; b[2] = v.y; b[4] = v.z; b[6] = v.w;
+        }
+    auto point = [&](int i) -> float4 {
+        if (!kLds) return pts[i];
+        const float* b = spf + 8 * (i >> 1) + (i & 1);
+        return make_float4(b[0], b[2], b[4], b[6]);
+    };
     RPROF_DECL
     RPROF_COUNT(18, 1);
-#pragma unroll 1
-    for (int g = 0; g < n_chunks && done < niters; ++g) {
-        const size_t hbase = (size_t)p * kMaxHyp + (size_t)g * kBatch;  // the chunk's first hypothesis slot
-        if (wave == 0) {
-            int v = nsol[hbase + lane];
+    // flattened candidate offsets over the chunks the solver kernels processed (those starting below niters)
+    const size_t hbase = (size_t)p * kMaxHyp;
+    for (int c = wave; c < n_chunks; c += kScoreThreads / 64) {
+        int v = done + c * kBatch < niters ? nsol[hbase + c * kBatch + lane] : 0;
 #pragma unroll
-            for (int m = 1; m < 64; m <<= 1) {  // inclusive scan over the 64 hypotheses
-                const int o = __shfl_up(v, m);
-                if (lane >= m) v += o;
-            }
-            flat_off[lane + 1] = v;
-            if (lane == 0) {
-                flat_off[0] = 0;
-                const uint32_t hi = kMsac ? ~best_score : (uint32_t)(best + 1);
-                best_key = ((unsigned long long)hi << 32) | 0xFFFFFFFFull;  // index -1: before all
-            }
+        for (int m = 1; m < 64; m <<= 1) {
+            const int o = __shfl_up(v, m);
+            if (lane >= m) v += o;
         }
-        __syncthreads();
-        RPROF(14);
-        const int total = flat_off[kBatch];
-        // candidate ci's E (fp64 in HBM); the next one of this wave is fetched while the current one is counted
-        auto fetch = [&](int ci, double (&e)[9]) {
-            const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
-            const double* ch = cand + (hbase + hl) * (kMaxSol * 9) + 9 * (ci - flat_off[hl]);
-#pragma unroll
-            for (int k = 0; k < 9; ++k) e[k] = ch[k];
-        };
-        double en[9];
-        if (wave < total) fetch(wave, en);
+        flat_off[c * kBatch + lane + 1] = v;
+        if (lane == 63) chunk_tot[c] = v;
+    }
+    // the pre-launch best as a key (flat index 0: before every candidate of this launch)
+    const uint32_t prev_bad = kMsac ? best_score : (best < 0 ? 0xFFFFFFFFu : (uint32_t)(M - best));
+    const unsigned long long prev_key = ((unsigned long long)prev_bad << 32) | (uint32_t)(best < 0 ? 0 : best);
+    if (tid < kMaxGroups) {
+        chunk_min[tid] = ~0ull;
+        pref[tid] = prev_key;
+    }
+    if (tid == 0) flat_off[0] = 0;
+    __syncthreads();
+    for (int h = tid; h < n_chunks * kBatch; h += kScoreThreads) {
+        int off = 0;
+        for (int j = 0; j < (h >> 6); ++j) off += chunk_tot[j];
+        flat_off[h + 1] += off;
+    }
+    __syncthreads();
+    for (int h = tid; h < n_chunks * kBatch; h += kScoreThreads) {
+        const int o = h == 0 ? 0 : flat_off[h], e = flat_off[h + 1];
+        for (int k = o; k < e; ++k) hyp_of[k] = (uint16_t)h;
+    }
+    __syncthreads();
+    const int total = flat_off[n_chunks * kBatch];
+    RPROF(14);
 #pragma unroll 1
-        for (int ci = wave; ci < total; ci += kScoreWaves) {
-            float E[9];
+    for (int ci = tid; ci < total; ci += kScoreThreads) {
+        const int h = hyp_of[ci], c = h >> 6;
+        const double* ch = cand + (hbase * kMaxSol * 9 + (size_t)9 * (ci - flat_off[h]) * kMaxHyp) + h;
+        float E[9];
 #pragma unroll
-            for (int e = 0; e < 9; ++e) E[e] = (float)en[e];
-            if (ci + kScoreWaves < total) fetch(ci + kScoreWaves, en);
-            const uint32_t my_low = 0xFFFFFFFEu - (uint32_t)ci;
-            int c = 0;
-            bool alive = true;
-            if constexpr (kMsac) {
-                uint32_t sc = 0;
+        for (int k = 0; k < 9; ++k) E[k] = (float)ch[(size_t)k * kMaxHyp];
+        const uint32_t myid = (uint32_t)ci + 1u;
+        uint32_t bad = 0;  // MSAC: partial score; RANSAC: outliers so far
+        int cnt = 0;
+        bool alive = true;
+        const int M4 = M & ~3;
 #pragma unroll 1
-                for (int base = 0; base < M; base += 64 * kMsacPpl) {  // 64 kMsacPpl points per reduction and exit test
-                    const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
-                    const int i = base + lane;
-                    uint32_t q = 0;
+        for (int base = 0; base < M; base += 4) {
+            const unsigned long long pk = __atomic_load_n(&pref[c], __ATOMIC_RELAXED);
+            const uint32_t pb = (uint32_t)(pk >> 32), pid = (uint32_t)(pk >> kKeyCountBits) & 0x1FFFu;
+            if (bad > pb || (bad == pb && myid > pid)) {
+                alive = false;
+                break;
+            }
+            if (base < M4) {  // four putatives as two packed pairs
 #pragma unroll
-                    for (int u = 0; u < kMsacPpl; ++u) {
-                        bool in = false;
-                        q += i + 64 * u < M ? msac_cost(E, sp[i + 64 * u], thr2, scale, in) : 0u;
-                        c += __popcll(__ballot(in));
+                for (int h = 0; h < 2; ++h) {
+                    f2 x1, y1, x2, y2;
+                    if (kLds) {
+                        const float4 lo = ((const float4*)spf)[(base >> 1) * 2 + 2 * h];
+                        const float4 hi = ((const float4*)spf)[(base >> 1) * 2 + 2 * h + 1];
+                        x1 = {lo.x, lo.y}; y1 = {lo.z, lo.w}; x2 = {hi.x, hi.y}; y2 = {hi.z, hi.w};
+                    } else {
+                        const float4 a = pts[base + 2 * h], b = pts[base + 2 * h + 1];
+                        x1 = {a.x, b.x}; y1 = {a.y, b.y}; x2 = {a.z, b.z}; y2 = {a.w, b.w};
                     }
-                    sc += wave_sum_u32(q);
-                    if (base + 64 * kMsacPpl < M) {
-                        const uint32_t bs = ~(uint32_t)(bk >> 32);
-                        if (sc > bs || (sc == bs && my_low < (uint32_t)bk)) {
-                            alive = false;
-                            break;
-                        }
-                    }
-                }
-                if (alive && lane == 0) {
-                    cand_cnt[ci] = c;
-                    atomicMax(&best_key, ((unsigned long long)(~sc) << 32) | my_low);
+                    score2<kMsac>(E, x1, y1, x2, y2, thr2, scale, bad, cnt);
                 }
                 continue;
             }
-#pragma unroll 1
-            for (int base = 0; base < M; base += 64) {
-                // read before the test so the LDS latency hides under it; a stale best is smaller, so the exit stays
-                // exact
-                const unsigned long long bk = __atomic_load_n(&best_key, __ATOMIC_RELAXED);
-                const int i = base + lane;
-                const bool in = i < M && sampson_inlier(E, sp[i], thr2);
-                c += __popcll(__ballot(in));
-                const int remaining = M - (base + 64);
-                if (remaining > 0) {
-                    const int bc = (int)(bk >> 32) - 1;
-                    if (c + remaining < bc || (c + remaining == bc && my_low < (uint32_t)bk)) {
-                        alive = false;
-                        break;
-                    }
+            for (int u = base; u < M; ++u) {
+                const float4 q = point(u);
+                if constexpr (kMsac) {
+                    bool in;
+                    bad += msac_cost(E, q, thr2, scale, in);
+                    cnt += in ? 1 : 0;
+                } else {
+                    const bool in = sampson_inlier(E, q, thr2);
+                    cnt += in ? 1 : 0;
+                    bad += in ? 0u : 1u;
                 }
             }
-            if (alive && lane == 0) atomicMax(&best_key, ((unsigned long long)(uint32_t)(c + 1) << 32) | my_low);
         }
-        RPROF(13);
-        __syncthreads();
-        if (wave == 0) {
-            const unsigned long long bk = best_key;
-            const uint32_t low = (uint32_t)bk;
-            // the winner's hypothesis: the first one whose running candidate count passes it (one ballot)
-            const int ci = (int)(0xFFFFFFFEu - low);
-            const int hl = __ffsll((unsigned long long)__ballot(flat_off[lane + 1] > ci)) - 1;
-            if (lane == 0) {
-                if (low != 0xFFFFFFFFu) {  // a candidate of this chunk beat the previous best
-                    const int sI = ci - flat_off[hl];
-                    if (kMsac) {
-                        best = cand_cnt[ci];
-                        best_score = ~(uint32_t)(bk >> 32);
-                    } else {
-                        best = (int)(bk >> 32) - 1;
-                    }
-                    best_h = done + hl;
-                    best_s = sI;
-                    best_off = (long)((hbase + hl) * (kMaxSol * 9) + 9 * sI);
-                }
-                if (best > 0) niters = min(niters, bound_tab[(size_t)p * (mcap + 1) + best]);
-                n_models += total;
-                sh_bound[0] = best;
-                sh_bound[1] = niters;
-            }
+        if (alive) {
+            const unsigned long long key = ((unsigned long long)bad << 32) |
+                                           ((unsigned long long)myid << kKeyCountBits) | (unsigned long long)cnt;
+            atomicMin(&chunk_min[c], key);
+            for (int j = c; j < n_chunks; ++j) atomicMin(&pref[j], key);
         }
-        __syncthreads();  // flat_off / best_key are rewritten by the next chunk
-        best = sh_bound[0];
-        niters = sh_bound[1];
-        done += kBatch;
     }
+    RPROF(13);
+    __syncthreads();
     if (tid == 0) {
+        long best_off = -1;  // cand offset of a winner found by this launch
+        unsigned long long cur = prev_key;
+        for (int c = 0; c < n_chunks && done < niters; ++c) {
+            const unsigned long long k = chunk_min[c];
+            if (k < cur) {  // a candidate of this chunk beat the best so far
+                cur = k;
+                const int ci = (int)((k >> kKeyCountBits) & 0x1FFFu) - 1;
+                const int h = hyp_of[ci], sI = ci - flat_off[h];
+                best = (int)(k & ((1u << kKeyCountBits) - 1u));
+                if (kMsac) best_score = (uint32_t)(k >> 32);
+                best_h = done + (h & (kBatch - 1));
+                best_s = sI;
+                best_off = (long)(hbase * kMaxSol * 9 + (size_t)9 * sI * kMaxHyp + h);
+            }
+            if (best > 0) niters = min(niters, bound_tab[(size_t)p * (mcap + 1) + best]);
+            n_models += flat_off[(c + 1) * kBatch] - flat_off[c * kBatch];
+            done += kBatch;
+        }
         PairState& o = st[p];
         o.best = best;
         o.best_h = best_h;
@@ -1402,7 +1546,7 @@ __global__ __launch_bounds__(64 * kScoreWaves) void ransac_score_kernel(const in
         o.n_models = n_models;
         o.best_score = best_score;
         if (best_off >= 0)
-            for (int e = 0; e < 9; ++e) o.bestE[e] = cand[best_off + e];
+            for (int e = 0; e < 9; ++e) o.bestE[e] = cand[best_off + (size_t)e * kMaxHyp];
     }
 }
 
@@ -1637,9 +1781,10 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     hipLaunchKernelGGL(ransac_init_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, stream, st, n_pairs, max_iters);
     GTSFM_CHECK_HIP(hipGetLastError());
     GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_solve1_kernel, (int)kSolveLds));
-    // the score kernel stages a pair's putatives in LDS when they fit (16 B each, up to 150 KiB)
-    const bool score_in_lds = (size_t)mcap * sizeof(float4) <= 150 * 1024;
-    const size_t score_lds = score_in_lds ? (size_t)mcap * sizeof(float4) : 0;
+    // the score kernel stages a pair's putatives in LDS when they fit (16 B each, up to 136 KiB beside its tables)
+    const size_t score_pts = (size_t)((mcap + 1) & ~1) * sizeof(float4);  // pair blocks of 32 B
+    const bool score_in_lds = score_pts <= 136 * 1024;
+    const size_t score_lds = score_in_lds ? score_pts : 0;
     if (score_lds > 65536) {
         GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true, false>, (int)score_lds));
         GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true, true>, (int)score_lds));
@@ -1657,7 +1802,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
                            d_match_count, mcap, x1n, x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs, g), dim3(64), kRootLds, stream, d_match_count, st,
                            stage, cand, nsol);
-        hipLaunchKernelGGL(score_fn, dim3(n_pairs), dim3(64 * kScoreWaves), score_lds, stream, d_pairs, d_intrinsics,
+        hipLaunchKernelGGL(score_fn, dim3(n_pairs), dim3(kScoreThreads), score_lds, stream, d_pairs, d_intrinsics,
                            d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
     }
     GTSFM_CHECK_HIP(hipGetLastError());

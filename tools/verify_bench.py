@@ -50,7 +50,8 @@ def main():
         os.makedirs(os.path.dirname(ref_path), exist_ok=True)
         np.savez(ref_path, **cur)
     print(json.dumps({"lib": os.path.relpath(native.LIB_PATH, REPO), "stage_ms": st,
-                      "hyp_total": int(n_hyp.sum()), "same_as_ref": same}), flush=True)
+                      "hyp_total": int(n_hyp.sum()),
+                      "hyp_chunks_hist": np.bincount((n_hyp + 63) // 64, minlength=17).tolist(), "same_as_ref": same}), flush=True)
 
 
 if __name__ == "__main__":
