@@ -1032,6 +1032,30 @@ __device__ __forceinline__ double shfl_xor_d(double v, int m) {
     return __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
+// Wave-wide fp64 sum, uniform result (read from lane 63): the DPP scan of wave_sum_u32 on the two halves of each
+// double (row_shr 1, 2, 4, 8 inside rows of 16, then row_bcast 15 / 31), all VALU, no LDS permutes. A fixed order,
+// so the result is deterministic.
+__device__ __forceinline__ double dpp_f64(double v, int ctrl_sel) {
+    const long long b = __double_as_longlong(v);
+    int lo = (int)(b & 0xffffffffll), hi = (int)(b >> 32);
+    switch (ctrl_sel) {
+        case 0: lo = __builtin_amdgcn_update_dpp(0, lo, 0x111, 0xf, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x111, 0xf, 0xf, false); break;
+        case 1: lo = __builtin_amdgcn_update_dpp(0, lo, 0x112, 0xf, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x112, 0xf, 0xf, false); break;
+        case 2: lo = __builtin_amdgcn_update_dpp(0, lo, 0x114, 0xf, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x114, 0xf, 0xf, false); break;
+        case 3: lo = __builtin_amdgcn_update_dpp(0, lo, 0x118, 0xf, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x118, 0xf, 0xf, false); break;
+        case 4: lo = __builtin_amdgcn_update_dpp(0, lo, 0x142, 0xa, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x142, 0xa, 0xf, false); break;
+        default: lo = __builtin_amdgcn_update_dpp(0, lo, 0x143, 0xc, 0xf, false); hi = __builtin_amdgcn_update_dpp(0, hi, 0x143, 0xc, 0xf, false); break;
+    }
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) v += dpp_f64(v, c);
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), 63), hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 // Wave-cooperative Sampson-weighted 8-point refit (see oracle refit_essential). The 45 unique normal-matrix
 // entries are summed per lane, then butterfly-reduced across the wave (fixed order: deterministic).
 __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const double* Esel, double th2,
@@ -1058,8 +1082,7 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
     for (int m = 32; m >= 1; m >>= 1) n += __shfl_xor(n, m);
     if (n < 8) return false;
 #pragma unroll
-    for (int k = 0; k < 45; ++k)
-        for (int m = 1; m < 64; m <<= 1) acc[k] += shfl_xor_d(acc[k], m);
+    for (int k = 0; k < 45; ++k) acc[k] = wave_sum_f64(acc[k]);
     // Smallest eigenvector of the normal matrix: shifted inverse iteration on its Cholesky factor, register-resident
     // and computed redundantly by every lane (no LDS, no barriers). The shift (1e-12 of the trace) keeps the factor
     // positive definite; 8 iterations contract the other eigen-directions by ((l1 + s) / (l2 + s))^8. Same

@@ -45,6 +45,7 @@ class FrontEndConfig:
     extract_first: int = 20          # host steps: size of a smaller first chunk (less exposed H2D); 0 = extract_chunk
     resident_chunk: int = 100        # device-resident steps: images per SIFT launch sequence (bounded by workspace)
     pair_chunk: int = 131072         # pairs per match / verify / compact launch sequence (C4: 272k -> 283k pairs/s vs 32768)
+    overlap: bool = True             # match of pair chunk c + 1 on a second stream while chunk c verifies
     bundle_adjust: bool = False      # TwoViewEstimator bundle_adjust_2view: two-view triangulation + BA after RANSAC
     ba_max_iters: int = 100          # bundle_adjust_2view_maxiters
     ba_reproj_thresh: float = 0.5    # ba_reproj_error_thresholds[-1]
@@ -284,6 +285,8 @@ class AllPairsFrontEnd:
         if self.cuda:
             self.copy_stream = torch.cuda.Stream(device=self.dev)
             self.copy_done = [torch.cuda.Event() for _ in self.chunks]
+            self.match_stream = torch.cuda.Stream(device=self.dev)
+            self.match_done = [torch.cuda.Event() for _ in self.pchunks]
         self.instrument = False
         self.marks: List[Tuple[str, object]] = []
         self.copy_marks: List[Tuple[str, object]] = []
@@ -350,9 +353,39 @@ class AllPairsFrontEnd:
         xy_all = f_all.xy
         self._mark("allgather")
         n_hyp, n_models, n_match = [], [], []
+        # With several pair chunks, the matcher runs on its own stream one chunk ahead: the distance GEMM of chunk
+        # c + 1 (MFMA) overlaps the RANSAC of chunk c (fp64 VALU) and fills the verifier's launch tails. Instrumented
+        # steps stay sequential so that every stage's events bracket that stage alone.
+        overlap = self.cuda and cfg.overlap and not self.instrument and len(self.pchunks) > 1
+        matched = {}
+
+        def issue_match(c: int):
+            a, b = self.pchunks[c]
+            if overlap:
+                with torch.cuda.stream(self.match_stream):
+                    matched[c] = self.kern.match(f_all, self.pairs_dev[a:b], cfg.ratio, groups=self.pgroups[c],
+                                                 image_hw=self.image_hw)
+                    self.match_done[c].record(self.match_stream)
+            else:
+                matched[c] = self.kern.match(f_all, self.pairs_dev[a:b], cfg.ratio, groups=self.pgroups[c],
+                                             image_hw=self.image_hw)
+
+        if overlap:
+            self.match_stream.wait_stream(torch.cuda.current_stream(self.dev))  # features gathered
+            issue_match(0)
         for c, (a, b) in enumerate(self.pchunks):
             pairs = self.pairs_dev[a:b]
-            idx, mcnt = self.kern.match(f_all, pairs, cfg.ratio, groups=self.pgroups[c], image_hw=self.image_hw)
+            if overlap:
+                cs = torch.cuda.current_stream(self.dev)
+                cs.wait_event(self.match_done[c])
+                if c + 1 < len(self.pchunks):
+                    issue_match(c + 1)
+                idx, mcnt = matched.pop(c)
+                idx.record_stream(cs)  # allocated on the match stream, read here
+                mcnt.record_stream(cs)
+            else:
+                issue_match(c)
+                idx, mcnt = matched.pop(c)
             self._mark("match")
             res = self.kern.verify(xy_all, self.intr, pairs, idx, mcnt, cfg.thresh_px, self.pair_id_base + a)
             self._mark("verify")
