@@ -1336,7 +1336,15 @@ __global__ __launch_bounds__(64, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         if (five_point_stage1(s1, s2, mem, part, N, Rt)) {
             ok = 1;
             double* out = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
+#ifdef GTSFM_S1_NOSTORE  // timing experiment only: the stage stores replaced by one dependent store
+            double acc = 0.0;
+            for (int r = 0; r < 6; ++r) for (int j = 0; j < 10; ++j) acc += Rt[r][j];
+            for (int k = 0; k < 4; ++k) for (int j = 0; j < 9; ++j) acc += N[k][j];
+            if (acc == 12345.678) out[0] = acc;
+            if (false) {
+#else
             if (part) {
+#endif
 #pragma unroll
                 for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -1397,7 +1405,7 @@ __global__ __launch_bounds__(64, 2) void ransac_solve2_kernel(const int* __restr
 // (oracle/ransac.c:679-706): best = min(best, chunk minimum), the iteration bound from the best count, done += 64,
 // stop once done >= niters (chunks past that point were solved speculatively and are discarded).
 #ifndef GTSFM_SCORE_THREADS
-#define GTSFM_SCORE_THREADS 256
+#define GTSFM_SCORE_THREADS 512  // measured 64 / 128 / 256 / 512: 11.9 / 9.1 / 7.8 / 7.4 ms C2 verify
 #endif
 constexpr int kScoreThreads = GTSFM_SCORE_THREADS;
 constexpr int kMaxCand = kMaxHyp * kMaxSol;  // candidates one launch may hold per pair (13 bits of the key)
