@@ -1491,61 +1491,71 @@ __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* 
     __syncthreads();
     const int total = flat_off[n_chunks * kBatch];
     RPROF(14);
-#pragma unroll 1
-    for (int ci = tid; ci < total; ci += kScoreThreads) {
-        const int h = hyp_of[ci], c = h >> 6;
+    auto finish = [&](int c, uint32_t myid, uint32_t bad, int cnt) {
+        const unsigned long long key = ((unsigned long long)bad << 32) |
+                                       ((unsigned long long)myid << kKeyCountBits) | (unsigned long long)cnt;
+        atomicMin(&chunk_min[c], key);
+        for (int j = c; j < n_chunks; ++j) atomicMin(&pref[j], key);
+    };
+    // one block of up to four putatives (block b = points 4b .. 4b + 3), packed pairs when the block is full
+    auto block = [&](const float (&E)[9], int b, uint32_t& bad, int& cnt) {
+        const int base = 4 * b;
+        if (base + 4 <= M) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                f2 x1, y1, x2, y2;
+                if (kLds) {
+                    const float4 lo = ((const float4*)spf)[(base >> 1) * 2 + 2 * h];
+                    const float4 hi = ((const float4*)spf)[(base >> 1) * 2 + 2 * h + 1];
+                    x1 = {lo.x, lo.y}; y1 = {lo.z, lo.w}; x2 = {hi.x, hi.y}; y2 = {hi.z, hi.w};
+                } else {
+                    const float4 a = pts[base + 2 * h], q = pts[base + 2 * h + 1];
+                    x1 = {a.x, q.x}; y1 = {a.y, q.y}; x2 = {a.z, q.z}; y2 = {a.w, q.w};
+                }
+                score2<kMsac>(E, x1, y1, x2, y2, thr2, scale, bad, cnt);
+            }
+            return;
+        }
+        for (int u = base; u < M; ++u) {
+            const float4 q = point(u);
+            if constexpr (kMsac) {
+                bool in;
+                bad += msac_cost(E, q, thr2, scale, in);
+                cnt += in ? 1 : 0;
+            } else {
+                const bool in = sampson_inlier(E, q, thr2);
+                cnt += in ? 1 : 0;
+                bad += in ? 0u : 1u;
+            }
+        }
+    };
+    auto load_E = [&](int ci, float (&E)[9], int& c) {
+        const int h = hyp_of[ci];
+        c = h >> 6;
         const double* ch = cand + (hbase * kMaxSol * 9 + (size_t)9 * (ci - flat_off[h]) * kMaxHyp) + h;
-        float E[9];
 #pragma unroll
         for (int k = 0; k < 9; ++k) E[k] = (float)ch[(size_t)k * kMaxHyp];
+    };
+#pragma unroll 1
+    for (int ci = tid; ci < total; ci += kScoreThreads) {
+        float E[9];
+        int c;
+        load_E(ci, E, c);
         const uint32_t myid = (uint32_t)ci + 1u;
         uint32_t bad = 0;  // MSAC: partial score; RANSAC: outliers so far
         int cnt = 0;
         bool alive = true;
-        const int M4 = M & ~3;
 #pragma unroll 1
-        for (int base = 0; base < M; base += 4) {
+        for (int b = 0; 4 * b < M; ++b) {
             const unsigned long long pk = __atomic_load_n(&pref[c], __ATOMIC_RELAXED);
             const uint32_t pb = (uint32_t)(pk >> 32), pid = (uint32_t)(pk >> kKeyCountBits) & 0x1FFFu;
             if (bad > pb || (bad == pb && myid > pid)) {
                 alive = false;
                 break;
             }
-            if (base < M4) {  // four putatives as two packed pairs
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    f2 x1, y1, x2, y2;
-                    if (kLds) {
-                        const float4 lo = ((const float4*)spf)[(base >> 1) * 2 + 2 * h];
-                        const float4 hi = ((const float4*)spf)[(base >> 1) * 2 + 2 * h + 1];
-                        x1 = {lo.x, lo.y}; y1 = {lo.z, lo.w}; x2 = {hi.x, hi.y}; y2 = {hi.z, hi.w};
-                    } else {
-                        const float4 a = pts[base + 2 * h], b = pts[base + 2 * h + 1];
-                        x1 = {a.x, b.x}; y1 = {a.y, b.y}; x2 = {a.z, b.z}; y2 = {a.w, b.w};
-                    }
-                    score2<kMsac>(E, x1, y1, x2, y2, thr2, scale, bad, cnt);
-                }
-                continue;
-            }
-            for (int u = base; u < M; ++u) {
-                const float4 q = point(u);
-                if constexpr (kMsac) {
-                    bool in;
-                    bad += msac_cost(E, q, thr2, scale, in);
-                    cnt += in ? 1 : 0;
-                } else {
-                    const bool in = sampson_inlier(E, q, thr2);
-                    cnt += in ? 1 : 0;
-                    bad += in ? 0u : 1u;
-                }
-            }
+            block(E, b, bad, cnt);
         }
-        if (alive) {
-            const unsigned long long key = ((unsigned long long)bad << 32) |
-                                           ((unsigned long long)myid << kKeyCountBits) | (unsigned long long)cnt;
-            atomicMin(&chunk_min[c], key);
-            for (int j = c; j < n_chunks; ++j) atomicMin(&pref[j], key);
-        }
+        if (alive) finish(c, myid, bad, cnt);
     }
     RPROF(13);
     __syncthreads();

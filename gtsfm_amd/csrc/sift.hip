@@ -319,12 +319,16 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
     for (int iy = tid / kBlurRowThr; iy < IH; iy += kBlurTX * kBlurTYT / kBlurRowThr) {
         const int g8 = (tid % kBlurRowThr) * kBlurRowOut;
         float* rowp = in + iy * IWP;
-        const float2* wp = (const float2*)(rowp + g8);
+        // volatile 8-byte reads: the compiler would otherwise pair them into ds_read2_b64, which banks by 16-lane
+        // groups mod 32 dwords (two rows x 8 lanes at an 8-dword stride: 2-way conflicts); ds_read_b64 banks by
+        // 32-lane groups mod 64, where the row stride IWP = 2 (mod 8) keeps the four rows' windows conflict-free
+        typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;
+        lds_u64* wp = (lds_u64*)(rowp + g8);
         float v[2 * NV];
 #pragma unroll
         for (int q = 0; q < NV; ++q) {
-            const float2 w2 = wp[q];
-            v[2 * q] = w2.x; v[2 * q + 1] = w2.y;
+            const unsigned long long w2 = wp[q];
+            v[2 * q] = __uint_as_float((uint32_t)w2); v[2 * q + 1] = __uint_as_float((uint32_t)(w2 >> 32));
         }
         asm volatile("" ::: "memory");  // all window reads issue before the in-place writes (neighbour lanes' windows)
         // two outputs per packed-fp32 op (v_pk_add_f32 / v_pk_fma_f32); per-lane rounding unchanged

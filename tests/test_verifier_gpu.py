@@ -150,3 +150,42 @@ def test_too_few_and_degenerate_in_batch(dev):
     st = res.status.cpu().numpy()
     assert st[0] == native.RANSAC_STATUS_TOO_FEW
     assert st[1] in (native.RANSAC_STATUS_OK, native.RANSAC_STATUS_NO_MODEL)  # collinear points: degenerate
+
+
+@pytest.mark.gpu
+def test_putatives_beyond_lds_staging(dev, oracle_mod):
+    """A pair with more putatives than the score kernel stages in LDS (> 8704: points read from global memory), and a
+    small pair in the same launch, against the oracle (same bar as the batched parity test)."""
+    from gtsfm_amd import device, native
+
+    rng = np.random.default_rng(31)
+    kps, Ks, Ms = [], [], []
+    for n_in, n_out in ((6000, 3500), (300, 200)):
+        kp1, kp2, K, _, _, _ = scenes.random_two_view(rng, n_in, n_out)
+        kps.append((kp1, kp2))
+        Ks.append(K)
+        Ms.append(len(kp1))
+    kmax = max(Ms)
+    assert kmax * 16 > 136 * 1024
+    kp = np.zeros((4, kmax, 2), np.float32)
+    intr = np.zeros((4, 3))
+    mi = np.zeros((2, kmax, 2), np.int32)
+    for p, ((a, b), K) in enumerate(zip(kps, Ks)):
+        kp[2 * p, : len(a)] = a
+        kp[2 * p + 1, : len(b)] = b
+        intr[2 * p] = intr[2 * p + 1] = (K[0, 0], K[0, 2], K[1, 2])
+        mi[p, : Ms[p]] = np.arange(Ms[p])[:, None]
+    res = device.ransac_essential(torch.from_numpy(kp).to(dev), torch.from_numpy(intr).to(dev),
+                                  torch.tensor([[0, 1], [2, 3]], dtype=torch.int32, device=dev),
+                                  torch.from_numpy(mi).to(dev), torch.tensor(Ms, dtype=torch.int32, device=dev), 4.0)
+    for p in range(2):
+        K = Ks[p]
+        a, b = kps[p]
+        x1 = (a.astype(np.float32).astype(np.float64) - K[:2, 2]) / K[0, 0]
+        x2 = (b.astype(np.float32).astype(np.float64) - K[:2, 2]) / K[0, 0]
+        _, rmask, rR, rt, rn, rh = oracle_mod.ransac_E(x1, x2, 4.0 / K[0, 0], pair_id=p)
+        assert int(res.status[p]) == native.RANSAC_STATUS_OK
+        assert int(res.n_hyp[p]) == rh, (p, int(res.n_hyp[p]), rh)
+        assert abs(int(res.n_inliers[p]) - rn) <= max(1, 0.01 * rn), (p, int(res.n_inliers[p]), rn)
+        assert scenes.rotation_angle_deg(res.R[p].cpu().numpy(), rR) < 0.05, p
+        assert scenes.direction_angle_deg(res.t[p].cpu().numpy(), rt) < 0.05, p

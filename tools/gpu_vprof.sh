@@ -11,7 +11,7 @@ for so in gtsfm_amd/_lib/libgtsfm_hip.so build_var/libgtsfm_hip_*.so; do
   case $so in *_old.so) continue;; esac
   n=$(basename $so .so)
   GTSFM_HIP_LIB=$so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/vp_${TAG}_$n -o run -- python -u tools/verify_bench.py >> gpurun_out/vp_${TAG}.jsonl 2>&1 || { tail -5 gpurun_out/vp_${TAG}.jsonl; exit 1; }
-  echo "== $n"; grep '^{' gpurun_out/vp_${TAG}.jsonl | tail -1 | cut -c1-400
+  rm -rf gpurun_out/vp_${TAG}_$n.keep; echo "== $n"; grep '^{' gpurun_out/vp_${TAG}.jsonl | tail -1 | cut -c1-400
   python tools/kstats.py "$(find gpurun_out/vp_${TAG}_$n -name "*kernel_stats.csv" | head -1)" | grep -i "ransac"
 done
 exit 0
