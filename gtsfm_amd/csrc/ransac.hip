@@ -1098,7 +1098,9 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
 #pragma unroll
         for (int i = 0; i < 9; ++i) tr += A(i, i);
         const double shift = 1e-12 * tr;
-        double L[45];  // packed lower triangle, row i at i (i + 1) / 2
+        // The factor's diagonal is kept as reciprocals (nine divisions instead of 36 in the factorisation and 144 in
+        // the eight inverse-iteration solves): fp64 division is a ~10-instruction sequence.
+        double L[45];  // packed lower triangle, row i at i (i + 1) / 2; the diagonal entries hold 1 / L_ii
         bool ok = tr > 0.0;
 #pragma unroll
         for (int i = 0; i < 9; ++i)
@@ -1109,9 +1111,9 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
                 for (int k = 0; k < j; ++k) v -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
                 if (i == j) {
                     ok = ok && v > 0.0;
-                    L[i * (i + 1) / 2 + i] = sqrt(fmax(v, 1e-300));
+                    L[i * (i + 1) / 2 + i] = 1.0 / sqrt(fmax(v, 1e-300));
                 } else {
-                    L[i * (i + 1) / 2 + j] = v / L[j * (j + 1) / 2 + j];
+                    L[i * (i + 1) / 2 + j] = v * L[j * (j + 1) / 2 + j];
                 }
             }
         if (ok) {
@@ -1124,14 +1126,14 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
                     double v = x[i];
 #pragma unroll
                     for (int k = 0; k < i; ++k) v -= L[i * (i + 1) / 2 + k] * x[k];
-                    x[i] = v / L[i * (i + 1) / 2 + i];
+                    x[i] = v * L[i * (i + 1) / 2 + i];
                 }
 #pragma unroll
                 for (int i = 8; i >= 0; --i) {  // L^T z = y
                     double v = x[i];
 #pragma unroll
                     for (int k = i + 1; k < 9; ++k) v -= L[k * (k + 1) / 2 + i] * x[k];
-                    x[i] = v / L[i * (i + 1) / 2 + i];
+                    x[i] = v * L[i * (i + 1) / 2 + i];
                 }
                 double nrm = 0.0;
 #pragma unroll
