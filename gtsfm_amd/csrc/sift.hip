@@ -535,7 +535,10 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 #ifndef GTSFM_EX_STRIP
 #define GTSFM_EX_STRIP 64
 #endif
-constexpr int kExWaves = 4, kExOut = 62, kExStrip = GTSFM_EX_STRIP;
+#ifndef GTSFM_EX_WAVES
+#define GTSFM_EX_WAVES 4
+#endif
+constexpr int kExWaves = GTSFM_EX_WAVES, kExOut = 62, kExStrip = GTSFM_EX_STRIP;
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
