@@ -1414,7 +1414,7 @@ constexpr int kMaxCand = kMaxHyp * kMaxSol;  // candidates one launch may hold p
 static_assert(kMaxCand < (1 << 13), "flat candidate index must fit the key's 13 bits");
 constexpr int kKeyCountBits = 19;
 
-template <bool kLds, bool kMsac>
+template <bool kLds, bool kMsac, int kS>
 __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* __restrict__ pairs,
                                                                     const double* __restrict__ intr,
                                                                     const int* __restrict__ match_count, int mcap,
@@ -1538,26 +1538,41 @@ __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* 
 #pragma unroll
         for (int k = 0; k < 9; ++k) E[k] = (float)ch[(size_t)k * kMaxHyp];
     };
+    // kS lanes per candidate (a power of two <= 64, aligned groups inside a wave): lane `sub` of the group takes the
+    // point blocks sub, sub + kS, ...; the group's partial badness (a butterfly sum over its lanes) drives the exact
+    // pruning test and the final key. kS = 1 for launches with many pairs; the host picks kS = 16 when a launch's
+    // candidates alone would not fill the GPU (few pairs with many putatives, e.g. C1's 66 pairs of ~2000).
+    const int sub = tid & (kS - 1), grp = tid / kS;
+    auto gsum = [&](uint32_t v) {
+#pragma unroll
+        for (int m = 1; m < kS; m <<= 1) v += (uint32_t)__shfl_xor((int)v, m);
+        return v;
+    };
+    const int nb = (M + 3) >> 2, n_it = (nb + kS - 1) / kS;
 #pragma unroll 1
-    for (int ci = tid; ci < total; ci += kScoreThreads) {
+    for (int ci = grp; ci < total; ci += kScoreThreads / kS) {
         float E[9];
         int c;
         load_E(ci, E, c);
         const uint32_t myid = (uint32_t)ci + 1u;
-        uint32_t bad = 0;  // MSAC: partial score; RANSAC: outliers so far
+        uint32_t bad = 0;  // MSAC: partial score; RANSAC: outliers so far (this lane's blocks)
         int cnt = 0;
         bool alive = true;
 #pragma unroll 1
-        for (int b = 0; 4 * b < M; ++b) {
+        for (int it = 0; it < n_it; ++it) {
             const unsigned long long pk = __atomic_load_n(&pref[c], __ATOMIC_RELAXED);
             const uint32_t pb = (uint32_t)(pk >> 32), pid = (uint32_t)(pk >> kKeyCountBits) & 0x1FFFu;
-            if (bad > pb || (bad == pb && myid > pid)) {
+            const uint32_t gb = gsum(bad);  // uniform over the group
+            if (gb > pb || (gb == pb && myid > pid)) {
                 alive = false;
                 break;
             }
-            block(E, b, bad, cnt);
+            const int b = it * kS + sub;
+            if (b < nb) block(E, b, bad, cnt);
         }
-        if (alive) finish(c, myid, bad, cnt);
+        bad = gsum(bad);
+        cnt = (int)gsum((uint32_t)cnt);
+        if (alive && sub == 0) finish(c, myid, bad, cnt);
     }
     RPROF(13);
     __syncthreads();
@@ -1828,12 +1843,19 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     const size_t score_pts = (size_t)((mcap + 1) & ~1) * sizeof(float4);  // pair blocks of 32 B
     const bool score_in_lds = score_pts <= 136 * 1024;
     const size_t score_lds = score_in_lds ? score_pts : 0;
-    if (score_lds > 65536) {
-        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true, false>, (int)score_lds));
-        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_score_kernel<true, true>, (int)score_lds));
-    }
-    const auto score_fn = score_in_lds ? (msac ? ransac_score_kernel<true, true> : ransac_score_kernel<true, false>)
-                                       : (msac ? ransac_score_kernel<false, true> : ransac_score_kernel<false, false>);
+    // lanes per candidate: 1, unless the launch's candidates (~272 per pair and chunk) would leave most of the GPU's
+    // lanes idle while each walks many putatives
+    const bool wide = (size_t)n_pairs * 272 < (size_t)64 * 1024 * 2 && mcap >= 256;
+    using ScoreFn = void (*)(const int*, const double*, const int*, int, const float4*, double, double, const double*,
+                             const int*, int, const int*, PairState*);
+    ScoreFn score_fn;
+    if (wide)
+        score_fn = score_in_lds ? (msac ? ransac_score_kernel<true, true, 16> : ransac_score_kernel<true, false, 16>)
+                                : (msac ? ransac_score_kernel<false, true, 16> : ransac_score_kernel<false, false, 16>);
+    else
+        score_fn = score_in_lds ? (msac ? ransac_score_kernel<true, true, 1> : ransac_score_kernel<true, false, 1>)
+                                : (msac ? ransac_score_kernel<false, true, 1> : ransac_score_kernel<false, false, 1>);
+    if (score_lds > 65536) GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)score_fn, (int)score_lds));
     // Chunks of 64 hypotheses, as the oracle; launches cover 1, 1, 2, 4, 8, 8, ... chunks. Most pairs stop within the
     // first two chunks; the pairs that run on are few, so their later chunks are solved together (speculatively: a
     // chunk the score kernel does not reach is discarded) to give the solver kernels enough waves.
