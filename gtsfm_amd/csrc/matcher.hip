@@ -1123,8 +1123,10 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     if (h == 0 && qn < nq) {
         const size_t o = ((size_t)side * n_pairs + p) * kmax + qn;
 #pragma unroll
-        for (int c = 0; c < kFlCand; ++c) cand[o * kFlCand + c] = id[c];
-        tkey[o] = v[kFlCand - 1];
+        for (int c = 0; c < kFlCand; ++c) {
+            cand[o * kFlCand + c] = id[c];
+            tkey[o * kFlCand + c] = v[c];  // ascending keys; the last one bounds every keypoint off the shortlist
+        }
     }
 }
 
@@ -1151,35 +1153,64 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
     const int i0 = blockIdx.x * kFlRerankRows;
     if (i0 >= nq) return;
     const int r = tid / kFlCand, c = tid % kFlCand, i = i0 + r;
+    // the exact squared distance of this thread's candidate, sequential and unfused (exact_top2_kernel's arithmetic)
+    auto exact_d2 = [&](int jj) {
+        const float* q = desc + ((size_t)iq * kmax + i) * dim;
+        const float* t = desc + ((size_t)it * kmax + jj) * dim;
+        float a = 0.f;
+        if ((dim & 3) == 0) {
+            const float4* q4 = (const float4*)q;
+            const float4* t4 = (const float4*)t;
+#pragma unroll 8
+            for (int k = 0; k < dim / 4; ++k) {
+                const float4 x = q4[k], y = t4[k];
+                const float e0 = x.x - y.x, e1 = x.y - y.y, e2 = x.z - y.z, e3 = x.w - y.w;
+                a = a + e0 * e0;  // unfused, in index order: contract(off) above
+                a = a + e1 * e1;
+                a = a + e2 * e2;
+                a = a + e3 * e3;
+            }
+        } else {
+            for (int k = 0; k < dim; ++k) {
+                const float df = q[k] - t[k];
+                a = a + df * df;
+            }
+        }
+        return a;
+    };
+    // the certificate's bound on the fp16 key error: (|a|^2 + key) - eps <= exact d^2 for every train keypoint
+    const bool safe = img_unsafe[iq] == 0u && img_unsafe[it] == 0u;
+    auto key_eps = [&](float na) {
+        const float an = sqrtf(na), bn = __uint_as_float(img_maxnorm[it]);
+        const float u = 1.f / 2048.f, eta = 1.f / 33554432.f, D = (float)dim;
+        const float e_dot = (2.f * u + u * u + D * 1.01f / 16777216.f) * an * bn + eta * sqrtf(D) * (an + bn) +
+                            D * eta * eta;
+        return 1.5f * (2.f * e_dot + (D + 4.f) * 2.f / 16777216.f * (na + bn * bn));
+    };
+    const size_t o = ((size_t)side * n_pairs + p) * kmax + i;
     int j = -1;
     float acc = __builtin_inff();
     if (i < nq) {
-        j = cand[(((size_t)side * n_pairs + p) * kmax + i) * kFlCand + c];
+        j = cand[o * kFlCand + c];
         if (j >= nt) j = -1;
-        if (j >= 0) {
-            const float* q = desc + ((size_t)iq * kmax + i) * dim;
-            const float* t = desc + ((size_t)it * kmax + j) * dim;
-            acc = 0.f;
-            if ((dim & 3) == 0) {
-                const float4* q4 = (const float4*)q;
-                const float4* t4 = (const float4*)t;
-#pragma unroll 8
-                for (int k = 0; k < dim / 4; ++k) {
-                    const float4 a = q4[k], b = t4[k];
-                    const float e0 = a.x - b.x, e1 = a.y - b.y, e2 = a.z - b.z, e3 = a.w - b.w;
-                    acc = acc + e0 * e0;  // unfused, in index order: contract(off) above
-                    acc = acc + e1 * e1;
-                    acc = acc + e2 * e2;
-                    acc = acc + e3 * e3;
-                }
-            } else {
-                for (int k = 0; k < dim; ++k) {
-                    const float df = q[k] - t[k];
-                    acc = acc + df * df;
-                }
-            }
-        }
     }
+    // Two rounds. The two best keys' candidates first; then a candidate whose key bound already exceeds the larger of
+    // those two exact distances (d^2 >= (|a|^2 + key) - eps > that) can be neither of the exact top two, nor tie
+    // them, and is dropped instead of summed (its slot reads as empty in the scan below).
+    if (c < 2 && j >= 0) acc = exact_d2(j);
+    sacc[r][c] = acc;
+    __syncthreads();
+    if (c >= 2 && j >= 0) {
+        const float a2 = fmaxf(sacc[r][0], sacc[r][1]);
+        bool skip = false;
+        if (safe && a2 < __builtin_inff()) {
+            const float na = norm2[(size_t)iq * kpad + i];
+            skip = (na + tkey[o * kFlCand + c]) - key_eps(na) > a2 * (1.f + 1e-4f) + key_eps(na);
+        }
+        if (skip) j = -1;
+        else acc = exact_d2(j);
+    }
+    __syncthreads();
     sacc[r][c] = acc;
     sj[r][c] = j;
     __syncthreads();
@@ -1211,14 +1242,11 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
         }
     }
     bool certified = nt <= kFlCand;
-    if (!certified && img_unsafe[iq] == 0u && img_unsafe[it] == 0u) {
+    if (!certified && safe) {
         const float na = norm2[(size_t)iq * kpad + ii];
-        const float an = sqrtf(na), bn = __uint_as_float(img_maxnorm[it]);
-        const float u = 1.f / 2048.f, eta = 1.f / 33554432.f, D = (float)dim;
-        const float e_dot = (2.f * u + u * u + D * 1.01f / 16777216.f) * an * bn + eta * sqrtf(D) * (an + bn) +
-                            D * eta * eta;
-        const float eps = 1.5f * (2.f * e_dot + (D + 4.f) * 2.f / 16777216.f * (na + bn * bn));
-        certified = (na + tkey[((size_t)side * n_pairs + p) * kmax + ii]) - eps > a2 * (1.f + 1e-4f) + eps;
+        const float eps = key_eps(na);
+        certified = (na + tkey[(((size_t)side * n_pairs + p) * kmax + ii) * kFlCand + kFlCand - 1]) - eps >
+                    a2 * (1.f + 1e-4f) + eps;
     }
     if (!certified) {
         redo[atomicAdd(redo_count, 1)] = make_int4(side, p, ii, 0);
@@ -1442,7 +1470,7 @@ size_t fl_layout(int n_img, int kmax, int dim, int n_pairs, size_t* off) {
     off[1] = o; o += gtsfm_align_up((size_t)n_img * kpad * sizeof(float), 256);             // norm2
     off[2] = o; o += gtsfm_align_up((size_t)2 * n_img * sizeof(unsigned), 256);             // maxnorm, unsafe
     off[3] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * kFlCand * sizeof(int), 256);  // cand
-    off[4] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * sizeof(float), 256);       // tkey
+    off[4] = o; o += gtsfm_align_up((size_t)2 * n_pairs * kmax * kFlCand * sizeof(float), 256);  // tkey
     off[5] = o; o += gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);       // rowres
     off[6] = o; o += gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);       // colres
     off[7] = o; o += 256;                                                                     // redo count
