@@ -630,24 +630,37 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
             if (gi < cap) cands[(size_t)shard * cap + gi] = Cand{b, layer, y, c};
         }
     };
+    // Branch-free per layer: "val > thr and val >= the 3x3x3 max" is val >= max(block max, thr_up) with thr_up the
+    // next float above thr (val > thr >= 0 also gives val > 0), and the same on the min side; the wave leaves the
+    // row at one exec test unless some lane has a flag (a few per thousand pixels).
+    const float thr_up = __uint_as_float(__float_as_uint(threshold) + 1u);  // threshold >= 0
     auto test_row = [&](int y, auto slot) {
         constexpr int s = decltype(slot)::value;
-        if (!col_ok || y < kBorder || y >= H - kBorder) return;
+        if (y < kBorder || y >= H - kBorder) return;
         float bmax[kIn], bmin[kIn];
 #pragma unroll
         for (int l = 0; l < kIn; ++l) {
             bmax[l] = fmaxf(fmaxf(hmax[l][0], hmax[l][1]), hmax[l][2]);
             bmin[l] = fminf(fminf(hmin[l][0], hmin[l][1]), hmin[l][2]);
         }
+        bool fmax_[kLayers], fmin_[kLayers];
+        bool any = false;
+#pragma unroll
+        for (int layer = 1; layer <= kLayers; ++layer) {
+            // DoG levels layer - 1 .. layer + 1; in registers: indices layer - 2 .. layer within [0, kIn)
+            float mx = fmaxf(bmax[layer - 1], thr_up), mn = fminf(bmin[layer - 1], -thr_up);
+            if (layer >= 2) { mx = fmaxf(mx, bmax[layer - 2]); mn = fminf(mn, bmin[layer - 2]); }
+            if (layer < kIn) { mx = fmaxf(mx, bmax[layer]); mn = fminf(mn, bmin[layer]); }
+            const float val = ctr[layer - 1][s];
+            fmax_[layer - 1] = val >= mx;
+            fmin_[layer - 1] = val <= mn;
+            any = any || fmax_[layer - 1] || fmin_[layer - 1];
+        }
+        if (!col_ok || !any) return;
 #pragma unroll
         for (int layer = 1; layer <= kLayers; ++layer) {
             const float val = ctr[layer - 1][s];
-            if (!(fabsf(val) > threshold)) continue;
-            // DoG levels layer - 1 .. layer + 1; in registers: indices layer - 2 .. layer within [0, kIn)
-            float mx = bmax[layer - 1], mn = bmin[layer - 1];
-            if (layer >= 2) { mx = fmaxf(mx, bmax[layer - 2]); mn = fminf(mn, bmin[layer - 2]); }
-            if (layer < kIn) { mx = fmaxf(mx, bmax[layer]); mn = fminf(mn, bmin[layer]); }
-            bool ismax = val > 0 && val >= mx, ismin = val < 0 && val <= mn;
+            bool ismax = fmax_[layer - 1], ismin = fmin_[layer - 1];
             if (!ismax && !ismin) continue;
             if (layer == 1 || layer == kLayers) {  // the outer DoG level (0 or kLayers + 1): queued
                 const int qi = atomicAdd(&n_pend, 1);
@@ -669,7 +682,9 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     using S2 = std::integral_constant<int, 2>;
     // rows y0-1 (slot 0) and y0 (slot 1) first; then row y0+1+3k+j goes to slot (2+j)%3 and completes the window of
     // row y0+3k+j, whose centre sits in slot (1+j)%3.
-    // The six rows of an iteration are fetched up front.
+    // Six rows' loads (24 per lane) stay in flight: a row's buffer is refilled with the row six below as soon as it
+    // has been consumed (rows past the strip's last needed row y_end re-read row y_end, an L2 hit).
+    const int y_end = min(y0 + kExStrip, H);
     {
         float ga[kInLv], gb[kInLv];
         fetch(y0 - 1, ga);
@@ -677,31 +692,36 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         finish(ga, S0{});
         finish(gb, S1{});
     }
-    const int y_end = min(y0 + kExStrip, H);
-    for (int y = y0; y < y_end; y += 6) {  // six rows' loads (24 per lane) in flight before the first is used
-        float g1[kInLv], g2[kInLv], g3[kInLv], g4[kInLv], g5[kInLv], g6[kInLv];
-        fetch(y + 1, g1);
-        fetch(y + 2, g2);
-        fetch(y + 3, g3);
-        fetch(y + 4, g4);
-        fetch(y + 5, g5);
-        fetch(y + 6, g6);
+    float g1[kInLv], g2[kInLv], g3[kInLv], g4[kInLv], g5[kInLv], g6[kInLv];
+    fetch(y0 + 1, g1);
+    fetch(y0 + 2, g2);
+    fetch(y0 + 3, g3);
+    fetch(y0 + 4, g4);
+    fetch(y0 + 5, g5);
+    fetch(y0 + 6, g6);
+    for (int y = y0; y < y_end; y += 6) {
         finish(g1, S2{});
+        fetch(min(y + 7, y_end), g1);
         test_row(y, S1{});
         if (y + 1 >= y_end) break;
         finish(g2, S0{});
+        fetch(min(y + 8, y_end), g2);
         test_row(y + 1, S2{});
         if (y + 2 >= y_end) break;
         finish(g3, S1{});
+        fetch(min(y + 9, y_end), g3);
         test_row(y + 2, S0{});
         if (y + 3 >= y_end) break;
         finish(g4, S2{});
+        fetch(min(y + 10, y_end), g4);
         test_row(y + 3, S1{});
         if (y + 4 >= y_end) break;
         finish(g5, S0{});
+        fetch(min(y + 11, y_end), g5);
         test_row(y + 4, S2{});
         if (y + 5 >= y_end) break;
         finish(g6, S1{});
+        fetch(min(y + 12, y_end), g6);
         test_row(y + 5, S0{});
     }
     __syncthreads();
