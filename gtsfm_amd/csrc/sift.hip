@@ -316,7 +316,10 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
     __syncthreads();
     // row pass: kBlurRowThr threads per row (consecutive lanes of one wave), kBlurRowOut consecutive outputs each,
     // written back in place at columns [g8, g8 + 8) (output column x sits at input column x + R)
-    for (int iy = tid / kBlurRowThr; iy < IH; iy += kBlurTX * kBlurTYT / kBlurRowThr) {
+#ifndef GTSFM_BLUR_DIAG  // diagnostic builds only: bit 0 = no row pass, bit 1 = no column taps
+#define GTSFM_BLUR_DIAG 0
+#endif
+    for (int iy = tid / kBlurRowThr; iy < ((GTSFM_BLUR_DIAG & 1) ? 0 : IH); iy += kBlurTX * kBlurTYT / kBlurRowThr) {
         const int g8 = (tid % kBlurRowThr) * kBlurRowOut;
         float* rowp = in + iy * IWP;
         // volatile 8-byte reads: the compiler would otherwise pair them into ds_read2_b64, which banks by 16-lane
@@ -363,7 +366,7 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
 #pragma unroll
     for (int h = 0; h < NP; ++h) acc[h] = pf2{k[0], k[0]} * pf2{c[R + 2 * h], c[R + 2 * h + 1]};
 #pragma unroll
-    for (int j = 1; j <= R; ++j) {
+    for (int j = 1; j <= ((GTSFM_BLUR_DIAG & 2) ? 0 : R); ++j) {
         pf2 sm[NP];
 #pragma unroll
         for (int h = 0; h < NP; ++h)
@@ -595,8 +598,15 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
 #pragma unroll
         for (int l = 0; l < kInLv; ++l) g[l] = gl[l + 1][off];
     };
+#ifdef GTSFM_EX_DIAG  // diagnostic builds only: 1 = sweep without the row test, 2 = loads only
+    float dsum = 0.f;
+#endif
     auto finish = [&](const float (&g)[kInLv], auto slot) {
         constexpr int s = decltype(slot)::value;
+#if defined(GTSFM_EX_DIAG) && GTSFM_EX_DIAG == 2
+        dsum += (g[0] + g[1]) + (g[2] + g[3]);
+        return;
+#endif
 #pragma unroll
         for (int l = 0; l < kIn; ++l) {
             const float d = g[l + 1] - g[l];
@@ -636,6 +646,12 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     const float thr_up = __uint_as_float(__float_as_uint(threshold) + 1u);  // threshold >= 0
     auto test_row = [&](int y, auto slot) {
         constexpr int s = decltype(slot)::value;
+#ifdef GTSFM_EX_DIAG
+#if GTSFM_EX_DIAG == 1
+        dsum += (hmax[0][s] + hmin[0][s]) + (hmax[1][s] + hmin[1][s]) + (hmax[2][s] + hmin[2][s]) + ctr[1][s];
+#endif
+        return;
+#endif
         if (y < kBorder || y >= H - kBorder) return;
         float bmax[kIn], bmin[kIn];
 #pragma unroll
@@ -724,6 +740,9 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         fetch(min(y + 12, y_end), g6);
         test_row(y + 5, S0{});
     }
+#ifdef GTSFM_EX_DIAG
+    if (dsum == -1.2345f) n_out[0] = 0;
+#endif
     __syncthreads();
     // the queued layer-1 / layer-3 pixels: outer DoG level's 3x3 block, every lane gathering at once
     for (int i = threadIdx.x; i < min(n_pend, kExPend); i += 64 * kExWaves) {
