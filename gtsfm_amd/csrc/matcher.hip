@@ -950,6 +950,10 @@ constexpr int kFlCand = 8;
 constexpr int kFlRows = 64;   // train rows per LDS chunk (two 32-row MFMA tiles)
 constexpr int kFlQ = 128;     // queries per workgroup: 4 waves x 32
 constexpr int kFlMaxDim = 256;
+#ifndef GTSFM_FL_DEPTH
+#define GTSFM_FL_DEPTH 2  // chunks of register prefetch in fl_shortlist_kernel (1 or 2; measured 535 / 524 ms)
+#endif
+
 
 __host__ __device__ inline int fl_dpad(int dim) { return dim <= 64 ? 64 : dim <= 128 ? 128 : 256; }
 __host__ __device__ inline int fl_kpad(int kmax) { return (kmax + kFlQ - 1) / kFlQ * kFlQ; }
@@ -1059,27 +1063,30 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     for (int c = 0; c < kFlCand; ++c) { v[c] = __builtin_inff(); id[c] = -1; }
     const _Float16* tbase = form + (size_t)it * kpad * DP;
     const float* nbase = norm2 + (size_t)it * kpad;
-    fl_u32x4 pre[NV];
-    float pn = 0.f;
     const int n_chunks = (nt + kFlRows - 1) / kFlRows;
-    if (n_chunks > 0) {
-        fl_fetch<NV, DP>(pre, pn, tbase, nbase, 0, tid);
-        fl_stash<NV, DP>(pre, pn, tl, nbl, 0, tid);
-    }
-    __syncthreads();
-    for (int c = 0; c < n_chunks; ++c) {
-        const int buf = c & 1, c0 = c * kFlRows;
-        if (c + 1 < n_chunks) {
-            fl_fetch<NV, DP>(pre, pn, tbase, nbase, c0 + kFlRows, tid);
-        }
+#ifndef GTSFM_FL_DIAG  // diagnostic builds only: 1 = no top-8 epilogue, 2 = no MFMA either (outputs are placeholders)
+#define GTSFM_FL_DIAG 0
+#endif
+    float dsum = 0.f;
+    // one chunk: two 32-row MFMA tiles against the wave's 32 queries, then the top-8 epilogue per tile
+    auto process = [&](int c, int buf) {
+        const int c0 = c * kFlRows;
         const _Float16* tb = tl + buf * kFlRows * RS;
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             fl_float16 acc = {};
             const _Float16* arow = tb + (t * 32 + (l & 31)) * RS + 8 * h;
+            if (GTSFM_FL_DIAG == 2) {
+                dsum += (float)arow[0] + (float)arow[16 * (NS - 1)];
+                continue;
+            }
 #pragma unroll
             for (int s = 0; s < NS; ++s)
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const fl_half8*)(arow + 16 * s), bq[s], acc, 0, 0, 0);
+            if (GTSFM_FL_DIAG == 1) {
+                dsum += acc[0] + acc[15];
+                continue;
+            }
             // the tile's 16 keys of this lane, a mask of those below the shortlist's current last key, then one
             // insert per wave iteration for every lane that still has a set bit, in index order: the same insertion
             // sequence as testing the keys one by one, but the wave runs max(popcount) inserts instead of one per
@@ -1108,10 +1115,47 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
                 }
             }
         }
-        if (c + 1 < n_chunks) {
-            fl_stash<NV, DP>(pre, pn, tl, nbl, buf ^ 1, tid);
-        }
+    };
+#if GTSFM_FL_DEPTH == 2
+    // register prefetch two chunks ahead (chunk c + 2 is loaded while chunk c is computed, chunk c + 1 waits in the
+    // other register set and is stashed at the end of chunk c): each load has two chunks of work to land
+    fl_u32x4 preA[NV], preB[NV];
+    float pnA = 0.f, pnB = 0.f;
+    if (n_chunks > 0) {
+        fl_fetch<NV, DP>(preA, pnA, tbase, nbase, 0, tid);
+        fl_stash<NV, DP>(preA, pnA, tl, nbl, 0, tid);
+    }
+    if (n_chunks > 1) fl_fetch<NV, DP>(preB, pnB, tbase, nbase, kFlRows, tid);
+    __syncthreads();
+    for (int c = 0; c < n_chunks; c += 2) {
+        if (c + 2 < n_chunks) fl_fetch<NV, DP>(preA, pnA, tbase, nbase, (c + 2) * kFlRows, tid);
+        process(c, 0);
+        if (c + 1 < n_chunks) fl_stash<NV, DP>(preB, pnB, tl, nbl, 1, tid);
         __syncthreads();
+        if (c + 1 >= n_chunks) break;
+        if (c + 3 < n_chunks) fl_fetch<NV, DP>(preB, pnB, tbase, nbase, (c + 3) * kFlRows, tid);
+        process(c + 1, 1);
+        if (c + 2 < n_chunks) fl_stash<NV, DP>(preA, pnA, tl, nbl, 0, tid);
+        __syncthreads();
+    }
+#else
+    fl_u32x4 pre[NV];
+    float pn = 0.f;
+    if (n_chunks > 0) {
+        fl_fetch<NV, DP>(pre, pn, tbase, nbase, 0, tid);
+        fl_stash<NV, DP>(pre, pn, tl, nbl, 0, tid);
+    }
+    __syncthreads();
+    for (int c = 0; c < n_chunks; ++c) {
+        if (c + 1 < n_chunks) fl_fetch<NV, DP>(pre, pn, tbase, nbase, (c + 1) * kFlRows, tid);
+        process(c, c & 1);
+        if (c + 1 < n_chunks) fl_stash<NV, DP>(pre, pn, tl, nbl, (c & 1) ^ 1, tid);
+        __syncthreads();
+    }
+#endif
+    if (GTSFM_FL_DIAG != 0) {  // placeholders that certify: candidates 0..7 with an unreachable last key
+#pragma unroll
+        for (int c = 0; c < kFlCand; ++c) { v[c] = dsum == -1.2345f ? 0.f : 1e30f; id[c] = c; }
     }
     // merge the two halves of each query's shortlist
 #pragma unroll
