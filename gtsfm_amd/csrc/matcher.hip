@@ -1104,15 +1104,16 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
 #pragma unroll
                 for (int e = 0; e < 4; ++e) mask |= (kk[4 * g + e] < thr ? 1u : 0u) << (4 * g + e);
             }
+            // branch-free body: a lane without a pending key (or whose key no longer beats the last slot) inserts
+            // +inf, which leaves the sorted list and its ids unchanged
             while (__ballot(mask != 0u) != 0ull) {
-                if (mask != 0u) {
-                    const int i = __builtin_ctz(mask);
-                    mask &= mask - 1u;
-                    float x = kk[0];
+                const int i = __builtin_ctz(mask | 0x10000u);  // 16: nothing pending
+                mask &= mask - 1u;
+                float x = __builtin_inff();
 #pragma unroll
-                    for (int q = 1; q < 16; ++q) x = i == q ? kk[q] : x;
-                    if (x < v[kFlCand - 1]) fl_insert(x, c0 + t * 32 + 8 * (i >> 2) + 4 * h + (i & 3), v, id);
-                }
+                for (int q = 0; q < 16; ++q) x = i == q ? kk[q] : x;
+                x = x < v[kFlCand - 1] ? x : __builtin_inff();
+                fl_insert(x, c0 + t * 32 + 8 * (i >> 2) + 4 * h + (i & 3), v, id);
             }
         }
     };
