@@ -950,6 +950,9 @@ constexpr int kFlCand = 8;
 constexpr int kFlRows = 64;   // train rows per LDS chunk (two 32-row MFMA tiles)
 constexpr int kFlQ = 128;     // queries per workgroup: 4 waves x 32
 constexpr int kFlMaxDim = 256;
+#ifndef GTSFM_FL_XCD
+#define GTSFM_FL_XCD 1    // fl_shortlist_kernel's XCD-contiguous block order
+#endif
 #ifndef GTSFM_FL_DEPTH
 #define GTSFM_FL_DEPTH 2  // chunks of register prefetch in fl_shortlist_kernel (1 or 2; measured 535 / 524 ms)
 #endif
@@ -1047,10 +1050,21 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     extern __shared__ __attribute__((aligned(16))) unsigned char fl_smem[];
     _Float16* tl = (_Float16*)fl_smem;                                  // [2][kFlRows * RS]
     float* nbl = (float*)(fl_smem + 2 * kFlRows * RS * sizeof(_Float16));  // [2][kFlRows]
-    const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 5;
+#if GTSFM_FL_XCD
+    // 1-D grid, XCD-contiguous: the hardware deals consecutive workgroups to the 8 XCDs in turn, so workgroup b runs
+    // logical block (b & 7) * per_xcd + (b >> 3); each XCD then walks whole (pair, side) groups of query blocks in
+    // order and the group's train image is read into that XCD's L2 once, not by every XCD
+    const int n_qb = kpad / kFlQ, total = n_qb * n_pairs * 2, per_xcd = (total + 7) / 8;
+    const int lb = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+    if (lb >= total) return;
+    const int qb = lb % n_qb, p = (lb / n_qb) % n_pairs, side = lb / (n_qb * n_pairs);
+#else
+    const int qb = blockIdx.x, p = blockIdx.y, side = blockIdx.z;
+#endif
+    const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 5;
     const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
     const int nq = counts[iq], nt = counts[it];
-    const int q0 = blockIdx.x * kFlQ;
+    const int q0 = qb * kFlQ;
     if (q0 >= nq) return;
     const int qn = q0 + w * 32 + (l & 31);
     fl_half8 bq[NS];
@@ -1529,7 +1543,12 @@ int launch_fl_shortlist(const _Float16* form, const float* norm2, const int* cou
                         int kpad, int kmax, int* cand, float* tkey, hipStream_t stream) {
     const size_t lds = 2 * kFlRows * (NS * 16 + 8) * sizeof(_Float16) + 2 * kFlRows * sizeof(float);
     GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)fl_shortlist_kernel<NS>, (int)lds));
-    hipLaunchKernelGGL(fl_shortlist_kernel<NS>, dim3(kpad / kFlQ, n_pairs, 2), dim3(256), lds, stream, form, norm2,
+#if GTSFM_FL_XCD
+    const dim3 grid((unsigned)((kpad / kFlQ * (size_t)n_pairs * 2 + 7) / 8 * 8));
+#else
+    const dim3 grid(kpad / kFlQ, n_pairs, 2);
+#endif
+    hipLaunchKernelGGL(fl_shortlist_kernel<NS>, grid, dim3(256), lds, stream, form, norm2,
                        counts, pairs, n_pairs, kpad, kmax, cand, tkey);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
