@@ -1,6 +1,6 @@
 // Micro-benchmark: the extrema sweep's read pattern (four fp32 planes, each wave walking a strip of rows down its
 // columns) with 4-byte loads (64 columns per wave) against 8- and 16-byte loads (128 / 256 columns per wave).
-// Reports GB/s of plane bytes read. Build: hipcc -O3 --offload-arch=gfx950 tools/ubench_rowwalk.hip -o /tmp/rowwalk
+// Reports GB/s of plane bytes read. Build: hipcc -O3 --offload-arch=gfx950 tools/ubench/rowwalk.hip -o /tmp/rowwalk
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
