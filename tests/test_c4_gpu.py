@@ -10,8 +10,8 @@ and on 48 sampled pairs (24 that pass the inlier-support filter, 24 seeded-rando
 own SIFT features (bit-exact vs the oracle elsewhere: tests/test_sift_gpu.py):
 - putatives: the oracle TwoWayMatcher's count equals the chunked launch's, and the verified rows are an in-order
   subsequence of the oracle's putatives (bit-exact indices);
-- verifier: the oracle's RANSAC on those putatives with the pair's global sampler key -> same status, inlier count
-  within 1 %, R / t within 0.05 deg (tests/test_verifier_gpu.py's bar), >= 99 % of the verified rows shared.
+- verifier: the oracle's RANSAC on those putatives with the pair's global sampler key -> same status, the same inlier
+  count, R / t within 2e-3 deg (tests/test_verifier_gpu.py's bar), >= 99 % of the verified rows shared.
 """
 from concurrent.futures import ThreadPoolExecutor
 
@@ -100,9 +100,9 @@ def test_c4_one_gpu_all_pairs_consistent_and_sampled_vs_oracle(oracle_mod):
             continue
         assert st[p] == 0, (p, st[p])
         _, rmask, rR, rt, rn, _ = ref
-        assert abs(int(n_inl[p]) - rn) <= max(1, 0.01 * rn), (p, n_inl[p], rn)
-        assert scenes.rotation_angle_deg(res.R[p], rR) < 0.05, p
-        assert scenes.direction_angle_deg(res.t[p], rt) < 0.05, p
+        assert int(n_inl[p]) == rn, (p, n_inl[p], rn)
+        assert scenes.rotation_angle_deg(res.R[p], rR) < 2e-3, p
+        assert scenes.direction_angle_deg(res.t[p], rt) < 2e-3, p
         o_rows = {(int(a), int(b)) for a, b in c["m"][rmask.astype(bool)]}
         shared = sum((int(a), int(b)) in o_rows for a, b in res.verified(p))
         assert shared >= 0.99 * max(len(o_rows), len(res.verified(p))) - 1, (p, shared, len(o_rows))

@@ -2,9 +2,9 @@
 
 Known answers (reference tests, committed as data): two-plane scene (all 8 verified, R/t < 2 deg), Argoverse
 hand-labelled pair (Euler +-1 deg, t +-0.01), the M<6 failure path, empty matches.
-Oracle parity: same sampling, same solver, same fp32 inlier test, same LO => per pair the inlier counts agree within
-1% and the poses within 0.05 deg (fp64 reductions are summed in a different order on the GPU, so bit-identity is not
-claimed for the LO refits).
+Oracle parity: same sampling, same solver, same fp32 inlier test, same LO => per pair the same number of hypotheses,
+the same inlier count and the poses within 2e-3 deg (fp64 reductions are summed in a different order on the GPU, so
+bit-identity is not claimed for the LO refits' poses; measured max 1e-5 deg).
 """
 import json
 import os
@@ -125,11 +125,11 @@ def test_batched_parity_with_oracle(dev, oracle_mod):
         _, rmask, rR, rt, rn, rh = ref
         # hypotheses evaluated: chunks of 64 with the bound re-evaluated per chunk, whatever chunks a launch covers
         assert int(n_hyp[p]) == rh, (p, n_hyp[p], rh)
-        assert abs(int(n_inl[p]) - rn) <= max(1, 0.01 * rn), (p, n_inl[p], rn)
+        assert int(n_inl[p]) == rn, (p, n_inl[p], rn)
         agree = (mask[p, : Ms[p]] == rmask).mean()
         assert agree >= 0.99, (p, agree)
-        assert scenes.rotation_angle_deg(R_all[p], rR) < 0.05, p
-        assert scenes.direction_angle_deg(t_all[p], rt) < 0.05, p
+        assert scenes.rotation_angle_deg(R_all[p], rR) < 2e-3, p
+        assert scenes.direction_angle_deg(t_all[p], rt) < 2e-3, p
         if rn >= 50:  # estimator accuracy vs ground truth (only meaningful with enough support)
             assert scenes.rotation_angle_deg(R_all[p], gts[p][0]) < 2.0, p
 
