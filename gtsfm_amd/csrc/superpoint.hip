@@ -127,24 +127,55 @@ __global__ __launch_bounds__(kConvThreads) void conv_mfma_kernel(ConvArgs a) {
     const int ncol = (lane & 31) + 32 * wn;
     const float* inb = a.in + (size_t)img * a.Hi * a.Wi * a.in_cstride + a.in_c0;
     f32x16 acc = {};
-    for (int c0 = 0; c0 < a.Cin; c0 += kCinChunk) {
-        for (int e = tid; e < PH * PW * 4; e += kConvThreads) {
+    // the next Cin chunk's patch and weights are loaded into registers while the current chunk's MFMAs run, then
+    // stored to LDS between the two barriers (the MFMA order, and so every sum, is unchanged)
+    constexpr int kNP = (PH * PW * 4 + kConvThreads - 1) / kConvThreads;
+    constexpr int kNW = (KS * KS * kCinChunk * 16 + kConvThreads - 1) / kConvThreads;
+    f32x4_t pv[kNP], wv[kNW];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int u = 0; u < kNP; ++u) {
+            const int e = tid + u * kConvThreads;
             const int pix = e >> 2, q = e & 3;
             const int py = pix / PW, px = pix - py * PW;
             const int gy = y0 - R + py, gx = x0 - R + px;
-            f32x4_t v = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi)
-                v = *(const f32x4_t*)(inb + ((size_t)gy * a.Wi + gx) * a.in_cstride + c0 + 4 * q);
-            float* d = patch + pix * kChanStride + 4 * q;
-            d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+            pv[u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            if (e < PH * PW * 4 && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi)
+                pv[u] = *(const f32x4_t*)(inb + ((size_t)gy * a.Wi + gx) * a.in_cstride + c0 + 4 * q);
         }
-        for (int e = tid; e < KS * KS * kCinChunk * 16; e += kConvThreads) {
+#pragma unroll
+        for (int u = 0; u < kNW; ++u) {
+            const int e = tid + u * kConvThreads;
             const int kk = e / (kCinChunk * 16), rem = e - kk * kCinChunk * 16;
             const int ci = rem >> 4, q4 = rem & 15;
-            *(f32x4_t*)(wt + (kk * kCinChunk + ci) * 64 + 4 * q4) =
-                *(const f32x4_t*)(a.w + ((size_t)kk * a.Cin + c0 + ci) * a.cout_pad + 64 * ct + 4 * q4);
+            if (e < KS * KS * kCinChunk * 16)
+                wv[u] = *(const f32x4_t*)(a.w + ((size_t)kk * a.Cin + c0 + ci) * a.cout_pad + 64 * ct + 4 * q4);
         }
-        __syncthreads();
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int u = 0; u < kNP; ++u) {
+            const int e = tid + u * kConvThreads;
+            if (e < PH * PW * 4) {
+                float* d = patch + (e >> 2) * kChanStride + 4 * (e & 3);
+                d[0] = pv[u][0]; d[1] = pv[u][1]; d[2] = pv[u][2]; d[3] = pv[u][3];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kNW; ++u) {
+            const int e = tid + u * kConvThreads;
+            if (e < KS * KS * kCinChunk * 16) {
+                const int kk = e / (kCinChunk * 16), rem = e - kk * kCinChunk * 16;
+                *(f32x4_t*)(wt + (kk * kCinChunk + (rem >> 4)) * 64 + 4 * (rem & 15)) = wv[u];
+            }
+        }
+    };
+    load(0);
+    stash();
+    __syncthreads();
+    for (int c0 = 0; c0 < a.Cin; c0 += kCinChunk) {
+        const bool more = c0 + kCinChunk < a.Cin;
+        if (more) load(c0 + kCinChunk);
 #pragma unroll
         for (int ky = 0; ky < KS; ++ky)
 #pragma unroll
@@ -155,6 +186,9 @@ __global__ __launch_bounds__(kConvThreads) void conv_mfma_kernel(ConvArgs a) {
                 for (int s = 0; s < 8; ++s)
                     acc = __builtin_amdgcn_mfma_f32_32x32x2f32(pa[s], pb[s * 64], acc, 0, 0, 0);
             }
+        if (!more) break;
+        __syncthreads();
+        stash();
         __syncthreads();
     }
     // epilogue: acc[g] = conv output at tile pixel 4 kh + (g & 3) + 8 (g >> 2), output channel ncol
