@@ -314,15 +314,23 @@ __device__ __forceinline__ int block_excl_scan(int v, int* sh, int& total) {
     return off + x - v;
 }
 
+// Image masks (gtsfm/frontend/detector_descriptor/superpoint.py:68-70, Keypoints.filter_by_mask): a detection at
+// integer pixel (x, y) survives iff mask[y][x] == 1 (the reference compares with == 1, so other nonzero values drop
+// it); masks[n][mH][mW] u8 over the full image (the detection grid, 8 * floor(H / 8) x 8 * floor(W / 8), lies inside).
+__device__ __forceinline__ bool mask_ok(const uint8_t* __restrict__ masks, int img, int mH, int mW, int y, int x) {
+    return masks == nullptr || masks[((size_t)img * mH + y) * mW + x] == 1;
+}
+
 __global__ __launch_bounds__(kRowThreads) void row_count_kernel(const float* __restrict__ N, int H, int W, float thr,
-                                                                 int border, int* __restrict__ rowcnt) {
+                                                                 int border, const uint8_t* __restrict__ masks, int mH,
+                                                                 int mW, int* __restrict__ rowcnt) {
     __shared__ int sh[4];
     const int img = blockIdx.y, y = blockIdx.x;
     const float* row = N + ((size_t)img * H + y) * W;
     int c = 0;
     const bool yok = y >= border && y < H - border;
     for (int x = threadIdx.x; x < W; x += kRowThreads)
-        c += (yok && x >= border && x < W - border && row[x] > thr) ? 1 : 0;
+        c += (yok && x >= border && x < W - border && row[x] > thr && mask_ok(masks, img, mH, mW, y, x)) ? 1 : 0;
     int total;
     block_excl_scan(c, sh, total);
     if (threadIdx.x == 0) rowcnt[(size_t)img * H + y] = total;
@@ -346,7 +354,8 @@ __global__ __launch_bounds__(kRowThreads) void row_scan_kernel(const int* __rest
 
 // candidates: per image, (y * W + x) raster index and score
 __global__ __launch_bounds__(kRowThreads) void row_emit_kernel(const float* __restrict__ N, int H, int W, float thr,
-                                                                int border, const int* __restrict__ rowoff, int cap,
+                                                                int border, const uint8_t* __restrict__ masks, int mH,
+                                                                int mW, const int* __restrict__ rowoff, int cap,
                                                                 int* __restrict__ cand_idx,
                                                                 float* __restrict__ cand_score) {
     __shared__ int sh[4];
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(kRowThreads) void row_emit_kernel(const float* __re
     for (int base = 0; base < W; base += kRowThreads) {
         const int x = base + threadIdx.x;
         const float s = x < W ? row[x] : 0.0f;
-        const int f = (x < W && x >= border && x < W - border && s > thr) ? 1 : 0;
+        const int f = (x < W && x >= border && x < W - border && s > thr && mask_ok(masks, img, mH, mW, y, x)) ? 1 : 0;
         int total;
         const int ex = block_excl_scan(f, sh, total);
         if (f && off + ex < cap) {
@@ -573,10 +582,10 @@ size_t gtsfm_superpoint_workspace_bytes(int n, int H, int W, int max_kpts) {
     return sp_layout(n, sp_dims(H, W)).total;
 }
 
-int gtsfm_superpoint_batched(const uint8_t* d_images, int n, int H, int W, int C, const float* d_weights,
-                             int max_kpts, float keypoint_threshold, int nms_radius, int remove_borders,
-                             void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_scores, float* d_desc,
-                             int* d_count, int* d_n_detected, void* stream_v) {
+int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, int n, int H, int W, int C,
+                             const float* d_weights, int max_kpts, float keypoint_threshold, int nms_radius,
+                             int remove_borders, void* d_workspace, size_t workspace_bytes, float* d_xy,
+                             float* d_scores, float* d_desc, int* d_count, int* d_n_detected, void* stream_v) {
     hipStream_t stream = (hipStream_t)stream_v;
     if (n == 0) return GTSFM_OK;
     if (!d_images || !d_weights || !d_workspace || !d_xy || !d_scores || !d_desc || !d_count || n < 0 || H <= 0 ||
@@ -663,10 +672,10 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, int n, int H, int W, int C
     int* cidx = (int*)(ws + L.cand_idx);
     float* cscore = (float*)(ws + L.cand_score);
     hipLaunchKernelGGL(row_count_kernel, dim3(d.Hs, n), dim3(kRowThreads), 0, stream, T, d.Hs, d.Ws,
-                       keypoint_threshold, remove_borders, rowcnt);
+                       keypoint_threshold, remove_borders, d_masks, H, W, rowcnt);
     hipLaunchKernelGGL(row_scan_kernel, dim3(n), dim3(kRowThreads), 0, stream, rowcnt, d.Hs, rowoff, ndet);
     hipLaunchKernelGGL(row_emit_kernel, dim3(d.Hs, n), dim3(kRowThreads), 0, stream, T, d.Hs, d.Ws,
-                       keypoint_threshold, remove_borders, rowoff, L.cap, cidx, cscore);
+                       keypoint_threshold, remove_borders, d_masks, H, W, rowoff, L.cap, cidx, cscore);
     hipLaunchKernelGGL(topk_select_kernel, dim3(n), dim3(kTopThreads), 0, stream, cidx, cscore, L.cap, ndet, max_kpts,
                        d.Ws, d_xy, d_scores, d_count);
     hipLaunchKernelGGL(desc_sample_kernel, dim3(max_kpts, n), dim3(64), 0, stream, buf1, d.H8, d.W8, d_xy, d_count,

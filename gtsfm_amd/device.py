@@ -333,12 +333,15 @@ class SuperPointResult:
 def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: int, keypoint_threshold: float = 0.005,
                        nms_radius: int = 4, remove_borders: int = 4,
                        stream: Optional[torch.cuda.Stream] = None, out: Optional[SuperPointResult] = None,
-                       workspace: Optional[torch.Tensor] = None) -> SuperPointResult:
+                       workspace: Optional[torch.Tensor] = None, masks: Optional[torch.Tensor] = None
+                       ) -> SuperPointResult:
     """SuperPoint on a batch of same-sized uint8 images (n, H, W) gray or (n, H, W, 3) RGB (gtsfm_superpoint_batched).
 
     weights: the packed fp32 blob (gtsfm_amd.frontend.detector_descriptor.superpoint.pack_superpoint_weights).
     out: optional preallocated outputs (xy (n,k,2), scores (n,k), desc (n,k,256), count, n_detected; rows past a
     count are unspecified); workspace: optional device buffer of at least gtsfm_superpoint_workspace_bytes.
+    masks: optional (n, H, W) uint8 device tensor; a detection at (x, y) is kept iff masks[i, y, x] == 1 (the
+    reference's Keypoints.filter_by_mask), before the top-k.
     """
     assert images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous()
     assert weights.is_cuda and weights.dtype == torch.float32 and weights.is_contiguous()
@@ -361,7 +364,11 @@ def superpoint_extract(images: torch.Tensor, weights: torch.Tensor, max_kpts: in
     ws = workspace if workspace is not None and workspace.numel() >= need else _workspace(need, dev)
     if stream is not None:
         ws.record_stream(stream)
-    rc = L.gtsfm_superpoint_batched(_ptr(images), n, H, W, C, _ptr(weights), max_kpts, float(keypoint_threshold),
+    if masks is not None:
+        assert masks.is_cuda and masks.dtype == torch.uint8 and masks.is_contiguous()
+        assert tuple(masks.shape) == (n, H, W), (tuple(masks.shape), (n, H, W))
+    rc = L.gtsfm_superpoint_batched(_ptr(images), _ptr(masks) if masks is not None else None, n, H, W, C,
+                                    _ptr(weights), max_kpts, float(keypoint_threshold),
                                     int(nms_radius), int(remove_borders), _ptr(ws), ws.numel(), _ptr(out.xy),
                                     _ptr(out.scores), _ptr(out.desc), _ptr(out.count), _ptr(out.n_detected),
                                     native.stream_handle(stream))

@@ -95,7 +95,8 @@ SP_GROUP_BYTES = 16 << 30  # SuperPoint workspace per launch (~0.75 GB per 1080p
 
 def extract_superpoint_batched(detector: SuperPointDetectorDescriptor, images: Sequence[Image]) -> DeviceFeatures:
     """gtsfm_superpoint_batched per image size in workspace-bounded groups; features gathered into one padded block
-    (scores kept for SuperGlue). Masks are not supported on the device path (the per-call plugin raises too)."""
+    (scores kept for SuperGlue). Image masks filter the detections on the device before the top-k, as the per-call
+    plugin (reference superpoint.py:68-72)."""
     native.require_gpu()
     n, k = len(images), detector.max_keypoints
     dev = torch.device("cuda")
@@ -105,8 +106,6 @@ def extract_superpoint_batched(detector: SuperPointDetectorDescriptor, images: S
     count = torch.zeros((n,), dtype=torch.int32, device=dev)
     by_shape: Dict[tuple, List[int]] = {}
     for i, im in enumerate(images):
-        if im.mask is not None:
-            raise NotImplementedError("image masks are not supported on the MI355X SuperPoint path yet")
         by_shape.setdefault(tuple(im.value_array.shape), []).append(i)
     L = native.lib()
     for shape, idx in by_shape.items():
@@ -114,7 +113,7 @@ def extract_superpoint_batched(detector: SuperPointDetectorDescriptor, images: S
         g = max(1, SP_GROUP_BYTES // per)
         for s0 in range(0, len(idx), g):
             part = idx[s0: s0 + g]
-            res = detector.extract_batch([images[i].value_array for i in part], k)
+            res = detector.extract_batch([images[i].value_array for i in part], k, masks=[images[i].mask for i in part])
             sel = torch.tensor(part, dtype=torch.long, device=dev)
             xy[sel], sc[sel], desc[sel], count[sel] = res.xy, res.scores, res.desc, res.count
     cnt = count.cpu().numpy()

@@ -77,13 +77,27 @@ class SuperPointDetectorDescriptor(DetectorDescriptorBase):
             self._blob = torch.from_numpy(pack_superpoint_weights(sd)).to(torch.device("cuda"))
         return self._blob
 
-    def extract_batch(self, arrays: List[np.ndarray], max_kpts: Optional[int] = None) -> device.SuperPointResult:
+    def extract_batch(self, arrays: List[np.ndarray], max_kpts: Optional[int] = None,
+                      masks: Optional[List[Optional[np.ndarray]]] = None) -> device.SuperPointResult:
+        """Same-sized images; masks: per image an (H, W) array (keypoints kept where it equals 1, as the reference's
+        Keypoints.filter_by_mask before get_top_k) or None (all kept)."""
         x = np.ascontiguousarray(np.stack(arrays), dtype=np.uint8)
         if x.ndim == 4 and x.shape[3] == 4:
             x = np.ascontiguousarray(x[..., :3])
-        t = torch.from_numpy(x).to(torch.device("cuda"))
+        dev = torch.device("cuda")
+        t = torch.from_numpy(x).to(dev)
+        m = None
+        if masks is not None and any(mk is not None for mk in masks):
+            H, W = x.shape[1], x.shape[2]
+            mm = np.ones((len(arrays), H, W), np.uint8)
+            for i, mk in enumerate(masks):
+                if mk is not None:
+                    mk = np.asarray(mk)
+                    assert mk.shape[:2] == (H, W), (mk.shape, (H, W))
+                    mm[i] = mk.reshape(H, W) == 1  # filter_by_mask's test, as 0 / 1 bytes
+            m = torch.from_numpy(mm).to(dev)
         return device.superpoint_extract(t, self.weights(), max_kpts or self.max_keypoints, self._thr, self._nms,
-                                         self._border)
+                                         self._border, masks=m)
 
     @staticmethod
     def _unpack(res: device.SuperPointResult, i: int) -> Tuple[Keypoints, np.ndarray]:
@@ -94,21 +108,19 @@ class SuperPointDetectorDescriptor(DetectorDescriptorBase):
         return Keypoints(coordinates=xy, scales=None, responses=scores), desc
 
     def detect_and_describe(self, image: Image) -> Tuple[Keypoints, np.ndarray]:
+        """Reference superpoint.py:48-74: network, then filter_by_mask(image.mask) when given, then
+        get_top_k(max_keypoints), all on the device."""
         native.require_gpu()
-        if image.mask is not None:
-            raise NotImplementedError("image masks are not supported on the MI355X SuperPoint path yet")
-        return self._unpack(self.extract_batch([image.value_array]), 0)
+        return self._unpack(self.extract_batch([image.value_array], masks=[image.mask]), 0)
 
     def detect_and_describe_batch(self, images: List[Image]) -> List[Tuple[Keypoints, np.ndarray]]:
         native.require_gpu()
         out: List[Tuple[Keypoints, np.ndarray]] = [None] * len(images)  # type: ignore
         by_shape: Dict[tuple, List[int]] = {}
         for i, im in enumerate(images):
-            if im.mask is not None:
-                raise NotImplementedError("image masks are not supported on the MI355X SuperPoint path yet")
             by_shape.setdefault(im.value_array.shape, []).append(i)
         for _, idx in by_shape.items():
-            res = self.extract_batch([images[i].value_array for i in idx])
+            res = self.extract_batch([images[i].value_array for i in idx], masks=[images[i].mask for i in idx])
             for j, i in enumerate(idx):
                 out[i] = self._unpack(res, j)
         return out

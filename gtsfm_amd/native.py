@@ -83,8 +83,8 @@ SIGNATURES = {
     "gtsfm_superpoint_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "gtsfm_superpoint_batched": (
         c_int,
-        [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_size_t, c_void_p,
-         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+        [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_float, c_int, c_int, c_void_p, c_size_t,
+         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     ),
     "gtsfm_superglue_weights_floats": (c_size_t, [c_int]),
     "gtsfm_superglue_workspace_bytes": (c_size_t, [c_int, c_int]),

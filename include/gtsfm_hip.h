@@ -239,18 +239,20 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
  * (k, cin, cout_pad) = (3,1,64) (3,64,64) (3,64,64) (3,64,64) (3,64,128) (3,128,128) (3,128,128) (3,128,128)
  * (3,128,512: Pa in 0..255, Da in 256..511) (1,256,128: 65 used) (1,256,256); padded outputs are zero.
  * Detection: softmax over 65, 8x8 depth-to-space, simple_nms(nms_radius), score > keypoint_threshold, border
- * remove_borders; the max_kpts highest scores are kept (ties by raster order) and emitted in raster order
- * (the reference's own order when max_kpts >= detections). Outputs: d_xy[n][max_kpts][2] (x, y) float,
- * d_scores[n][max_kpts], d_desc[n][max_kpts][256] unit-norm, d_count[n], d_n_detected[n] (may be NULL).
+ * remove_borders; d_masks[n][H][W] u8 or NULL: as Keypoints.filter_by_mask (reference superpoint.py:68-70), a
+ * detection at pixel (x, y) is kept iff mask[y][x] == 1, before the top-k; the max_kpts highest scores are kept
+ * (ties by raster order) and emitted in raster order (the reference's own order when max_kpts >= detections).
+ * Outputs: d_xy[n][max_kpts][2] (x, y) float, d_scores[n][max_kpts], d_desc[n][max_kpts][256] unit-norm,
+ * d_count[n], d_n_detected[n] (detections after border and mask, before the top-k; may be NULL).
  * ---------------------------------------------------------------------------------------------- */
 size_t gtsfm_superpoint_weights_floats(void);
 
 size_t gtsfm_superpoint_workspace_bytes(int n, int H, int W, int max_kpts);
 
-int gtsfm_superpoint_batched(const uint8_t* d_images, int n, int H, int W, int C, const float* d_weights,
-                             int max_kpts, float keypoint_threshold, int nms_radius, int remove_borders,
-                             void* d_workspace, size_t workspace_bytes, float* d_xy, float* d_scores, float* d_desc,
-                             int* d_count, int* d_n_detected, void* stream);
+int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, int n, int H, int W, int C,
+                             const float* d_weights, int max_kpts, float keypoint_threshold, int nms_radius,
+                             int remove_borders, void* d_workspace, size_t workspace_bytes, float* d_xy,
+                             float* d_scores, float* d_desc, int* d_count, int* d_n_detected, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
  * SuperGlue matcher. Replaces SuperGlueMatcher.match (gtsfm/frontend/matcher/superglue_matcher.py:43-111) and

@@ -17,7 +17,7 @@ superglue_random_w0.npz, written in this container by tests/golden/make_*_golden
 """
 from __future__ import annotations
 
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -60,9 +60,12 @@ def simple_nms(scores: torch.Tensor, r: int) -> torch.Tensor:
 
 
 def superpoint(gray: np.ndarray, sd: Dict[str, np.ndarray], max_keypoints: int = -1, keypoint_threshold: float = 0.005,
-               nms_radius: int = 4, border: int = 4) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+               nms_radius: int = 4, border: int = 4, mask: Optional[np.ndarray] = None
+               ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """keypoints (N, 2) float32 (x, y), scores (N,), descriptors (N, 256) of one uint8 gray image. Raster order
-    (torch.nonzero's) when max_keypoints < 0, else the max_keypoints highest scores (ties: raster order)."""
+    (torch.nonzero's) when max_keypoints < 0, else the max_keypoints highest scores (ties: raster order).
+    mask: (H, W) or None; as gtsfm's SuperPointDetectorDescriptor (superpoint.py:68-72), a keypoint is kept iff
+    mask[round(y), round(x)] == 1 (Keypoints.filter_by_mask, keypoints.py:112-127), before the top-k."""
     with torch.no_grad():
         x = superpoint_encoder(gray, sd)
         semi = _conv(_conv(x, sd, "convPa"), sd, "convPb", relu=False)
@@ -75,6 +78,9 @@ def superpoint(gray: np.ndarray, sd: Dict[str, np.ndarray], max_keypoints: int =
         H, W = h * 8, w * 8
         keep = (kp[:, 0] >= border) & (kp[:, 0] < H - border) & (kp[:, 1] >= border) & (kp[:, 1] < W - border)
         kp, s = kp[keep], s[keep]
+        if mask is not None:
+            mk = torch.from_numpy(np.asarray(mask)[kp[:, 0].numpy(), kp[:, 1].numpy()] == 1)
+            kp, s = kp[mk], s[mk]
         if 0 <= max_keypoints < len(kp):
             order = np.argsort(-s.numpy(), kind="stable")[:max_keypoints]
             order = torch.from_numpy(np.sort(order))

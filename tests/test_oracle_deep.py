@@ -28,6 +28,27 @@ def test_superpoint_restatement_matches_reference(sp_golden, case):
     np.testing.assert_allclose(desc[rows], g[f"{case}__desc"], atol=2e-6)
 
 
+def test_superpoint_mask_follows_reference_filter(sp_golden):
+    """The oracle's mask = the reference module's keypoints (golden) through gtsfm's Keypoints.filter_by_mask
+    (keypoints.py:124-125: mask[round(y), round(x)] == 1) and then get_top_k's highest-score set (superpoint.py:68-72)."""
+    from oracle import deep
+
+    g = sp_golden
+    img = g["lund_480x640__image"]
+    rng = np.random.default_rng(5)
+    mask = (rng.random(img.shape) < 0.7).astype(np.uint8)
+    mask[rng.random(img.shape) < 0.1] = 2  # filter_by_mask keeps only == 1
+    ref = g["lund_480x640__keypoints"]
+    r = np.round(ref).astype(int)
+    kept = ref[mask[r[:, 1], r[:, 0]] == 1]
+    kp, _, _ = deep.superpoint(img, superpoint_state_dict(0), mask=mask)
+    np.testing.assert_array_equal(kp, kept)
+    k = len(kept) // 2
+    kp_k, sc_k, _ = deep.superpoint(img, superpoint_state_dict(0), max_keypoints=k, mask=mask)
+    sc_all = g["lund_480x640__scores"][mask[r[:, 1], r[:, 0]] == 1]
+    assert len(kp_k) == k and np.isclose(np.sort(sc_k), np.sort(sc_all)[-k:], rtol=1e-5).all()
+
+
 @pytest.mark.parametrize("case", ["small_150x170", "mid_700x650"])
 def test_superglue_restatement_matches_reference(case):
     from oracle import deep

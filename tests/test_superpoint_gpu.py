@@ -125,3 +125,68 @@ def test_c3_1080p_top_4096(det, golden, golden_dir):
     for r, d in zip(golden["lund_1920x1080__desc_rows"], golden["lund_1920x1080__desc"]):
         if ref_pos[r] >= 0:
             np.testing.assert_allclose(desc[ref_pos[r]], d, atol=2e-4)
+
+
+def _c3_mask(H, W):
+    """A mask with a hole, a margin and stray values 2 (filter_by_mask keeps only == 1)."""
+    rng = np.random.default_rng(11)
+    m = np.ones((H, W), np.uint8)
+    m[H // 4: H // 2, W // 3: 2 * W // 3] = 0
+    m[:, : W // 10] = 0
+    m[rng.random((H, W)) < 0.05] = 2
+    return m
+
+
+def test_c3_1080p_mask_top_4096(det, golden_dir):
+    """Row a16 with image.mask (reference superpoint.py:68-72: filter_by_mask, then get_top_k(4096)): the masked
+    device run equals, bit for bit, the unmasked device run's detections filtered by mask == 1 and cut to the 4096
+    highest scores (raster order within, ties by raster order); and keeps >= 99.5 % of the oracle's masked set."""
+    from PIL import Image as PILImage
+
+    gray = np.asarray(PILImage.open(os.path.join(golden_dir, "lund_door_DSC_0001_gray.png")))
+    img = np.ascontiguousarray(gray[8:1928, 108:1188])
+    H, W = img.shape
+    mask = _c3_mask(H, W)
+    full = det.extract_batch([img], max_kpts=1 << 17)
+    n = int(full.count[0])
+    assert n == int(full.n_detected[0]) and n > 8192
+    xy = full.xy[0, :n].cpu().numpy()
+    sc = full.scores[0, :n].cpu().numpy()
+    desc = full.desc[0, :n].cpu().numpy()
+    keep = np.flatnonzero(mask[xy[:, 1].astype(int), xy[:, 0].astype(int)] == 1)
+    assert 0 < len(keep) < n
+    top = keep[np.sort(np.argsort(-sc[keep], kind="stable")[:4096])]
+    res = det.extract_batch([img], max_kpts=4096, masks=[mask])
+    m = int(res.count[0])
+    assert m == min(4096, len(keep)) and int(res.n_detected[0]) == len(keep)
+    assert np.array_equal(res.xy[0, :m].cpu().numpy(), xy[top])
+    assert np.array_equal(res.scores[0, :m].cpu().numpy(), sc[top])
+    assert np.array_equal(res.desc[0, :m].cpu().numpy(), desc[top])
+    # the oracle (reference module restated on the host) with the same mask
+    from oracle import deep
+
+    o_xy, o_sc, _ = deep.superpoint(img, superpoint_state_dict(0), max_keypoints=4096, mask=mask)
+    a, b = _keyset(res.xy[0, :m].cpu().numpy()), _keyset(o_xy)
+    assert len(a & b) >= 0.995 * max(len(a), len(b)), (len(a), len(b), len(a & b))
+
+
+def test_plugin_mask_equals_batched(det, golden):
+    """The drop-in's detect_and_describe(Image(value, mask)) and the batched generator's extraction agree, and a mask
+    of all ones changes nothing."""
+    from gtsfm_amd.common.image import Image
+    from gtsfm_amd.frontend.correspondence_generator.det_desc_correspondence_generator import \
+        extract_superpoint_batched
+
+    img = golden["lund_480x640__image"]
+    mask = _c3_mask(*img.shape)
+    d = type(det)(max_keypoints=700, state_dict=superpoint_state_dict(0))
+    kp, desc = d.detect_and_describe(Image(img, mask=mask))
+    assert len(kp) <= 700 and (mask[kp.coordinates[:, 1].astype(int), kp.coordinates[:, 0].astype(int)] == 1).all()
+    feats = extract_superpoint_batched(d, [Image(img, mask=mask), Image(img)])
+    n0 = int(feats.count[0])
+    assert n0 == len(kp)
+    assert np.array_equal(feats.xy[0, :n0].cpu().numpy(), kp.coordinates)
+    assert np.array_equal(feats.desc[0, :n0].cpu().numpy(), desc)
+    kp1, desc1 = d.detect_and_describe(Image(img, mask=np.ones(img.shape, np.uint8)))
+    kp2, desc2 = d.detect_and_describe(Image(img))
+    assert np.array_equal(kp1.coordinates, kp2.coordinates) and np.array_equal(desc1, desc2)
