@@ -1560,7 +1560,12 @@ __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* 
         bool alive = true;
 #pragma unroll 1
         for (int it = 0; it < n_it; ++it) {
-            const unsigned long long pk = __atomic_load_n(&pref[c], __ATOMIC_RELAXED);
+            unsigned long long pk = __atomic_load_n(&pref[c], __ATOMIC_RELAXED);
+            if constexpr (kS > 1) {  // one lane's read for the whole group: the prune decision is provably uniform
+                const int src = (tid & 63) & ~(kS - 1);
+                const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)pk, src), hi = (uint32_t)__shfl((int)(pk >> 32), src);
+                pk = ((unsigned long long)hi << 32) | lo;
+            }
             const uint32_t pb = (uint32_t)(pk >> 32), pid = (uint32_t)(pk >> kKeyCountBits) & 0x1FFFu;
             const uint32_t gb = gsum(bad);  // uniform over the group
             if (gb > pb || (gb == pb && myid > pid)) {
@@ -1820,6 +1825,9 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
         (scoring != GTSFM_RANSAC_SCORING_RANSAC && scoring != GTSFM_RANSAC_SCORING_MSAC))
         return GTSFM_ERR_ARG;
     const bool msac = scoring == GTSFM_RANSAC_SCORING_MSAC;
+    // selection key widths (ransac_score_kernel): the inlier count holds kKeyCountBits bits, and an MSAC score (at
+    // most 65536 per putative) must not wrap its 32 bits
+    if (mcap >= (1 << kKeyCountBits) || (msac && mcap > 65535)) return GTSFM_ERR_ARG;
     size_t o_x2, o_pts, o_st, o_cand, o_nsol, o_stage;
     const size_t need = ransac_layout(n_pairs, mcap, &o_x2, &o_pts, &o_st, &o_cand, &o_nsol, &o_stage);
     if (workspace_bytes < need) return GTSFM_ERR_CAPACITY;

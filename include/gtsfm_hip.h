@@ -113,7 +113,8 @@ int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop);
  * 6 putatives, 2 no model), number of hypotheses evaluated (d_n_hyp may be NULL), number of candidate models scored
  * (the real 5-point solutions of those hypotheses; d_n_models may be NULL; a measurement output with no reference
  * counterpart, it prices the RANSAC FLOP count of SURVEY.md §8(d)) and the inlier mask d_inlier_mask[n_pairs][mcap]
- * over the putatives in matcher order.
+ * over the putatives in matcher order. mcap < 2^19, and mcap <= 65535 with MSAC (the selection key's widths):
+ * GTSFM_ERR_ARG otherwise.
  * ---------------------------------------------------------------------------------------------- */
 size_t gtsfm_ransac_workspace_bytes(int n_pairs, int mcap);
 
