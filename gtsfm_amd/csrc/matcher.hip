@@ -137,10 +137,7 @@ constexpr int kPpWaves = 2 * kPpGroupWaves;
 constexpr int kPpThreads = kPpWaves * 64;
 constexpr int kPpRowsPerPass = kPpWaves * 64;  // 512
 constexpr int kUnitCols = 64;
-#ifndef GTSFM_PP_MAX_GROUP
-#define GTSFM_PP_MAX_GROUP 4
-#endif
-constexpr int kMaxGroup = GTSFM_PP_MAX_GROUP;
+constexpr int kMaxGroup = 4;
 constexpr int kPpLdsBudget = 160 * 1024;
 constexpr int kRowAlign = 256;                 // kpad granularity of the packed forms
 
@@ -156,13 +153,6 @@ struct PpCfg {
 typedef unsigned pp_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int uniform(int x) { return __builtin_amdgcn_readfirstlane(x); }
-// a wave-uniform pointer kept in SGPRs (so a lane offset added to it makes a saddr + 32-bit voffset access)
-template <typename T>
-__device__ __forceinline__ T* uniform_ptr(T* p) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (T*)(((unsigned long long)hi << 32) | lo);
-}
 
 // x from lane (l ^ d) within each 32-lane half (ds_swizzle bit mode: and 0x1F, xor d; no address VGPR)
 __device__ __forceinline__ uint32_t xor_swizzle(uint32_t x, int d) {
@@ -219,26 +209,6 @@ __device__ __forceinline__ void ins2x4(uint32_t& b10, uint32_t& b20, uint32_t a0
         : "v"(a0), "v"(c0), "v"(a1), "v"(c1), "v"(a2), "v"(c2), "v"(a3), "v"(c3));
 }
 
-// two independent inserts in one asm statement, interleaved
-__device__ __forceinline__ void ins2x2(uint32_t& b10, uint32_t& b20, uint32_t a0, uint32_t c0,
-                                       uint32_t& b11, uint32_t& b21, uint32_t a1, uint32_t c1) {
-    uint32_t m0, m1;
-    asm("v_med3_u32 %4, %0, %6, %7\n\t"
-        "v_med3_u32 %5, %2, %8, %9\n\t"
-        "v_min3_u32 %0, %0, %6, %7\n\t"
-        "v_min3_u32 %2, %2, %8, %9\n\t"
-        "v_min_u32 %1, %1, %4\n\t"
-        "v_min_u32 %3, %3, %5"
-        : "+v"(b10), "+v"(b20), "+v"(b11), "+v"(b21), "=&v"(m0), "=&v"(m1)
-        : "v"(a0), "v"(c0), "v"(a1), "v"(c1));
-}
-
-#ifndef GTSFM_PP_LEGACY  // default epilogue: 4-way asm inserts, t-merged column keys, deferred C2 atomic, pinned B reads
-#define GTSFM_PP_X4 1
-#define GTSFM_PP_DEFER 1
-#define GTSFM_PP_TMERGE 1
-#define GTSFM_PP_SGB 1
-#endif
 
 // Per-slot (pair) description, wave-uniform.
 struct PpSlot {
@@ -253,12 +223,7 @@ struct PpIter {
     PpSlot cur;
 };
 
-#ifdef GTSFM_PP_STAMPS  // diagnostic builds only: per-wave cycle sums of M, barrier after M, E, barrier after E
-__device__ unsigned long long g_pp_stamps[kPpWaves * 8];
-#define PP_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
 #define PP_STAMP(v)
-#endif
 
 template <int NK, bool kClamp>
 __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* __restrict__ a_form,
@@ -376,11 +341,9 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 #pragma unroll
         for (int g = 0; g < 16; ++g) rb1[t][g] = rb2[t][g] = kNoKey;
     f32x16 acc[2][2];  // [sub (32-column tile)][t (32-row tile)]
-#ifdef GTSFM_PP_DEFER
     uint32_t dold = 0, dm1 = 0, dm2 = 0;  // the pending C2 update of the previous unit
     uint32_t* dptr = colstate;
     bool dpend = false;
-#endif
 
     PpIter work = first, cpy = first;
     if (first.valid) {  // unit 0 -> ring[0]
@@ -407,15 +370,8 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         if (pending) stage_store(cpy_pending);
         pending = false;
     };
-#ifdef GTSFM_PP_STATIC_PRIO
-    if (grp == 1) __builtin_amdgcn_s_setprio(1);  // the younger half wins arbitration, no per-segment flips
-#endif
     if (grp == 1 && n_units > 0) copy_begin();  // group 1's leading phase 0: the load of unit 1
     if (grp == 1 && n_units > 0) __syncthreads();
-#ifdef GTSFM_PP_STAMPS
-    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long te0 = 0, te1 = 0, te2 = 0, te3 = 0;
-#endif
     for (int k = 0; k < n_units; ++k) {
         PP_STAMP(t0);
         const PpSlot si = work.cur;
@@ -426,15 +382,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         // a short stall the partner wave's E covers).
         load_a(si.img_a, work.pass);
         if (grp == 0) copy_begin();  // after the A loads, so the MFMAs never wait for the staged copy
-#ifndef GTSFM_PP_PRIO_M
-#define GTSFM_PP_PRIO_M 2
-#endif
-#ifndef GTSFM_PP_PRIO_E
-#define GTSFM_PP_PRIO_E 0
-#endif
-#ifndef GTSFM_PP_STATIC_PRIO
-        __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_M);  // the MFMA stream outranks the partner wave's VALU epilogue
-#endif
+        __builtin_amdgcn_s_setprio(2);  // the MFMA stream outranks the partner wave's VALU epilogue
         if (rows_here) {
             const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
 #pragma unroll
@@ -442,9 +390,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
             half8 bf[2][2];  // [k-step parity][sub]: the next k-step's B fragments are read ahead
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) bf[0][sub] = *(const half8*)(bb + sub * Cfg::kChunkBytes);
-#ifdef GTSFM_PP_SGB
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#endif
 #pragma unroll
             for (int s = 0; s < NK; ++s) {
                 if (s + 1 < NK) {
@@ -457,10 +403,8 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                     acc[sub][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[0][s], bf[s & 1][sub], acc[sub][0], 0, 0, 0);
                     acc[sub][1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[1][s], bf[s & 1][sub], acc[sub][1], 0, 0, 0);
                 }
-#ifdef GTSFM_PP_SGB  // pin the schedule: the next k-step's two B reads ahead of this k-step's four MFMAs
                 if (s + 1 < NK) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                 __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-#endif
             }
         }
         if (grp == 1) copy_end();  // loaded at the start of phase 2k
@@ -468,23 +412,14 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         __syncthreads();
         PP_STAMP(t2);
         // ---- phase B: group 0 -> phase 2k+1, group 1 -> phase 2k+2 (load of unit k+2)
-#ifndef GTSFM_PP_STATIC_PRIO
-        __builtin_amdgcn_s_setprio(GTSFM_PP_PRIO_E);
-#endif
+        __builtin_amdgcn_s_setprio(0);
         if (grp == 1) copy_begin();
-#ifdef GTSFM_PP_STAMPS
-        te0 = te1 = te2 = te3 = __builtin_amdgcn_s_memtime();
-#endif
         if (rows_here) {
-#ifdef GTSFM_PP_STAMPS
-            te1 = __builtin_amdgcn_s_memtime();
-#endif
             // columns: value-only top-2 over the lane's 16 rows of each (column tile, row tile) -> keys
             // (d2 << ib) | row with row = rowbase | code; the two row tiles merged; a permlane32 swap then gives lane L
             // both halves' top-2 of column tile L >> 5, column L & 31, so lane L owns unit column L: one returning
             // atomic min on C1 and one on C2 per lane (min(max(old, k1), k2) keeps the exact top-2 in any order)
             uint32_t s1[2], s2[2];
-#ifdef GTSFM_PP_X4
             uint32_t cv1[2][2], cv2[2][2];  // the four (sub, t) column chains, advanced together
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub)
@@ -499,8 +434,6 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                 ins2x4(cv1[0][0], cv2[0][0], PPU(0, 0, g), PPU(0, 0, g + 1), cv1[0][1], cv2[0][1], PPU(0, 1, g),
                        PPU(0, 1, g + 1), cv1[1][0], cv2[1][0], PPU(1, 0, g), PPU(1, 0, g + 1), cv1[1][1], cv2[1][1],
                        PPU(1, 1, g), PPU(1, 1, g + 1));
-#endif
-#ifdef GTSFM_PP_TMERGE
             // the two row tiles of a column merge on the raw values (ties to t = 0: its rows come first), so one key
             // is built per column tile instead of two
 #pragma unroll
@@ -516,51 +449,17 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                 s1[sub] = (d1 << ib) | rowbase | (u & 15u);
                 s2[sub] = d2 << ib;
             }
-#else
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub) {
-                uint32_t k1[2], k2[2];
-#pragma unroll
-                for (int t = 0; t < 2; ++t) {
-#ifdef GTSFM_PP_X4
-                    const uint32_t v1 = cv1[sub][t], v2 = cv2[sub][t];
-#else
-                    const f32x16& a = acc[sub][t];
-                    uint32_t v1 = umin(__float_as_uint(a[0]), __float_as_uint(a[1]));
-                    uint32_t v2 = umax(__float_as_uint(a[0]), __float_as_uint(a[1]));
-#pragma unroll
-                    for (int g = 2; g < 16; g += 2) ins2(v1, v2, __float_as_uint(a[g]), __float_as_uint(a[g + 1]));
-#endif
-                    const uint32_t u = (uint32_t)(__uint_as_float(v1) * 16.f);
-                    uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
-                    if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
-                    const uint32_t rowbase = (uint32_t)(r0w + 32 * t + 16 * half);
-                    k1[t] = (d1 << ib) | rowbase | (u & 15u);
-                    k2[t] = d2 << ib;  // the second's index never matters
-                }
-                s1[sub] = umin(k1[0], k1[1]);
-                s2[sub] = med3u(k1[0], k1[1], umin(k2[0], k2[1]));
-            }
-#endif
             const auto x1 = __builtin_amdgcn_permlane32_swap(s1[0], s1[1], false, false);
             const auto x2 = __builtin_amdgcn_permlane32_swap(s2[0], s2[1], false, false);
             const uint32_t m1 = umin(x1[0], x1[1]), m2 = med3u(x1[0], x1[1], umin(x2[0], x2[1]));
-#ifdef GTSFM_PP_STAMPS
-            te2 = __builtin_amdgcn_s_memtime();
-#endif
             uint32_t* c1s = colstate + work.slot * 2 * kmax64 + work.sc * kUnitCols + lane;
-#ifdef GTSFM_PP_DEFER
             if (dpend) __hip_atomic_fetch_min(dptr + kmax64, umin(umax(dold, dm1), dm2), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_WORKGROUP);
             dold = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             dm1 = m1; dm2 = m2; dptr = c1s; dpend = true;
-#else
-            const uint32_t old = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
             // the row inserts run while the returning atomic is in flight
             __builtin_amdgcn_sched_barrier(0);
             // rows: both column tiles' values of row (t, g) in one paired insert
-#ifdef GTSFM_PP_X4
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -569,20 +468,7 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                            PPU(0, t, g + 1), PPU(1, t, g + 1), rb1[t][g + 2], rb2[t][g + 2], PPU(0, t, g + 2),
                            PPU(1, t, g + 2), rb1[t][g + 3], rb2[t][g + 3], PPU(0, t, g + 3), PPU(1, t, g + 3));
 #undef PPU
-#else
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int g = 0; g < 16; ++g)
-                    ins2(rb1[t][g], rb2[t][g], __float_as_uint(acc[0][t][g]), __float_as_uint(acc[1][t][g]));
-#endif
             __builtin_amdgcn_sched_barrier(0);
-#ifndef GTSFM_PP_DEFER
-            __hip_atomic_fetch_min(c1s + kmax64, umin(umax(old, m1), m2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
-#ifdef GTSFM_PP_STAMPS
-            te3 = __builtin_amdgcn_s_memtime();
-#endif
             if (work.sc == si.nsup - 1) {
                 // the pass is over for this pair: halving exchange across each half-wave's 32 lanes, then lane
                 // (lrow, half) holds register j = lrow = 16 t + g, i.e. keypoint r0w + 32 t + 16 half + g
@@ -612,19 +498,9 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         PP_STAMP(t3);
         __syncthreads();
         PP_STAMP(t4);
-#ifdef GTSFM_PP_STAMPS
-        st[0] += t1 - t0; st[1] += t2 - t1; st[2] += t3 - t2; st[3] += t4 - t3;
-        st[4] += te1 - te0; st[5] += te2 - te1; st[6] += te3 - te2; st[7] += t3 - te3;
-#endif
     }
-#ifdef GTSFM_PP_STAMPS
-    if (lane == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd(&g_pp_stamps[wave * 8 + i], st[i]);
-#endif
-#ifdef GTSFM_PP_DEFER
     if (dpend) __hip_atomic_fetch_min(dptr + kmax64, umin(umax(dold, dm1), dm2), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
     if (grp == 0 && n_units > 0) __syncthreads();  // group 0's trailing phase 2U (group 1's E of the last unit)
     __syncthreads();
     for (int s = 0; s < G; ++s) {
@@ -633,653 +509,6 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         const uint32_t* c1s = colstate + s * 2 * kmax64;
         const uint32_t* c2s = c1s + kmax64;
         for (int c = tid; c < si.nb; c += kPpThreads) colres[(size_t)si.pair * kmax + c] = make_uint2(c1s[c], c2s[c]);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused distance GEMM + row/column top-2 at FOUR waves per SIMD (mnn_q_kernel, the default INT_F16 kernel).
-//
-// mnn_pp_kernel's single epilogue wave per SIMD issues at most one VALU per ~4-5 cycles (one wave's own cadence),
-// while a SIMD-32 issues a wave64 VALU every 2 cycles when two waves supply them: its epilogue, not the matrix pipe,
-// set the phase length. Here a workgroup is 16 waves in two teams of 8 (waves w, w + 4, w + 8, w + 12 share a SIMD:
-// two of each team per SIMD). Each wave holds ONE 32-row tile of A in registers (36 VGPRs at NK = 9), so a pass is
-// still 512 rows; a unit is 64 columns (two 32-column tiles, 18 MFMAs per wave). Team 0 runs M(k) in phase 2k and
-// E(k) in phase 2k + 1, team 1 one phase later, so in every phase each SIMD has two waves streaming MFMAs (36 per
-// phase, 1152 matrix cycles) beside two waves whose epilogue VALU interleave.
-// B: unit k + 1 is copied into the free ring slot during the E phases, each wave moving its own 1/16 of the unit
-// (team 0 in phase 2k + 1, team 1's share of unit k + 2 in phase 2k + 2), staged through VGPRs that are dead in M.
-// Epilogue per wave and unit: columns as mnn_pp_kernel (value-only top-2 over the lane's 16 rows, two row halves per
-// column tile as independent chains, merged, one packed key per column tile, permlane32 swap, returning LDS atomicMin
-// on C1 and a deferred one on C2); rows: value-only top-2 of the tile's 16 rows per lane, both column tiles' values
-// in one paired insert.
-// ---------------------------------------------------------------------------------------------
-constexpr int kQWaves = 16;
-__device__ unsigned long long g_q_stamps[kQWaves * 8];  // kVar 5 (diagnostic): per-wave cycles M, bar, E cols, E rows, E wait, bar
-constexpr int kQThreads = kQWaves * 64;            // 1024
-constexpr int kQRowsPerPass = kQWaves * 32;        // 512
-
-template <int NK, bool kClamp, int kVar = 0>
-__global__ __launch_bounds__(kQThreads, 1) void mnn_q_kernel(const _Float16* __restrict__ a_form,
-                                                             const _Float16* __restrict__ b_form,
-                                                             const int* __restrict__ counts,
-                                                             const int* __restrict__ pairs, int n_pairs,
-                                                             const int* __restrict__ groups, int n_groups,
-                                                             int group_size, int kpad, int kmax, int kmax64, int ib,
-                                                             uint2* __restrict__ rowres, uint2* __restrict__ colres) {
-    using Cfg = PpCfg<NK>;
-    constexpr int kWaveBytes = Cfg::kUnitBytes / kQWaves;            // NK * 128: each wave's share of a unit
-    constexpr int kMain = kWaveBytes >= 1024 ? 1024 : kWaveBytes;    // 16 B per lane, lanes < kMain / 16
-    constexpr int kRest = kWaveBytes - kMain;                        // lanes < kRest / 16 (NK = 9: 128 B)
-    static_assert(Cfg::kUnitBytes % kQWaves == 0 && kMain % 16 == 0 && kRest % 16 == 0 && kRest <= 1024, "copy split");
-    __shared__ __attribute__((aligned(1024))) unsigned char ring[2 * Cfg::kUnitBytes];
-    __shared__ int sinfo[kMaxGroup * 8];
-    extern __shared__ __attribute__((aligned(16))) uint32_t colstate[];  // [G][2][kmax64]
-
-    const int tid = threadIdx.x, wave = uniform(tid >> 6), lane = tid & 63;
-    const int lrow = lane & 31, half = lane >> 5, team = wave >> 3;
-    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_groups >> 3, r8 = n_groups & 7;
-    const int grp_idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
-    const int G = groups ? group_size : 1;
-
-    if (tid < kMaxGroup) {
-        int p = -1;
-        if (tid < G) p = groups ? groups[(size_t)grp_idx * group_size + tid] : grp_idx;
-        if (p >= n_pairs) p = -1;
-        int ia = 0, ibm = 0, na = 0, nb = 0;
-        if (p >= 0) {
-            ia = pairs[2 * p];
-            ibm = pairs[2 * p + 1];
-            na = counts[ia];
-            nb = counts[ibm];
-            if (na <= 0 || nb <= 0) na = nb = 0;
-        }
-        int* si = sinfo + tid * 8;
-        si[0] = p; si[1] = ia; si[2] = ibm; si[3] = na; si[4] = nb; si[5] = (nb + kUnitCols - 1) / kUnitCols;
-    }
-    for (int c = tid; c < G * 2 * kmax64; c += kQThreads) colstate[c] = kNoKey;
-    __syncthreads();
-
-    auto slot_info = [&](int s) {
-        const int* si = sinfo + s * 8;
-        PpSlot r;
-        r.pair = uniform(si[0]); r.img_a = uniform(si[1]); r.img_b = uniform(si[2]);
-        r.na = uniform(si[3]); r.nb = uniform(si[4]); r.nsup = uniform(si[5]);
-        return r;
-    };
-    int npass = 0;
-    for (int s = 0; s < G; ++s) npass = max(npass, (slot_info(s).na + kQRowsPerPass - 1) / kQRowsPerPass);
-    auto seek = [&](PpIter& it) {
-        while (it.pass < npass) {
-            it.cur = slot_info(it.slot);
-            if (it.cur.pair >= 0 && it.cur.nsup > 0 && it.pass * kQRowsPerPass < it.cur.na) break;
-            if (++it.slot == G) { it.slot = 0; ++it.pass; }
-        }
-        it.valid = it.pass < npass;
-    };
-    auto advance = [&](PpIter& it) {
-        ++it.seq;
-        if (++it.sc < it.cur.nsup) return;
-        it.sc = 0;
-        if (++it.slot == G) { it.slot = 0; ++it.pass; }
-        seek(it);
-    };
-    PpIter first;
-    first.pass = first.slot = first.sc = first.seq = 0;
-    seek(first);
-    int n_units = 0;
-    for (PpIter it = first; it.valid; ) {
-        n_units += it.cur.nsup;
-        it.seq += it.cur.nsup - 1;
-        it.sc = it.cur.nsup - 1;
-        advance(it);
-    }
-
-    // this wave's share of a B unit, bytes [wave * kWaveBytes, +kWaveBytes), by LDS-DMA (global_load_lds_dwordx4:
-    // 16 B per lane straight into the ring, no VGPR staging); the issuing wave waits for it before the barrier that
-    // publishes the slot
-    auto copy_dma = [&](const PpIter& it) {
-        // buffer resource over image img_b's B form: a 32-bit lane offset and a uniform soffset, no 64-bit VGPR address
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(b_form + (size_t)it.cur.img_b * kpad * Cfg::kDa), (short)0, kpad * Cfg::kDa * 2, 0x00020000);
-        const int soff = it.sc * kUnitCols * Cfg::kDa * 2 + wave * kWaveBytes;
-        unsigned char* dst = ring + (it.seq & 1) * Cfg::kUnitBytes + wave * kWaveBytes;
-        if (kMain == 1024 || lane < kMain / 16)
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)dst, 16, lane * 16,
-                                                     soff, 0, 0);
-        if constexpr (kRest > 0)
-            if (lane < kRest / 16)
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(dst + kMain),
-                                                         16, lane * 16, soff + kMain, 0, 0);
-    };
-
-    half8 afrag[NK];
-    int a_loaded_img = -1, a_loaded_pass = -1;
-    auto load_a = [&](int img, int pass) {
-        if (img == a_loaded_img && pass == a_loaded_pass) return;
-        a_loaded_img = img;
-        a_loaded_pass = pass;
-        const int r0w = pass * kQRowsPerPass + wave * 32;
-        if (r0w >= kpad) return;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(a_form + (size_t)img * kpad * Cfg::kDa), (short)0, kpad * Cfg::kDa * 2, 0x00020000);
-        const int voff = (lrow * Cfg::kDa + 8 * half) * 2;
-#pragma unroll
-        for (int s = 0; s < NK; ++s) {
-            const pp_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, r0w * Cfg::kDa * 2 + 32 * s, 0);
-            afrag[s] = __builtin_bit_cast(half8, v);
-        }
-        __builtin_amdgcn_s_waitcnt(0x0070);
-    };
-
-    const uint32_t dsat = (1u << (32 - ib)) - 1u;
-    uint32_t rb1[16], rb2[16];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) rb1[g] = rb2[g] = kNoKey;
-    f32x16 acc[2];  // [sub (32-column tile)]
-    uint32_t dold = 0, dm1 = 0, dm2 = 0;  // the pending C2 update of the previous unit
-    uint32_t* dptr = colstate;
-    bool dpend = false;
-
-    PpIter work = first, cpy = first;
-    if (first.valid) {  // unit 0 -> ring[0], every wave its share
-        copy_dma(cpy);
-        advance(cpy);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    if (team == 1 && n_units > 0) {  // team 1's leading phase 0: its share of unit 1
-        if (cpy.valid) {
-            copy_dma(cpy);
-            advance(cpy);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    unsigned long long qs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < n_units; ++k) {
-        unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0, qa = 0, qb = 0;
-        if constexpr (kVar == 5) q0 = __builtin_amdgcn_s_memtime();
-        const PpSlot si = work.cur;
-        const int r0w = work.pass * kQRowsPerPass + wave * 32;
-        const bool rows_here = r0w < si.na;
-        // ---- M(k): 2 column tiles x 9 k-steps against this wave's 32 rows
-        load_a(si.img_a, work.pass);
-        __builtin_amdgcn_s_setprio(2);
-        if (rows_here && kVar != 4) {
-            const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
-            acc[0] = acc[1] = f32x16{};
-            half8 bf[2][2];
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub) bf[0][sub] = *(const half8*)(bb + sub * Cfg::kChunkBytes);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-            for (int s = 0; s < NK; ++s) {
-                if (s + 1 < NK) {
-#pragma unroll
-                    for (int sub = 0; sub < 2; ++sub)
-                        bf[(s + 1) & 1][sub] = *(const half8*)(bb + sub * Cfg::kChunkBytes + 1024 * (s + 1));
-                }
-#pragma unroll
-                for (int sub = 0; sub < 2; ++sub)
-                    acc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[s], bf[s & 1][sub], acc[sub], 0, 0, 0);
-                if (s + 1 < NK) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            }
-        }
-        if constexpr (kVar == 5) q1 = __builtin_amdgcn_s_memtime();
-        __syncthreads();
-        if constexpr (kVar == 5) q2 = __builtin_amdgcn_s_memtime();
-        // ---- E(k), plus this wave's share of the next unit to copy (into the slot the unit before k held: free since
-        // the barrier that ended the phase of its last reader)
-        __builtin_amdgcn_s_setprio(0);
-        const bool do_copy = cpy.valid && kVar != 2;
-        if (kVar == 1 && do_copy) copy_dma(cpy);
-        if (kVar == 4) acc[0] = acc[1] = f32x16{};
-        if (rows_here && kVar != 3) {
-            uint32_t cv1[2][2], cv2[2][2];  // [sub][row half of the lane's 16 rows]
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    cv1[sub][h] = umin(__float_as_uint(acc[sub][8 * h]), __float_as_uint(acc[sub][8 * h + 1]));
-                    cv2[sub][h] = umax(__float_as_uint(acc[sub][8 * h]), __float_as_uint(acc[sub][8 * h + 1]));
-                }
-#define PQU(sub, g) __float_as_uint(acc[sub][g])
-#pragma unroll
-            for (int g = 2; g < 8; g += 2)
-                ins2x4(cv1[0][0], cv2[0][0], PQU(0, g), PQU(0, g + 1), cv1[0][1], cv2[0][1], PQU(0, g + 8),
-                       PQU(0, g + 9), cv1[1][0], cv2[1][0], PQU(1, g), PQU(1, g + 1), cv1[1][1], cv2[1][1],
-                       PQU(1, g + 8), PQU(1, g + 9));
-            uint32_t s1[2], s2[2];
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub) {
-                // the two row halves hold distinct rows (distinct codes): merge on the raw values
-                const uint32_t a0 = cv1[sub][0], a1 = cv1[sub][1];
-                const uint32_t v1 = umin(a0, a1);
-                const uint32_t v2 = med3u(a0, a1, umin(cv2[sub][0], cv2[sub][1]));
-                const uint32_t u = (uint32_t)(__uint_as_float(v1) * 16.f);
-                uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
-                if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
-                s1[sub] = (d1 << ib) | (uint32_t)(r0w + 16 * half) | (u & 15u);
-                s2[sub] = d2 << ib;
-            }
-            const auto x1 = __builtin_amdgcn_permlane32_swap(s1[0], s1[1], false, false);
-            const auto x2 = __builtin_amdgcn_permlane32_swap(s2[0], s2[1], false, false);
-            const uint32_t m1 = umin(x1[0], x1[1]), m2 = med3u(x1[0], x1[1], umin(x2[0], x2[1]));
-            uint32_t* c1s = colstate + work.slot * 2 * kmax64 + work.sc * kUnitCols + lane;
-            if (dpend) __hip_atomic_fetch_min(dptr + kmax64, umin(umax(dold, dm1), dm2), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-            dold = __hip_atomic_fetch_min(c1s, m1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            dm1 = m1; dm2 = m2; dptr = c1s; dpend = true;
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (kVar == 5) qa = __builtin_amdgcn_s_memtime();
-            if (kVar != 1 && do_copy) copy_dma(cpy);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int g = 0; g < 16; g += 4)
-                ins2x4(rb1[g], rb2[g], PQU(0, g), PQU(1, g), rb1[g + 1], rb2[g + 1], PQU(0, g + 1), PQU(1, g + 1),
-                       rb1[g + 2], rb2[g + 2], PQU(0, g + 2), PQU(1, g + 2), rb1[g + 3], rb2[g + 3], PQU(0, g + 3),
-                       PQU(1, g + 3));
-#undef PQU
-            __builtin_amdgcn_sched_barrier(0);
-            if (work.sc == si.nsup - 1) {
-                // the pass is over for this pair: halving exchange over register bits 3..0 within each half-wave,
-                // then lanes l and l ^ 16 merge, so lane (lrow, half) holds row r0w + 16 half + (lrow & 15)
-#pragma unroll
-                for (int d = 8; d >= 1; d >>= 1) {
-                    const bool up = (lrow & d) != 0;
-#pragma unroll
-                    for (int j = 0; j < d; ++j) {
-                        const uint32_t t1 = up ? rb1[j] : rb1[j + d], t2 = up ? rb2[j] : rb2[j + d];
-                        const uint32_t q1 = up ? rb1[j + d] : rb1[j], q2 = up ? rb2[j + d] : rb2[j];
-                        const uint32_t o1 = xor_swizzle(t1, d), o2 = xor_swizzle(t2, d);
-                        rb1[j] = umin(q1, o1);
-                        rb2[j] = med3u(q1, o1, umin(q2, o2));
-                        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-                {
-                    const uint32_t o1 = xor_swizzle(rb1[0], 16), o2 = xor_swizzle(rb2[0], 16);
-                    const uint32_t q1 = rb1[0], q2 = rb2[0];
-                    rb1[0] = umin(q1, o1);
-                    rb2[0] = med3u(q1, o1, umin(q2, o2));
-                }
-                const int key = r0w + 16 * half + (lrow & 15);
-                if (lrow < 16 && key < si.na) rowres[(size_t)si.pair * kmax + key] = make_uint2(rb1[0], rb2[0]);
-#pragma unroll
-                for (int g = 0; g < 16; ++g) rb1[g] = rb2[g] = kNoKey;
-            }
-        } else if (kVar != 1 && do_copy) {
-            copy_dma(cpy);
-        }
-        if (cpy.valid) advance(cpy);
-        advance(work);
-        if constexpr (kVar == 5) qb = __builtin_amdgcn_s_memtime();
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if constexpr (kVar == 5) q3 = __builtin_amdgcn_s_memtime();
-        __syncthreads();
-        if constexpr (kVar == 5) {
-            const unsigned long long q4 = __builtin_amdgcn_s_memtime();
-            if (qa == 0) qa = q2;
-            if (qb == 0) qb = q3;
-            qs[0] += q1 - q0; qs[1] += q2 - q1; qs[2] += qa - q2; qs[3] += qb - qa; qs[4] += q3 - qb; qs[5] += q4 - q3;
-        }
-    }
-    if constexpr (kVar == 5)
-        if (lane == 0)
-            for (int i = 0; i < 8; ++i) atomicAdd(&g_q_stamps[wave * 8 + i], qs[i]);
-    if (dpend) __hip_atomic_fetch_min(dptr + kmax64, umin(umax(dold, dm1), dm2), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (team == 0 && n_units > 0) __syncthreads();  // team 0's trailing phase (team 1's E of the last unit)
-    __syncthreads();
-    for (int s = 0; s < G; ++s) {
-        const PpSlot si = slot_info(s);
-        if (si.pair < 0 || si.na == 0) continue;
-        const uint32_t* c1s = colstate + s * 2 * kmax64;
-        const uint32_t* c2s = c1s + kmax64;
-        for (int c = tid; c < si.nb; c += kQThreads) colres[(size_t)si.pair * kmax + c] = make_uint2(c1s[c], c2s[c]);
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused distance GEMM + row/column top-2, ROTATING roles at four waves per SIMD (mnn_r_kernel, the default INT_F16
-// kernel).
-//
-// Measured (tools/ubench/mfma_valu.hip): a SIMD issues this epilogue's v_min3/v_med3/v_min stream at ~7.5 cycles per
-// instruction from one wave, ~4.5 from two, ~3.6 from three; beside a wave streaming MFMAs, ~13 / 7.6 / 5.0. The
-// epilogue needs ~250 such instructions per 64 x 64 block, the MFMAs 36 x 32 = 1152 matrix cycles: with one epilogue
-// wave beside one MFMA wave (mnn_pp_kernel) the epilogue is the pole at ~2050 cycles per block.
-// Here the four waves of a SIMD (w, w + 4, w + 8, w + 12; role r = w >> 2) take turns: in phase p the wave of role
-// p mod 4 runs M (18 MFMAs: its 32 rows x the unit's 64 columns), the three others each run one third of their last
-// unit's epilogue (E1: column chains; E2: column keys, atomics and 4 rows; E3: 12 rows + the pass-end row exchange).
-// Per phase and SIMD: 576 matrix cycles beside ~125 epilogue instructions from three waves. A unit of B (64 columns)
-// serves the four phases 4k .. 4k + 3; unit k + 1 is copied into the other ring slot during them by LDS-DMA
-// (buffer_load ... lds, issued from inline asm so the compiler adds no waits on the ring reads) and waited for
-// before the barrier that ends phase 4k + 3.
-// Every wave holds ONE 32-row tile of A in registers (36 VGPRs at NK = 9): a pass covers 512 rows, as in
-// mnn_pp_kernel; pairs, groups, column state and results are laid out exactly as there.
-// ---------------------------------------------------------------------------------------------
-constexpr int kRWaves = 16;
-constexpr int kRThreads = kRWaves * 64;        // 1024
-constexpr int kRRowsPerPass = kRWaves * 32;    // 512
-typedef int r_i32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ r_i32x4 r_buffer_rsrc(const void* base, uint32_t bytes) {
-    const unsigned long long v = (unsigned long long)base;
-    r_i32x4 r;
-    r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));  // stride 0
-    r[2] = (int)bytes;
-    r[3] = 0x00020000;
-    return r;
-}
-
-// 16 bytes per lane from rsrc + soff + voff into LDS at lds + 16 * lane (LDS-DMA). M0 is set here: the kernel has no
-// other M0 user (checked in its ISA: every m0 write is this statement's).
-__device__ __forceinline__ void r_dma16(r_i32x4 rsrc, uint32_t voff, uint32_t soff, uint32_t lds) {
-    asm volatile("s_mov_b32 m0, %3\n\t"
-                 "s_nop 0\n\t"
-                 "buffer_load_dwordx4 %0, %1, %2 offen lds"
-                 :
-                 : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds)
-                 : "memory");
-}
-
-template <int NK, bool kClamp, bool kStamp = false>
-__global__ __launch_bounds__(kRThreads, 1) void mnn_r_kernel(const _Float16* __restrict__ a_form,
-                                                             const _Float16* __restrict__ b_form,
-                                                             const int* __restrict__ counts,
-                                                             const int* __restrict__ pairs, int n_pairs,
-                                                             const int* __restrict__ groups, int n_groups,
-                                                             int group_size, int kpad, int kmax, int kmax64, int ib,
-                                                             uint2* __restrict__ rowres, uint2* __restrict__ colres) {
-    using Cfg = PpCfg<NK>;
-    constexpr int kWaveBytes = Cfg::kUnitBytes / kRWaves;            // NK * 128: each wave's share of a unit
-    constexpr int kMain = kWaveBytes >= 1024 ? 1024 : kWaveBytes;    // lanes < kMain / 16
-    constexpr int kRest = kWaveBytes - kMain;                        // lanes < kRest / 16 (NK = 9: 128 B)
-    static_assert(Cfg::kUnitBytes % kRWaves == 0 && kMain % 16 == 0 && kRest % 16 == 0 && kRest <= 1024, "copy");
-    __shared__ __attribute__((aligned(1024))) unsigned char ring[2 * Cfg::kUnitBytes];
-    __shared__ int sinfo[kMaxGroup * 8];
-    extern __shared__ __attribute__((aligned(16))) uint32_t colstate[];  // [G][2][kmax64]
-
-    const int tid = threadIdx.x, wave = uniform(tid >> 6), lane = tid & 63;
-    const int lrow = lane & 31, half = lane >> 5, role = wave >> 2;
-    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_groups >> 3, r8 = n_groups & 7;
-    const int grp_idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
-    const int G = groups ? group_size : 1;
-
-    if (tid < kMaxGroup) {
-        int p = -1;
-        if (tid < G) p = groups ? groups[(size_t)grp_idx * group_size + tid] : grp_idx;
-        if (p >= n_pairs) p = -1;
-        int ia = 0, ibm = 0, na = 0, nb = 0;
-        if (p >= 0) {
-            ia = pairs[2 * p];
-            ibm = pairs[2 * p + 1];
-            na = counts[ia];
-            nb = counts[ibm];
-            if (na <= 0 || nb <= 0) na = nb = 0;
-        }
-        int* si = sinfo + tid * 8;
-        si[0] = p; si[1] = ia; si[2] = ibm; si[3] = na; si[4] = nb; si[5] = (nb + kUnitCols - 1) / kUnitCols;
-    }
-    for (int c = tid; c < G * 2 * kmax64; c += kRThreads) colstate[c] = kNoKey;
-    __syncthreads();
-
-    auto slot_info = [&](int s) {
-        const int* si = sinfo + s * 8;
-        PpSlot r;
-        r.pair = uniform(si[0]); r.img_a = uniform(si[1]); r.img_b = uniform(si[2]);
-        r.na = uniform(si[3]); r.nb = uniform(si[4]); r.nsup = uniform(si[5]);
-        return r;
-    };
-    int npass = 0;
-    for (int s = 0; s < G; ++s) npass = max(npass, (slot_info(s).na + kRRowsPerPass - 1) / kRRowsPerPass);
-    auto seek = [&](PpIter& it) {
-        while (it.pass < npass) {
-            it.cur = slot_info(it.slot);
-            if (it.cur.pair >= 0 && it.cur.nsup > 0 && it.pass * kRRowsPerPass < it.cur.na) break;
-            if (++it.slot == G) { it.slot = 0; ++it.pass; }
-        }
-        it.valid = it.pass < npass;
-    };
-    auto advance = [&](PpIter& it) {
-        ++it.seq;
-        if (++it.sc < it.cur.nsup) return;
-        it.sc = 0;
-        if (++it.slot == G) { it.slot = 0; ++it.pass; }
-        seek(it);
-    };
-    PpIter first;
-    first.pass = first.slot = first.sc = first.seq = 0;
-    seek(first);
-    int n_units = 0;
-    for (PpIter it = first; it.valid; ) {
-        n_units += it.cur.nsup;
-        it.seq += it.cur.nsup - 1;
-        it.sc = it.cur.nsup - 1;
-        advance(it);
-    }
-
-    // this wave's share of unit `it` (bytes [wave * kWaveBytes, +kWaveBytes)) into its ring slot
-    const uint32_t ring_lds = (uint32_t)(size_t)ring;
-    auto copy_unit = [&](const PpIter& it) {
-        const r_i32x4 rs = r_buffer_rsrc(b_form + (size_t)it.cur.img_b * kpad * Cfg::kDa, kpad * Cfg::kDa * 2);
-        const uint32_t soff = (uint32_t)(it.sc * kUnitCols * Cfg::kDa * 2 + wave * kWaveBytes);
-        const uint32_t dst = (uint32_t)uniform((int)(ring_lds + (it.seq & 1) * Cfg::kUnitBytes + wave * kWaveBytes));
-        if (kMain == 1024 || lane < kMain / 16) r_dma16(rs, lane * 16, soff, dst);
-        if constexpr (kRest > 0)
-            if (lane < kRest / 16) r_dma16(rs, lane * 16, soff + kMain, dst + kMain);
-    };
-
-    half8 afrag[NK];
-    int a_loaded_img = -1, a_loaded_pass = -1;
-    auto load_a = [&](int img, int pass) {
-        if (img == a_loaded_img && pass == a_loaded_pass) return;
-        a_loaded_img = img;
-        a_loaded_pass = pass;
-        const int r0w = pass * kRRowsPerPass + wave * 32;
-        if (r0w >= kpad) return;
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(a_form + (size_t)img * kpad * Cfg::kDa), (short)0, kpad * Cfg::kDa * 2, 0x00020000);
-        const int voff = (lrow * Cfg::kDa + 8 * half) * 2;
-#pragma unroll
-        for (int s = 0; s < NK; ++s) {
-            const pp_u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, r0w * Cfg::kDa * 2 + 32 * s, 0);
-            afrag[s] = __builtin_bit_cast(half8, v);
-        }
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as a builtin: the compiler then knows A has landed
-    };
-
-    const uint32_t dsat = (1u << (32 - ib)) - 1u;
-    uint32_t rb1[16], rb2[16];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) rb1[g] = rb2[g] = kNoKey;
-    f32x16 acc[2];  // [sub (32-column tile)], M -> E1 .. E3
-
-    PpIter work = first, cpy = first;
-    if (first.valid) {  // unit 0 -> ring[0], every wave its share
-        copy_unit(cpy);
-        advance(cpy);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    // Phase p: the wave of role p mod 4 runs M, the others an epilogue chunk. Each wave runs, per unit k, M(k) E1(k)
-    // E2(k) E3(k) with a barrier after each: role r starts r phases late (r leading barriers) and ends 3 - r phases
-    // early (3 - r trailing barriers), so M(k) of role r falls in phase 4k + r. The share of unit k + 1 is copied in
-    // phase 4k + (r == 0 ? 1 : 0) (role 0: E1(k); role r >= 1: E(4 - r) of unit k - 1, or a leading phase for k = 0)
-    // and waited for at the end of phase 4k + 3 (role r: after chunk 3 - r of unit k).
-    auto copy_next = [&]() {
-        if (cpy.valid) {
-            copy_unit(cpy);
-            advance(cpy);
-        }
-    };
-    unsigned long long qs[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_pre[4] = {0, 0, 0, 0}, st_post[4] = {0, 0, 0, 0},
-                       t_start = 0;
-    (void)qs; (void)st_pre; (void)st_post; (void)t_start;
-    if (n_units > 0) {
-        for (int q = 0; q < role; ++q) {  // leading phases
-            if (q == 0) copy_next();
-            __syncthreads();
-        }
-    }
-    for (int k = 0; k < n_units; ++k) {
-        const PpSlot si = work.cur;
-        const int r0w = work.pass * kRRowsPerPass + wave * 32;
-        const bool rows_here = r0w < si.na;
-        auto phase_end = [&](int c) {  // end of this wave's chunk c of unit k
-            if (c == 3 - role) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if constexpr (kStamp) st_pre[c] = __builtin_amdgcn_s_memtime();
-            __syncthreads();
-            if constexpr (kStamp) st_post[c] = __builtin_amdgcn_s_memtime();
-        };
-        if constexpr (kStamp) st_post[3] = __builtin_amdgcn_s_memtime();
-        // ---- M: this wave's 32 rows x the unit's 2 column tiles, 9 k-steps
-        load_a(si.img_a, work.pass);
-        __builtin_amdgcn_s_setprio(1);
-        if (rows_here) {
-            const unsigned char* bb = ring + (work.seq & 1) * Cfg::kUnitBytes + lane * 16;
-            acc[0] = acc[1] = f32x16{};
-            // B fragments read RA MFMAs ahead (a ring of RA): the MFMA of step t reads fragment t = 2 s + sub
-            constexpr int kT = 2 * NK, RA = 4;
-            half8 bf[RA];
-            auto bread = [&](int t) { return *(const half8*)(bb + (t & 1) * Cfg::kChunkBytes + 1024 * (t >> 1)); };
-#pragma unroll
-            for (int t = 0; t < RA; ++t) bf[t] = bread(t);
-            __builtin_amdgcn_sched_group_barrier(0x100, RA, 0);
-#pragma unroll
-            for (int t = 0; t < kT; ++t) {
-                acc[t & 1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(afrag[t >> 1], bf[t % RA], acc[t & 1], 0, 0, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                if (t + RA < kT) {
-                    bf[t % RA] = bread(t + RA);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
-            }
-        }
-        __builtin_amdgcn_s_setprio(0);
-        phase_end(0);
-#define PRU(sub, g) __float_as_uint(acc[sub][g])
-        // The epilogue in three chunks of ~40 VALU each (a SIMD issues them fastest when its three epilogue waves are
-        // all still issuing):
-        //   E1: column tile 0's value-only top-2 over the lane's 16 rows (two independent row halves) and its key
-        //       (d2 << ib) | row; rows 0..3
-        //   E2: the same for column tile 1, the permlane32 swap (lane L: unit column L's top-2 over the wave's 32
-        //       rows), the returning C1 atomic; rows 4..5
-        //   E3: the C2 atomic min(C2, min(max(old, k1), k2)) (the exact top-2 in any arrival order); rows 6..15 and,
-        //       at the pass's last unit, the row exchange + store
-        // (rows: both column tiles' values of a row in one paired insert)
-        auto col_key = [&](int sub, uint32_t& k1, uint32_t& k2) {
-            uint32_t c1[2], c2[2];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                c1[h] = umin(PRU(sub, 8 * h), PRU(sub, 8 * h + 1));
-                c2[h] = umax(PRU(sub, 8 * h), PRU(sub, 8 * h + 1));
-            }
-#pragma unroll
-            for (int g = 2; g < 8; g += 2)
-                ins2x2(c1[0], c2[0], PRU(sub, g), PRU(sub, g + 1), c1[1], c2[1], PRU(sub, g + 8), PRU(sub, g + 9));
-            const uint32_t v1 = umin(c1[0], c1[1]);  // the halves hold distinct rows (codes): no ties
-            const uint32_t v2 = med3u(c1[0], c1[1], umin(c2[0], c2[1]));
-            const uint32_t u = (uint32_t)(__uint_as_float(v1) * 16.f);
-            uint32_t d1 = u >> 4, d2 = (uint32_t)__uint_as_float(v2);
-            if constexpr (kClamp) { d1 = umin(d1, dsat); d2 = umin(d2, dsat); }
-            k1 = (d1 << ib) | (uint32_t)(r0w + 16 * half) | (u & 15u);
-            k2 = d2 << ib;
-        };
-        auto rows4 = [&](int g) {
-            ins2x4(rb1[g], rb2[g], PRU(0, g), PRU(1, g), rb1[g + 1], rb2[g + 1], PRU(0, g + 1), PRU(1, g + 1),
-                   rb1[g + 2], rb2[g + 2], PRU(0, g + 2), PRU(1, g + 2), rb1[g + 3], rb2[g + 3], PRU(0, g + 3),
-                   PRU(1, g + 3));
-        };
-        // ---- E1
-        if (role == 3) copy_next();
-        uint32_t s1a = 0, s2a = 0;
-        if (rows_here) {
-            col_key(0, s1a, s2a);
-            rows4(0);
-        }
-        if (role == 0) copy_next();
-        phase_end(1);
-        // ---- E2
-        if (role == 2) copy_next();
-        uint32_t cm1 = 0, cm2 = 0, cold = 0;
-        uint32_t* c1s = colstate + work.slot * 2 * kmax64 + work.sc * kUnitCols + lane;
-        if (rows_here) {
-            uint32_t s1b, s2b;
-            col_key(1, s1b, s2b);
-            const auto x1 = __builtin_amdgcn_permlane32_swap(s1a, s1b, false, false);
-            const auto x2 = __builtin_amdgcn_permlane32_swap(s2a, s2b, false, false);
-            cm1 = umin(x1[0], x1[1]);
-            cm2 = med3u(x1[0], x1[1], umin(x2[0], x2[1]));
-            cold = __hip_atomic_fetch_min(c1s, cm1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            ins2x2(rb1[4], rb2[4], PRU(0, 4), PRU(1, 4), rb1[5], rb2[5], PRU(0, 5), PRU(1, 5));
-        }
-        phase_end(2);
-        // ---- E3
-        if (role == 1) copy_next();
-        if (rows_here) {
-            __hip_atomic_fetch_min(c1s + kmax64, umin(umax(cold, cm1), cm2), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            ins2x2(rb1[6], rb2[6], PRU(0, 6), PRU(1, 6), rb1[7], rb2[7], PRU(0, 7), PRU(1, 7));
-            rows4(8);
-            rows4(12);
-#undef PRU
-            if (work.sc == si.nsup - 1) {
-                // the pass is over for this pair: halving exchange over register bits 3..0 within each half-wave,
-                // then lanes l and l ^ 16 merge: lane (lrow, half) holds row r0w + 16 half + lrow % 16
-#pragma unroll
-                for (int d = 8; d >= 1; d >>= 1) {
-                    const bool up = (lrow & d) != 0;
-#pragma unroll
-                    for (int q = 0; q < d; ++q) {
-                        const uint32_t t1 = up ? rb1[q] : rb1[q + d], t2 = up ? rb2[q] : rb2[q + d];
-                        const uint32_t q1 = up ? rb1[q + d] : rb1[q], q2 = up ? rb2[q + d] : rb2[q];
-                        const uint32_t o1 = xor_swizzle(t1, d), o2 = xor_swizzle(t2, d);
-                        rb1[q] = umin(q1, o1);
-                        rb2[q] = med3u(q1, o1, umin(q2, o2));
-                        if ((q & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-                    }
-                }
-                {
-                    const uint32_t o1 = xor_swizzle(rb1[0], 16), o2 = xor_swizzle(rb2[0], 16);
-                    const uint32_t q1 = rb1[0], q2 = rb2[0];
-                    rb1[0] = umin(q1, o1);
-                    rb2[0] = med3u(q1, o1, umin(q2, o2));
-                }
-                const int key = r0w + 16 * half + (lrow & 15);
-                if (lrow < 16 && key < si.na) rowres[(size_t)si.pair * kmax + key] = make_uint2(rb1[0], rb2[0]);
-#pragma unroll
-                for (int g = 0; g < 16; ++g) rb1[g] = rb2[g] = kNoKey;
-            }
-        }
-        advance(work);
-        if constexpr (kStamp) t_start = st_post[3];
-        phase_end(3);
-        if constexpr (kStamp) {
-            unsigned long long prev = t_start;
-            for (int c = 0; c < 4; ++c) {
-                qs[2 * c] += st_pre[c] - prev;
-                qs[2 * c + 1] += st_post[c] - st_pre[c];
-                prev = st_post[c];
-            }
-        }
-    }
-    if constexpr (kStamp)
-        if (lane == 0)
-            for (int i = 0; i < 8; ++i) atomicAdd(&g_q_stamps[wave * 8 + i], qs[i]);
-    if (n_units > 0)
-        for (int q = role; q < 3; ++q) __syncthreads();  // trailing phases
-    __syncthreads();
-    for (int s = 0; s < G; ++s) {
-        const PpSlot si = slot_info(s);
-        if (si.pair < 0 || si.na == 0) continue;
-        const uint32_t* c1s = colstate + s * 2 * kmax64;
-        const uint32_t* c2s = c1s + kmax64;
-        for (int c = tid; c < si.nb; c += kRThreads) colres[(size_t)si.pair * kmax + c] = make_uint2(c1s[c], c2s[c]);
     }
 }
 
@@ -1568,52 +797,10 @@ int launch_pp_t(const _Float16* a_form, const _Float16* b_form, const int* count
     const int gs = groups ? group_size : 1;
     if (pp_lds_bytes<NK>(kmax, gs) > (size_t)kPpLdsBudget) return GTSFM_ERR_ARG;
     const size_t lds = pp_dyn_lds_bytes(kmax, gs);
-    static const bool use_pp = [] {  // experiment selector: GTSFM_MNN=r / rs / q<n> run the variants below
-        const char* e = getenv("GTSFM_MNN");
-        return !(e && (e[0] == 'q' || e[0] == 'r'));
-    }();
-    if (use_pp) {
-        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)mnn_pp_kernel<NK, kClamp>, (int)lds));
-        hipLaunchKernelGGL((mnn_pp_kernel<NK, kClamp>), dim3(n_groups), dim3(kPpThreads), lds, stream, a_form,
-                           b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax, pp_kmax64(kmax),
-                           ib, rowres, colres);
-    } else {
-        static const int var = [] {
-            const char* e = getenv("GTSFM_MNN");
-            if (e && e[0] == 'r' && e[1] == 's') return -2;
-            return e && e[0] == 'q' ? atoi(e + 1) : -1;
-        }();
-        auto go = [&](auto kern) -> int {
-            GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)kern, (int)lds));
-            hipLaunchKernelGGL(kern, dim3(n_groups), dim3(kQThreads), lds, stream, a_form, b_form, counts, pairs,
-                               n_pairs, groups, n_groups, group_size, kpad, kmax, pp_kmax64(kmax), ib, rowres, colres);
-            return GTSFM_OK;
-        };
-        int rc = GTSFM_OK;
-        if (var == -2) {  // diagnostic: per-wave phase stamps (tools/qstamps.py)
-            GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)mnn_r_kernel<NK, kClamp, true>, (int)lds));
-            hipLaunchKernelGGL((mnn_r_kernel<NK, kClamp, true>), dim3(n_groups), dim3(kRThreads), lds, stream, a_form,
-                               b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax,
-                               pp_kmax64(kmax), ib, rowres, colres);
-        } else if (var < 0) {
-            GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)mnn_r_kernel<NK, kClamp>, (int)lds));
-            hipLaunchKernelGGL((mnn_r_kernel<NK, kClamp>), dim3(n_groups), dim3(kRThreads), lds, stream, a_form,
-                               b_form, counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax,
-                               pp_kmax64(kmax), ib, rowres, colres);
-        } else if constexpr (NK == 9 && !kClamp) {
-            switch (var) {
-                case 1: rc = go(mnn_q_kernel<NK, kClamp, 1>); break;
-                case 2: rc = go(mnn_q_kernel<NK, kClamp, 2>); break;
-                case 3: rc = go(mnn_q_kernel<NK, kClamp, 3>); break;
-                case 4: rc = go(mnn_q_kernel<NK, kClamp, 4>); break;
-                case 5: rc = go(mnn_q_kernel<NK, kClamp, 5>); break;
-                default: rc = go(mnn_q_kernel<NK, kClamp, 0>); break;
-            }
-        } else {
-            rc = go(mnn_q_kernel<NK, kClamp, 0>);
-        }
-        if (rc != GTSFM_OK) return rc;
-    }
+    GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)mnn_pp_kernel<NK, kClamp>, (int)lds));
+    hipLaunchKernelGGL((mnn_pp_kernel<NK, kClamp>), dim3(n_groups), dim3(kPpThreads), lds, stream, a_form, b_form,
+                       counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax, pp_kmax64(kmax), ib, rowres,
+                       colres);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
 
@@ -1660,12 +847,6 @@ constexpr int kFlCand = 8;
 constexpr int kFlRows = 64;   // train rows per LDS chunk (two 32-row MFMA tiles)
 constexpr int kFlQ = 128;     // queries per workgroup: 4 waves x 32
 constexpr int kFlMaxDim = 256;
-#ifndef GTSFM_FL_XCD
-#define GTSFM_FL_XCD 1    // fl_shortlist_kernel's XCD-contiguous block order
-#endif
-#ifndef GTSFM_FL_DEPTH
-#define GTSFM_FL_DEPTH 2  // chunks of register prefetch in fl_shortlist_kernel (1 or 2; measured 535 / 524 ms)
-#endif
 
 
 __host__ __device__ inline int fl_dpad(int dim) { return dim <= 64 ? 64 : dim <= 128 ? 128 : 256; }
@@ -1760,7 +941,6 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     extern __shared__ __attribute__((aligned(16))) unsigned char fl_smem[];
     _Float16* tl = (_Float16*)fl_smem;                                  // [2][kFlRows * RS]
     float* nbl = (float*)(fl_smem + 2 * kFlRows * RS * sizeof(_Float16));  // [2][kFlRows]
-#if GTSFM_FL_XCD
     // 1-D grid, XCD-contiguous: the hardware deals consecutive workgroups to the 8 XCDs in turn, so workgroup b runs
     // logical block (b & 7) * per_xcd + (b >> 3); each XCD then walks whole (pair, side) groups of query blocks in
     // order and the group's train image is read into that XCD's L2 once, not by every XCD
@@ -1768,9 +948,6 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     const int lb = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
     if (lb >= total) return;
     const int qb = lb % n_qb, p = (lb / n_qb) % n_pairs, side = lb / (n_qb * n_pairs);
-#else
-    const int qb = blockIdx.x, p = blockIdx.y, side = blockIdx.z;
-#endif
     const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 5;
     const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
     const int nq = counts[iq], nt = counts[it];
@@ -1788,10 +965,6 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     const _Float16* tbase = form + (size_t)it * kpad * DP;
     const float* nbase = norm2 + (size_t)it * kpad;
     const int n_chunks = (nt + kFlRows - 1) / kFlRows;
-#ifndef GTSFM_FL_DIAG  // diagnostic builds only: 1 = no top-8 epilogue, 2 = no MFMA either (outputs are placeholders)
-#define GTSFM_FL_DIAG 0
-#endif
-    float dsum = 0.f;
     // one chunk: two 32-row MFMA tiles against the wave's 32 queries, then the top-8 epilogue per tile
     auto process = [&](int c, int buf) {
         const int c0 = c * kFlRows;
@@ -1800,17 +973,9 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
         for (int t = 0; t < 2; ++t) {
             fl_float16 acc = {};
             const _Float16* arow = tb + (t * 32 + (l & 31)) * RS + 8 * h;
-            if (GTSFM_FL_DIAG == 2) {
-                dsum += (float)arow[0] + (float)arow[16 * (NS - 1)];
-                continue;
-            }
 #pragma unroll
             for (int s = 0; s < NS; ++s)
                 acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(*(const fl_half8*)(arow + 16 * s), bq[s], acc, 0, 0, 0);
-            if (GTSFM_FL_DIAG == 1) {
-                dsum += acc[0] + acc[15];
-                continue;
-            }
             // the tile's 16 keys of this lane, a mask of those below the shortlist's current last key, then one
             // insert per wave iteration for every lane that still has a set bit, in index order: the same insertion
             // sequence as testing the keys one by one, but the wave runs max(popcount) inserts instead of one per
@@ -1841,7 +1006,6 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
             }
         }
     };
-#if GTSFM_FL_DEPTH == 2
     // register prefetch two chunks ahead (chunk c + 2 is loaded while chunk c is computed, chunk c + 1 waits in the
     // other register set and is stashed at the end of chunk c): each load has two chunks of work to land
     fl_u32x4 preA[NV], preB[NV];
@@ -1862,25 +1026,6 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
         process(c + 1, 1);
         if (c + 2 < n_chunks) fl_stash<NV, DP>(preA, pnA, tl, nbl, 0, tid);
         __syncthreads();
-    }
-#else
-    fl_u32x4 pre[NV];
-    float pn = 0.f;
-    if (n_chunks > 0) {
-        fl_fetch<NV, DP>(pre, pn, tbase, nbase, 0, tid);
-        fl_stash<NV, DP>(pre, pn, tl, nbl, 0, tid);
-    }
-    __syncthreads();
-    for (int c = 0; c < n_chunks; ++c) {
-        if (c + 1 < n_chunks) fl_fetch<NV, DP>(pre, pn, tbase, nbase, (c + 1) * kFlRows, tid);
-        process(c, c & 1);
-        if (c + 1 < n_chunks) fl_stash<NV, DP>(pre, pn, tl, nbl, (c & 1) ^ 1, tid);
-        __syncthreads();
-    }
-#endif
-    if (GTSFM_FL_DIAG != 0) {  // placeholders that certify: candidates 0..7 with an unreachable last key
-#pragma unroll
-        for (int c = 0; c < kFlCand; ++c) { v[c] = dsum == -1.2345f ? 0.f : 1e30f; id[c] = c; }
     }
     // merge the two halves of each query's shortlist
 #pragma unroll
@@ -2044,10 +1189,7 @@ __device__ __forceinline__ bool fl_both(const int* unc, const int* counts, const
 // state in colres with a returning 64-bit atomicMin on (d1 bits << 32 | row) (slots j1 | pad of the record) and a
 // 32-bit atomicMin of min(max(old d1, d1), d2) on d2 -- the exact top-2 in any arrival order, ties to the lowest row,
 // as the strict-'<' scan of that side. Distances are symmetric bit for bit ((a - b)^2 == (b - a)^2).
-#ifndef GTSFM_XK
-#define GTSFM_XK 16  // 16: the transposed tile stores hit 64 distinct banks (C3: 32 -> 16 took 8.09 -> 7.63 s of matching)
-#endif
-constexpr int kXT = 64, kXK = GTSFM_XK;
+constexpr int kXT = 64, kXK = 16;
 template <bool kBoth>
 __global__ __launch_bounds__(256) void fl_exact_tile_kernel(const float* __restrict__ desc,
                                                             const int* __restrict__ counts, int kmax, int dim,
@@ -2253,11 +1395,7 @@ int launch_fl_shortlist(const _Float16* form, const float* norm2, const int* cou
                         int kpad, int kmax, int* cand, float* tkey, hipStream_t stream) {
     const size_t lds = 2 * kFlRows * (NS * 16 + 8) * sizeof(_Float16) + 2 * kFlRows * sizeof(float);
     GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)fl_shortlist_kernel<NS>, (int)lds));
-#if GTSFM_FL_XCD
     const dim3 grid((unsigned)((kpad / kFlQ * (size_t)n_pairs * 2 + 7) / 8 * 8));
-#else
-    const dim3 grid(kpad / kFlQ, n_pairs, 2);
-#endif
     hipLaunchKernelGGL(fl_shortlist_kernel<NS>, grid, dim3(256), lds, stream, form, norm2,
                        counts, pairs, n_pairs, kpad, kmax, cand, tkey);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
@@ -2340,23 +1478,6 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
     return 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
 }
 
-#ifdef GTSFM_PP_STAMPS
-int gtsfm_pp_stamps(unsigned long long* out) {  // diagnostic builds: read and clear the per-wave cycle sums
-    GTSFM_CHECK_HIP(hipDeviceSynchronize());
-    GTSFM_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pp_stamps), sizeof(g_pp_stamps)));
-    static const unsigned long long zero[kPpWaves * 8] = {};
-    GTSFM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_pp_stamps), zero, sizeof(zero)));
-    return GTSFM_OK;
-}
-#endif
-
-int gtsfm_diag_mnn_q_stamps(unsigned long long* out) {  // diagnostic (GTSFM_MNN=q5): read and clear
-    GTSFM_CHECK_HIP(hipDeviceSynchronize());
-    GTSFM_CHECK_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_q_stamps), sizeof(g_q_stamps)));
-    static const unsigned long long zero[kQWaves * 8] = {};
-    GTSFM_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_q_stamps), zero, sizeof(zero)));
-    return GTSFM_OK;
-}
 
 int gtsfm_match_max_group(int kmax, int dim) {
     if (kmax <= 0 || kmax > kMaxKmaxPacked || dim <= 0 || dim > 139) return 0;

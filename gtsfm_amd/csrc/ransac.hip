@@ -174,10 +174,7 @@ __device__ __forceinline__ RootMem root_mem(unsigned char* smem, int lane) {
 // the padded row equals Horner from the row's true degree bit for bit (leading zeros contribute exact zeros), and
 // rows past the chain length evaluate to 0 and are skipped exactly like the oracle's loop bound.
 constexpr int kChain = 66;
-#ifndef GTSFM_ROOT_GROUP
-#define GTSFM_ROOT_GROUP 4  // root slots bisected / polished together (independent Horner chains)
-#endif
-constexpr int kRootGroup = GTSFM_ROOT_GROUP;
+constexpr int kRootGroup = 4;  // root slots bisected / polished together (independent Horner chains)
 __device__ __forceinline__ constexpr int row_off(int k) { return 11 * k - k * (k - 1) / 2; }
 
 __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], double x) {
@@ -1338,15 +1335,7 @@ __global__ __launch_bounds__(64, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         if (five_point_stage1(s1, s2, mem, part, N, Rt)) {
             ok = 1;
             double* out = stage + (size_t)p * kStageVals * kMaxHyp + hyp;
-#ifdef GTSFM_S1_NOSTORE  // timing experiment only: the stage stores replaced by one dependent store
-            double acc = 0.0;
-            for (int r = 0; r < 6; ++r) for (int j = 0; j < 10; ++j) acc += Rt[r][j];
-            for (int k = 0; k < 4; ++k) for (int j = 0; j < 9; ++j) acc += N[k][j];
-            if (acc == 12345.678) out[0] = acc;
-            if (false) {
-#else
             if (part) {
-#endif
 #pragma unroll
                 for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -1406,10 +1395,7 @@ __global__ __launch_bounds__(64, 2) void ransac_solve2_kernel(const int* __restr
 // all lanes finish, thread 0 walks the chunks in order exactly like the oracle's batch loop
 // (oracle/ransac.c:679-706): best = min(best, chunk minimum), the iteration bound from the best count, done += 64,
 // stop once done >= niters (chunks past that point were solved speculatively and are discarded).
-#ifndef GTSFM_SCORE_THREADS
-#define GTSFM_SCORE_THREADS 512  // measured 64 / 128 / 256 / 512: 11.9 / 9.1 / 7.8 / 7.4 ms C2 verify
-#endif
-constexpr int kScoreThreads = GTSFM_SCORE_THREADS;
+constexpr int kScoreThreads = 512;  // measured 64 / 128 / 256 / 512: 11.9 / 9.1 / 7.8 / 7.4 ms C2 verify
 constexpr int kMaxCand = kMaxHyp * kMaxSol;  // candidates one launch may hold per pair (13 bits of the key)
 static_assert(kMaxCand < (1 << 13), "flat candidate index must fit the key's 13 bits");
 constexpr int kKeyCountBits = 19;
@@ -1614,10 +1600,8 @@ __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* 
 }
 
 // Per pair: status, iterative LO from the best hypothesis, final mask, recoverPose.
-#ifndef GTSFM_REFINE_OCC
-#define GTSFM_REFINE_OCC 2  // two waves per SIMD (256 VGPRs, 22 spilled): 0.92 -> 0.73 ms per C2 step
-#endif
-__global__ __launch_bounds__(64, GTSFM_REFINE_OCC) void ransac_refine_kernel(const int* __restrict__ pairs,
+// two waves per SIMD (256 VGPRs, 22 spilled): 0.92 -> 0.73 ms per C2 step against one
+__global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restrict__ pairs,
                                                            const double* __restrict__ intr,
                                                            const int* __restrict__ match_count, int mcap,
                                                            const double2* __restrict__ x1n_all,

@@ -150,17 +150,8 @@ struct LevelTable {  // gauss levels 1..3 of every octave (descriptor stage)
 constexpr int kBlurTX = 64;
 // Tile height per radius: 64 rows x 4 waves, or for the wide kernels (and the upsampling one) 96 rows x 8 waves, where
 // the smaller row-pass halo share pays for the coarser tiling (measured per radius on octave 0).
-#ifndef GTSFM_BLUR_WIDE_R
-#define GTSFM_BLUR_WIDE_R 9
-#endif
-#ifndef GTSFM_BLUR_U8_TY
-#define GTSFM_BLUR_U8_TY 96
-#endif
-#ifndef GTSFM_BLUR_WIDE_TY
-#define GTSFM_BLUR_WIDE_TY 96
-#endif
 __host__ __device__ constexpr int blur_ty(int r, bool u8) {
-    return u8 ? GTSFM_BLUR_U8_TY : (r >= GTSFM_BLUR_WIDE_R ? GTSFM_BLUR_WIDE_TY : 64);
+    return u8 ? 96 : (r >= 9 ? 96 : 64);
 }
 __host__ __device__ constexpr int blur_tyt(int r, bool u8) { return blur_ty(r, u8) == 64 ? 4 : 8; }
 constexpr int kBlurRowOut = 8, kBlurRowThr = kBlurTX / kBlurRowOut;  // row pass: outputs per thread, threads per row
@@ -316,10 +307,7 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
     __syncthreads();
     // row pass: kBlurRowThr threads per row (consecutive lanes of one wave), kBlurRowOut consecutive outputs each,
     // written back in place at columns [g8, g8 + 8) (output column x sits at input column x + R)
-#ifndef GTSFM_BLUR_DIAG  // diagnostic builds only: bit 0 = no row pass, bit 1 = no column taps
-#define GTSFM_BLUR_DIAG 0
-#endif
-    for (int iy = tid / kBlurRowThr; iy < ((GTSFM_BLUR_DIAG & 1) ? 0 : IH); iy += kBlurTX * kBlurTYT / kBlurRowThr) {
+    for (int iy = tid / kBlurRowThr; iy < IH; iy += kBlurTX * kBlurTYT / kBlurRowThr) {
         const int g8 = (tid % kBlurRowThr) * kBlurRowOut;
         float* rowp = in + iy * IWP;
         // volatile 8-byte reads: the compiler would otherwise pair them into ds_read2_b64, which banks by 16-lane
@@ -366,7 +354,7 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
 #pragma unroll
     for (int h = 0; h < NP; ++h) acc[h] = pf2{k[0], k[0]} * pf2{c[R + 2 * h], c[R + 2 * h + 1]};
 #pragma unroll
-    for (int j = 1; j <= ((GTSFM_BLUR_DIAG & 2) ? 0 : R); ++j) {
+    for (int j = 1; j <= R; ++j) {
         pf2 sm[NP];
 #pragma unroll
         for (int h = 0; h < NP; ++h)
@@ -535,13 +523,7 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 // thousand): they are queued in LDS and their 3x3 blocks gathered after the sweep, all lanes at once. Each pixel's
 // levels 1..4 are read once (plus 2 halo rows per strip and 2 halo lanes per wave): 16 B per pixel instead of all six
 // levels' 24.
-#ifndef GTSFM_EX_STRIP
-#define GTSFM_EX_STRIP 64
-#endif
-#ifndef GTSFM_EX_WAVES
-#define GTSFM_EX_WAVES 4
-#endif
-constexpr int kExWaves = GTSFM_EX_WAVES, kExOut = 62, kExStrip = GTSFM_EX_STRIP;
+constexpr int kExWaves = 4, kExOut = 62, kExStrip = 64;
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
@@ -558,12 +540,6 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane l gets lane 
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
-#ifndef GTSFM_ORI_SCRAMBLE
-#define GTSFM_ORI_SCRAMBLE 1
-#endif
-#ifndef GTSFM_SIFT_FUSED_REFINE
-#define GTSFM_SIFT_FUSED_REFINE 1
-#endif
 __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int H, int W, Cand* __restrict__ cands,
                                                                 int* __restrict__ n_cand, int cap,
                                                                 uint32_t* __restrict__ seen, Refined* __restrict__ out,
@@ -598,15 +574,8 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
 #pragma unroll
         for (int l = 0; l < kInLv; ++l) g[l] = gl[l + 1][off];
     };
-#ifdef GTSFM_EX_DIAG  // diagnostic builds only: 1 = sweep without the row test, 2 = loads only
-    float dsum = 0.f;
-#endif
     auto finish = [&](const float (&g)[kInLv], auto slot) {
         constexpr int s = decltype(slot)::value;
-#if defined(GTSFM_EX_DIAG) && GTSFM_EX_DIAG == 2
-        dsum += (g[0] + g[1]) + (g[2] + g[3]);
-        return;
-#endif
 #pragma unroll
         for (int l = 0; l < kIn; ++l) {
             const float d = g[l + 1] - g[l];
@@ -646,12 +615,6 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     const float thr_up = __uint_as_float(__float_as_uint(threshold) + 1u);  // threshold >= 0
     auto test_row = [&](int y, auto slot) {
         constexpr int s = decltype(slot)::value;
-#ifdef GTSFM_EX_DIAG
-#if GTSFM_EX_DIAG == 1
-        dsum += (hmax[0][s] + hmin[0][s]) + (hmax[1][s] + hmin[1][s]) + (hmax[2][s] + hmin[2][s]) + ctr[1][s];
-#endif
-        return;
-#endif
         if (y < kBorder || y >= H - kBorder) return;
         float bmax[kIn], bmin[kIn];
 #pragma unroll
@@ -740,9 +703,6 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         fetch(min(y + 12, y_end), g6);
         test_row(y + 5, S0{});
     }
-#ifdef GTSFM_EX_DIAG
-    if (dsum == -1.2345f) n_out[0] = 0;
-#endif
     __syncthreads();
     // the queued layer-1 / layer-3 pixels: outer DoG level's 3x3 block, every lane gathering at once
     for (int i = threadIdx.x; i < min(n_pend, kExPend); i += 64 * kExWaves) {
@@ -770,7 +730,6 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     }
     __syncthreads();
     const int n = min(n_list, kExList);
-#if GTSFM_SIFT_FUSED_REFINE
     // refine the block's own candidates now, while the strip's Gaussian rows are still in L2 (a separate pass
     // re-fetched each candidate's 3x3x3 window from HBM)
     // (entries dealt round-robin to the waves: a short list keeps every wave busy on the dependent gathers)
@@ -780,16 +739,9 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         const bool keep = i < n && refine_one(list[i], G, H, W, seen, res);
         append_refined(keep, res, out, n_out, out_cap);
     }
-#else
-    if (threadIdx.x == 0) gbase = n ? atomicAdd(&n_cand[shard], n) : 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < n; i += 64 * kExWaves)
-        if (gbase + i < cap) cands[(size_t)shard * cap + gbase + i] = list[i];
-#endif
 }
 
-// Candidates left in the kCandShards global segments (extrema blocks whose LDS list overflowed; with
-// GTSFM_SIFT_FUSED_REFINE 0, all of them) are refined here.
+// Candidates left in the kCandShards global segments (extrema blocks whose LDS list overflowed) are refined here.
 __global__ __launch_bounds__(256) void refine_kernel(const Cand* __restrict__ cands,
                                                      const int* __restrict__ shard_counts, int cap, GaussSet G, int H,
                                                      int W, int n_img, uint32_t* __restrict__ seen,
@@ -816,13 +768,9 @@ __global__ __launch_bounds__(64) void orientation_kernel(const Refined* __restri
     for (int id = blockIdx.x; id < n_ref; id += gridDim.x) {
         if (lane < kOriBins) hist[lane] = 0ull;
         __syncthreads();
-#if GTSFM_ORI_SCRAMBLE
         // the refinement appends in extrema-block order (spatial clusters); a fixed bijective scramble spreads
         // concurrent waves over the image (2654435761 is prime, n_ref < 2^31)
         const Refined rf = refs[(int)(((unsigned long long)id * 2654435761ull) % (unsigned)n_ref)];
-#else
-        const Refined rf = refs[id];
-#endif
         const float size_oct = kSigma * exp2_det(((float)rf.layer + rf.xi) / kLayers);
         const float scl = size_oct;
         const int radius = (int)rintf(kOriRadius * scl);
@@ -1101,12 +1049,6 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __rest
 }
 
 // ------------------------------------------------------------------ descriptors: one wave per kept keypoint
-#ifndef GTSFM_DESC_SPREAD
-#define GTSFM_DESC_SPREAD 1
-#endif
-#ifndef GTSFM_DESC_COPIES
-#define GTSFM_DESC_COPIES 2
-#endif
 constexpr int kDescChunk = 512;
 
 __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict__ kps, int kp_cap,
@@ -1117,7 +1059,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
     constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
     // kCopies private histograms (lane & 1 picks one): adjacent samples usually land in the same bins, and same-address
     // LDS atomics of one instruction serialise. Integer (fixed-point) sums, so merging the copies is exact.
-    constexpr int kCopies = GTSFM_DESC_COPIES, HBP = HB + 1;  // +1: copies start on different banks
+    constexpr int kCopies = 2, HBP = HB + 1;  // +1: copies start on different banks
     __shared__ unsigned long long hist[kCopies * HBP];
     __shared__ int slist[kDescChunk];  // valid samples of the current chunk, (i << 16) | (j & 0xffff)
     __shared__ float dst[128];
@@ -1176,16 +1118,12 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
                 nv += __popcll(m);
             }
             __syncthreads();
-#if GTSFM_DESC_SPREAD
             // lane l takes the contiguous run [l nit, (l + 1) nit) of the chunk's samples: one instruction's 64 atomics
             // spread over the whole chunk's rows (and bins) instead of one or two raster rows
             const int nit = (nv + 63) >> 6;
             for (int it = 0; it < nit; ++it) {
             const int t = lane * nit + it;
             if (t >= nv) continue;
-#else
-            for (int t = lane; t < nv; t += 64) {
-#endif
             const int sv = slist[t];
             const int i = sv >> 16, j = (short)(sv & 0xffff);
             const float c_rot = j * cos_t - i * sin_t;
@@ -1446,7 +1384,7 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
                            (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref), counters + kCandShards,
                            B * kCandCapPerImg);
         // fused: only list overflows reach the shards, so one block per shard
-        hipLaunchKernelGGL(refine_kernel, dim3(GTSFM_SIFT_FUSED_REFINE ? kCandShards : 2048), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
+        hipLaunchKernelGGL(refine_kernel, dim3(kCandShards), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
                            shard_cap, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg);
         hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),

@@ -49,10 +49,7 @@ __host__ __device__ constexpr size_t sg_weights_floats(int n_layers) {
 
 // ------------------------------------------------------------------ batched GEMM on fp32 MFMA
 constexpr int kGemmThreads = 256;
-#ifndef GTSFM_SG_KC
-#define GTSFM_SG_KC 16
-#endif
-constexpr int kKc = GTSFM_SG_KC;  // K chunk staged in LDS (a multiple of 16; chunks past K are zero-filled)
+constexpr int kKc = 16;  // K chunk staged in LDS (a multiple of 16; chunks past K are zero-filled)
 static_assert(kKc % 16 == 0, "K chunk");
 
 struct GemmArgs {
@@ -166,10 +163,7 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
 constexpr int kAttnKeys = 64;
 constexpr int kKvStride = kHd + 1;
 
-#ifndef GTSFM_SG_ATT_OCC
-#define GTSFM_SG_ATT_OCC 3  // 168 VGPRs (4 spilled), 3 x 49.9 KB LDS per CU: C5 281 -> 315 pairs/s (r02m)
-#endif
-__global__ __launch_bounds__(256, GTSFM_SG_ATT_OCC) void sg_attention_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
+__global__ __launch_bounds__(256, 3) void sg_attention_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
                                                            const int* __restrict__ side_counts /*(2P)*/, int kmax,
                                                            int cross, float* __restrict__ out /*(2P, kmax, 256)*/) {
     __shared__ float Kc[kAttnKeys * kKvStride];
