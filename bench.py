@@ -82,6 +82,21 @@ def pmc_traffic():
     return float(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
 
 
+def deep_pmc(config: str):
+    """The latest committed per-kernel PMC summary of a deep config (profiles/*_<config>_pmc.json, written by
+    tools/gpu_pmc_deep.sh through tools/pmc_summary.py --kernels): HBM bytes per launch per kernel (FETCH_SIZE doubled +
+    WRITE_SIZE, as pmc_traffic) and the profiled step count. None when none is committed."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{config}_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    d["source"] = os.path.relpath(files[-1], REPO)
+    return d
+
+
 def cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, threads: int = 16, n_sift: int = 16,
                  n_pairs: int = 120) -> dict:
     """Oracle restatement (oracle/*.c through ctypes, which drops the GIL) timed on `threads` host threads -- the
@@ -318,20 +333,22 @@ def superglue_flop(k1: np.ndarray, k2: np.ndarray) -> np.ndarray:
     return lin + quad
 
 
-def deep_weights(dev, superglue: bool):
+def deep_weights(dev, superglue: bool, head=True):
     """Seeded random SuperPoint / SuperGlue weights in the ABI's packed layout (the pretrained .pth files are not
     available offline; tests/superpoint_weights.py builds state dicts of the reference architectures). SuperPoint's
     1x1 descriptor layer is the whitening of its seeded encoder's activations over the benchmark scene
     (tests/golden/make_superpoint_whitening.py), so descriptors of the scene behave like trained ones (unrelated
     keypoints near-orthogonal, repeated points similar); SuperGlue's final projection gain is 24 (see
     superglue_state_dict), which gives ~1000 matches on adjacent views. Weights change what is matched, never how
-    much work a step does."""
+    much work a step does. C3 (TwoWayMatcher: mutual NN + ratio test, no context) uses the head fitted to its strafe
+    scene, head="c3" (32 leading principal directions whitened, the rest at a quarter weight: ~185 putatives per
+    pair, 95 % of the pairs verified)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from superpoint_weights import superglue_state_dict, superpoint_state_dict
 
     from gtsfm_amd.frontend.detector_descriptor.superpoint import pack_superpoint_weights
 
-    sd = superpoint_state_dict(0, whitened=True)
+    sd = superpoint_state_dict(0, whitened=head)
     sp = torch.from_numpy(pack_superpoint_weights(sd)).to(dev)
     if not superglue:
         return sd, sp, None, None
@@ -342,12 +359,14 @@ def deep_weights(dev, superglue: bool):
 
 
 def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_sd, sg_sd, threads: int = 16,
-                      n_img_sample: int = 3) -> dict:
+                      n_img_sample: int = 5) -> dict:
     """CPU restatement of the deep front-end timed on `threads` host threads over a bounded sample, scaled to n_img
     images / all their pairs: oracle/deep.py's SuperPoint (torch fp32 on the host, `threads` intra-op threads, as the
     reference's torch modules run on a CPU) on n_img_sample images spread over the scene, then for every pair among
-    them the matcher (oracle/deep.py SuperGlue, or the oracle TwoWayMatcher in C on the float descriptors) and the
-    oracle 5-point RANSAC."""
+    them the matcher (oracle/deep.py SuperGlue with `threads` intra-op threads, pair after pair; or the oracle
+    TwoWayMatcher in C on the float descriptors, `threads` pairs at once) and the oracle 5-point RANSAC."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import deep, oracle
 
     sample = sample_images(n_img, n_img_sample)
@@ -360,8 +379,8 @@ def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_
     t_img = (time.time() - t0) / len(imgs)
     pairs = [(a, b) for a in range(len(sample)) for b in range(a + 1, len(sample))]
     K = np.asarray(intrinsics, dtype=np.float64)
-    t0 = time.time()
-    for a, b in pairs:
+    def pair_one(ab):
+        a, b = ab
         (k1, s1, d1), (k2, s2, d2) = feats[a], feats[b]
         if sg_sd is not None:
             hw = imgs[a].shape[:2]
@@ -375,6 +394,14 @@ def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_
             x1 = (k1[m[:, 0]].astype(np.float64) - f1[1:3]) / f1[0]
             x2 = (k2[m[:, 1]].astype(np.float64) - f2[1:3]) / f2[0]
             oracle.ransac_E(x1, x2, THRESH_PX / max(f1[0], f2[0]))
+
+    t0 = time.time()
+    if sg_sd is not None:  # torch on `threads` intra-op threads
+        for ab in pairs:
+            pair_one(ab)
+    else:  # the C matcher / RANSAC drop the GIL: `threads` pairs at once
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(pair_one, pairs))
     t_pair = (time.time() - t0) / len(pairs)
     P = n_img * (n_img - 1) // 2
     total = n_img * t_img + P * t_pair
@@ -382,7 +409,7 @@ def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_
     return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port",
             "sample": f"CPU restatement on {threads} threads: SuperPoint (oracle/deep.py, torch fp32) of "
                       f"{len(sample)} of the {n_img} images ({t_img:.2f} s/img), {what} + oracle RANSAC on the "
-                      f"{len(pairs)} pairs among them ({t_pair:.2f} s/pair), scaled to {n_img} images / {P} pairs"}
+                      f"{len(pairs)} pairs among them ({t_pair:.2f} s/pair wall), scaled to {n_img} images / {P} pairs"}
 
 
 def main_frontend(args, info, config: str):
@@ -422,14 +449,15 @@ def main_frontend(args, info, config: str):
         kpts = args.kpts if not (config == "c3" and args.kpts == 2048) else 4096
         mine = sharding.local_images(n_img, world, rank)
         # every rank renders (seeded, identical cameras) only the images it extracts; rendering is data generation
-        scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine)
+        scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine,
+                                       path="strafe" if config == "c3" else "orbit")
         host_images = scene.images.cpu().pin_memory()
         intrinsics = scene.intrinsics
         del scene.images
         torch.cuda.empty_cache()
         baseline_images = None
         if want_baseline:
-            baseline_images = host_images.numpy()[sample_images(n_img, 3 if deep else 16)]
+            baseline_images = host_images.numpy()[sample_images(n_img, 5 if deep else 16)]
     cfg = FrontEndConfig(kpts=kpts, ratio=RATIO, thresh_px=THRESH_PX, min_inliers=MIN_INLIERS,
                          min_inlier_ratio=MIN_INLIER_RATIO)
     if deep:
@@ -445,7 +473,7 @@ def main_frontend(args, info, config: str):
     cfg.bundle_adjust = args.ba
     kernels = sp_sd = sg_sd = None
     if deep:
-        sp_sd, sp_w, sg_sd, sg_w = deep_weights(dev, config == "c5")
+        sp_sd, sp_w, sg_sd, sg_w = deep_weights(dev, config == "c5", head=True if config == "c5" else "c3")
         kernels = HipSuperPointKernels(sp_w, "superglue" if config == "c5" else "twoway", sg_w)
     fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg, kernels=kernels)
 
@@ -556,7 +584,14 @@ def main_frontend(args, info, config: str):
                                    "stage (GEMMs, attention, Sinkhorn) timed together" % len(pr)}
             roof = dict(match_stage)
             roof["kernel"] = "SuperGlue stage (sg_gemm / sg_attention / Sinkhorn kernels), HIP events on its stream"
-            roof["traffic"] = None
+            pmc = deep_pmc("c5")
+            roof["traffic"] = round(pmc["hbm_bytes_per_step"]) if pmc else None
+            if pmc:
+                roof["traffic_source"] = pmc["source"]
+                roof["traffic_note"] = ("HBM bytes per step of the SuperGlue stage's kernels (FETCH_SIZE x 2 + "
+                                        "WRITE_SIZE, separate --pmc passes); per launch: " + ", ".join(
+                                            f"{k} {v['hbm_bytes_per_launch'] / 1e6:.1f} MB x {v['launches']}"
+                                            for k, v in pmc["kernels"].items()))
         else:
             match_stage = {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS,
                            "unit": "TFLOP/s", "frac": round(gemm_tf / MFMA_F16_PEAK_TFLOPS, 4),
@@ -565,7 +600,15 @@ def main_frontend(args, info, config: str):
                                    "computes the matrix once per side: 2x this)" % len(pl)}
             roof = dict(match_stage)
             roof["kernel"] = "fl_shortlist_kernel (F16_RERANK fp16 MFMA shortlist; one launch per pair chunk)"
-            roof["traffic"] = None
+            pmc = deep_pmc("c3")
+            ks = pmc["kernels"].get("fl_shortlist_kernel") if pmc else None
+            roof["traffic"] = round(ks["hbm_bytes_per_launch"]) if ks else None
+            if ks:
+                roof["traffic_source"] = pmc["source"]
+                roof["traffic_note"] = ("HBM bytes per fl_shortlist_kernel launch (FETCH_SIZE x 2 + WRITE_SIZE, "
+                                        "separate --pmc passes); also per launch: " + ", ".join(
+                                            f"{k} {v['hbm_bytes_per_launch'] / 1e6:.1f} MB x {v['launches']}"
+                                            for k, v in pmc["kernels"].items() if k != "fl_shortlist_kernel"))
         roof["stages"] = {"extract": ex_stage, "match": match_stage, "verify": verify_stage}
     wl = {"c1": "C1", "c4": "C4", "c3": "C3", "c5": "C5 slice"}.get(config, "C2")
     if deep:
@@ -574,8 +617,9 @@ def main_frontend(args, info, config: str):
                    f"TwoWayMatcher ratio {RATIO} (F16_RERANK)") + f", 5-pt RANSAC {THRESH_PX}px + inlier support")
         dtype = ("u8 image / fp32-MFMA SuperPoint / " + ("fp32-MFMA SuperGlue" if config == "c5" else
                  "fp16-MFMA shortlist + fp32 exact re-rank") + " / fp64 RANSAC solver")
-        data = ("synthetic (rendered textured room, seeds 0/1/2); seeded random network weights with a whitened "
-                "SuperPoint descriptor head (tests/golden/make_superpoint_whitening.py)")
+        data = ("synthetic (rendered textured room, seeds 0/1/2" + ("; 1 m strafe path" if config == "c3" else "")
+                + "); seeded random network weights with a whitened SuperPoint descriptor head "
+                "(tests/golden/make_superpoint_whitening.py" + (" --c3" if config == "c3" else "") + ")")
     else:
         desc = (f"{wl}: {n_img} {'Lund Door' if config == 'c1' else 'synthetic'} {W}x{H} images, all "
                 f"{fe.total_pairs} pairs, SIFT {kpts} kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px"

@@ -89,9 +89,16 @@ def _room_planes() -> List[Tuple]:
 
 def render_scene(n_images: int = 100, height: int = 1080, width: int = 1920, seed_scene: int = 0,
                  seed_cameras: int = 1, seed_texture: int = 2, device: str = "cuda",
-                 tex_size: int = 2048, indices: Optional[Sequence[int]] = None) -> SyntheticScene:
+                 tex_size: int = 2048, indices: Optional[Sequence[int]] = None,
+                 path: str = "orbit") -> SyntheticScene:
     """Renders the scene's cameras `indices` (default: all n_images); `images` holds them in that order, while K,
-    wRc and wtc always describe all n_images cameras (a rank renders only the images it extracts)."""
+    wRc and wtc always describe all n_images cameras (a rank renders only the images it extracts).
+
+    path "orbit" (default; configs C2 / C4): the cameras on a jittered circle around the room, looking inwards.
+    path "strafe" (config C3): the cameras on a jittered 1 m line 7.5 m in front of the room's centre, all looking at
+    the far wall 17.5 m away (the boxes in between give parallax): every pair of views overlaps by > 90 % with a mostly
+    translational image motion, the regime in which descriptors of a network without trained invariances (the seeded
+    random SuperPoint weights) repeat."""
     dev = torch.device(device)
     indices = list(range(n_images)) if indices is None else [int(i) for i in indices]
     tex = make_texture(tex_size, seed_texture, "cpu").to(dev)[None, None]
@@ -108,11 +115,17 @@ def render_scene(n_images: int = 100, height: int = 1080, width: int = 1920, see
     f = 1.2 * max(width, height)
     K = np.array([[f, 0, width / 2.0], [0, f, height / 2.0], [0, 0, 1.0]])
     wRc, wtc = [], []
+    assert path in ("orbit", "strafe"), path
     for i in range(n_images):
-        ang = 2 * math.pi * i / n_images + rng_c.normal(0, 0.02)
-        rad = 7.5 + rng_c.normal(0, 0.3)
-        center = np.array([rad * math.cos(ang), rad * math.sin(ang), 1.6 + rng_c.normal(0, 0.2)])
-        target = np.array([0.0, 0.0, 0.8]) + rng_c.normal(0, 0.5, 3) * np.array([1, 1, 0.3])
+        if path == "orbit":
+            ang = 2 * math.pi * i / n_images + rng_c.normal(0, 0.02)
+            rad = 7.5 + rng_c.normal(0, 0.3)
+            center = np.array([rad * math.cos(ang), rad * math.sin(ang), 1.6 + rng_c.normal(0, 0.2)])
+            target = np.array([0.0, 0.0, 0.8]) + rng_c.normal(0, 0.5, 3) * np.array([1, 1, 0.3])
+        else:
+            s_i = -0.5 + 1.0 * i / max(n_images - 1, 1)
+            center = np.array([s_i + rng_c.normal(0, 0.01), -7.5 + rng_c.normal(0, 0.05), 1.6 + rng_c.normal(0, 0.05)])
+            target = center + np.array([0.0, 17.5, -0.6]) + rng_c.normal(0, 0.05, 3)
         wRc.append(_look_at(center, target))
         wtc.append(center)
     wRc = np.stack(wRc)

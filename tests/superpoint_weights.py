@@ -17,14 +17,17 @@ SUPERPOINT_LAYERS = [  # (name, cin, cout, kernel) in the reference module's ord
 
 
 WHITENED_CONVDB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "superpoint_w0_convDb_whitened.npz")
+C3_CONVDB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "superpoint_w0_convDb_pca32_strafe.npz")
 
 
-def superpoint_state_dict(seed: int = 0, whitened: bool = False) -> dict:
+def superpoint_state_dict(seed: int = 0, whitened=False) -> dict:
     """name.weight (cout, cin, k, k) float32 and name.bias (cout,) float32 for every SuperPoint conv.
 
     whitened=True (seed 0 only): convDb replaced by the ZCA whitening of convDa's activations over the benchmark
     scene (tests/golden/make_superpoint_whitening.py), so that descriptors of unrelated keypoints are decorrelated
-    and repeated scene points match -- the descriptor statistics the matchers see with trained weights."""
+    and repeated scene points match -- the descriptor statistics the matchers see with trained weights.
+    whitened="c3": the head fitted for config C3's strafe scene (32 leading principal directions whitened, the rest
+    at a quarter weight)."""
     rng = np.random.default_rng(seed)
     sd = {}
     for name, cin, cout, k in SUPERPOINT_LAYERS:
@@ -33,7 +36,7 @@ def superpoint_state_dict(seed: int = 0, whitened: bool = False) -> dict:
         sd[f"{name}.bias"] = rng.uniform(-0.05, 0.05, size=cout).astype(np.float32)
     if whitened:
         assert seed == 0, "the whitened head is fitted to the seed-0 encoder"
-        with np.load(WHITENED_CONVDB) as z:
+        with np.load(C3_CONVDB if whitened == "c3" else WHITENED_CONVDB) as z:
             sd["convDb.weight"] = np.ascontiguousarray(z["weight"], dtype=np.float32)
             sd["convDb.bias"] = np.ascontiguousarray(z["bias"], dtype=np.float32)
     return sd
