@@ -150,7 +150,7 @@ __device__ void pose_log(const Pose& T, double* xi) {
 // ------------------------------------------------------------------ relative-pose prior (oracle/ba2.c between_t)
 // BetweenFactorPose3(X0, X1, m = i2Ti1_prior^-1, Diagonal.Sigmas) (bundle_adjustment.py:136-152): whitened
 // e = Logmap(m^-1 X0^-1 X1) / sigma; d e / d X1 = Jr^-1(e), d e / d X0 = -Jr^-1(e) Ad(hx^-1), hx = X0^-1 X1, with
-// Jr^-1(e) = I + ad(e) / 2 + ad(e)^2 / 12. Same operations as the oracle; computed redundantly by every lane.
+// the closed-form Jr^-1 of se3_jr_inv. Same operations as the oracle; computed redundantly by every lane.
 struct Between {
     bool on;
     Pose minv;       // the prior's value i2Ti1 (= m^-1)
@@ -192,27 +192,61 @@ __device__ double between_error(const Between& f, const Pose* X) {
     return 0.5 * s;
 }
 
+// exact inverse right Jacobian of SE(3) at e = (w, v), rotation first (GTSAM Pose3::LogmapDerivative):
+// Jr(e) = [[Jw, 0], [Q, Jw]] so Jr^-1 = [[A, 0], [-A Q A, A]] with A = Jw^-1 = I + W/2 + c W^2,
+// c = 1/th^2 - 1/(2 th tan(th/2)), and Q the right-Jacobian coupling block (Barfoot & Furgale 2014, eq. 102,
+// evaluated at -e): Q = -P/2 + c1 (WP + PW - WPW) - c2 (WWP + PWW - 3 WPW) + c3 (WPWW + WWPW), W = w^, P = v^,
+// c1 = (th - sin th) / th^3, c2 = (th^2 + 2 cos th - 2) / (2 th^4), c3 = (2 th - 3 sin th + th cos th) / (2 th^5);
+// below th = 1e-2 the coefficients use their Taylor series to th^2.
+__device__ void se3_jr_inv(const double* e, double* Ji) {
+    const double* w = e;
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double c, c1, c2, c3;
+    if (th2 < 1e-4) {
+        c = 1.0 / 12.0 + th2 / 720.0;
+        c1 = 1.0 / 6.0 - th2 / 120.0;
+        c2 = 1.0 / 24.0 - th2 / 720.0;
+        c3 = 1.0 / 120.0 - th2 / 2520.0;
+    } else {
+        const double th = sqrt(th2), s = sin(th), co = cos(th);
+        c = 1.0 / th2 - 1.0 / (2.0 * th * tan(0.5 * th));
+        c1 = (th - s) / (th2 * th);
+        c2 = (th2 + 2.0 * co - 2.0) / (2.0 * th2 * th2);
+        c3 = (2.0 * th - 3.0 * s + th * co) / (2.0 * th2 * th2 * th);
+    }
+    double W[9], P[9], W2[9], WP[9], PW[9], WPW[9], W2P[9], PW2[9], WPW2[9], W2PW[9], A[9], Q[9], AQ[9], B[9];
+    skew3(w, W);
+    skew3(e + 3, P);
+    mm3(W, W, W2);
+    mm3(W, P, WP);
+    mm3(P, W, PW);
+    mm3(WP, W, WPW);
+    mm3(W, WP, W2P);
+    mm3(PW, W, PW2);
+    mm3(WPW, W, WPW2);
+    mm3(W, WPW, W2PW);
+    for (int k = 0; k < 9; ++k) {
+        A[k] = (k % 4 == 0 ? 1.0 : 0.0) + 0.5 * W[k] + c * W2[k];
+        Q[k] = -0.5 * P[k] + c1 * (WP[k] + PW[k] - WPW[k]) - c2 * (W2P[k] + PW2[k] - 3.0 * WPW[k]) +
+               c3 * (WPW2[k] + W2PW[k]);
+    }
+    mm3(A, Q, AQ);
+    mm3(AQ, A, B);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Ji[6 * i + j] = A[3 * i + j];
+            Ji[6 * i + 3 + j] = 0.0;
+            Ji[6 * (3 + i) + j] = -B[3 * i + j];
+            Ji[6 * (3 + i) + 3 + j] = A[3 * i + j];
+        }
+}
+
 __device__ void between_linearize(const Between& f, const Pose* X, double* r, double* J) {
     double e[6];
     Pose hx, hi;
     between_residual(f, X, e, hx);
-    double ad[36], Ji[36], Ad[36];
-    for (int k = 0; k < 36; ++k) ad[k] = 0.0;
-    double Ws[9], Vs[9];
-    skew3(e, Ws);
-    skew3(e + 3, Vs);
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            ad[6 * i + j] = Ws[3 * i + j];
-            ad[6 * (3 + i) + j] = Vs[3 * i + j];
-            ad[6 * (3 + i) + 3 + j] = Ws[3 * i + j];
-        }
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 6; ++j) {
-            double a = 0;
-            for (int k = 0; k < 6; ++k) a += ad[6 * i + k] * ad[6 * k + j];
-            Ji[6 * i + j] = (i == j ? 1.0 : 0.0) + 0.5 * ad[6 * i + j] + a / 12.0;
-        }
+    double Ji[36], Ad[36];
+    se3_jr_inv(e, Ji);
     pose_inv(hx, hi);
     for (int k = 0; k < 36; ++k) Ad[k] = 0.0;
     double T[9], TR[9];

@@ -156,8 +156,8 @@ static void pose_log(const pose_t* T, double* xi) {
  * BetweenFactorPose3(X0, X1, m, Diagonal.Sigmas(sigmas)) with m = i2Ti1_prior.value.inverse()
  * (bundle_adjustment.py:136-152; two_view_estimator.py:165,192 passes the prior). GTSAM's error is
  * e = Pose3::Logmap(m^-1 * X0^-1 * X1) (Local of the Expmap chart), whitened by 1 / sigma. With X_c <- X_c Exp(d_c):
- * de/dd1 = Jr^-1(e), de/dd0 = -Jr^-1(e) Ad(hx^-1), hx = X0^-1 X1; Jr^-1(e) is taken to second order,
- * I + ad(e) / 2 + ad(e)^2 / 12 (exact to O(|e|^4)); ad((w, v)) = [[w^, 0], [v^, w^]], Ad((R, t)) = [[R, 0], [t^ R, R]]. */
+ * de/dd1 = Jr^-1(e), de/dd0 = -Jr^-1(e) Ad(hx^-1), hx = X0^-1 X1, with the closed-form Jr^-1 of se3_jr_inv
+ * (GTSAM's BetweenFactor H1/H2 through Pose3::LogmapDerivative); Ad((R, t)) = [[R, 0], [t^ R, R]]. */
 typedef struct {
     int on;
     pose_t minv;    /* m^-1 = i2Ti1_prior (the prior's value itself) */
@@ -200,29 +200,62 @@ static double between_error(const between_t* f, const pose_t* X) {
     return 0.5 * s;
 }
 
+/* exact inverse right Jacobian of SE(3) at e = (w, v), rotation first (GTSAM Pose3::LogmapDerivative):
+ * Jr(e) = [[Jw, 0], [Q, Jw]] so Jr^-1 = [[A, 0], [-A Q A, A]] with A = Jw^-1 = I + W/2 + c W^2,
+ * c = 1/th^2 - 1/(2 th tan(th/2)), and Q the right-Jacobian coupling block (Barfoot & Furgale 2014, eq. 102,
+ * evaluated at -e): Q = -P/2 + c1 (WP + PW - WPW) - c2 (WWP + PWW - 3 WPW) + c3 (WPWW + WWPW), W = w^, P = v^,
+ * c1 = (th - sin th) / th^3, c2 = (th^2 + 2 cos th - 2) / (2 th^4), c3 = (2 th - 3 sin th + th cos th) / (2 th^5);
+ * below th = 1e-2 the coefficients use their Taylor series to th^2. */
+static void se3_jr_inv(const double* e, double* Ji) {
+    const double* w = e;
+    const double th2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double c, c1, c2, c3;
+    if (th2 < 1e-4) {
+        c = 1.0 / 12.0 + th2 / 720.0;
+        c1 = 1.0 / 6.0 - th2 / 120.0;
+        c2 = 1.0 / 24.0 - th2 / 720.0;
+        c3 = 1.0 / 120.0 - th2 / 2520.0;
+    } else {
+        const double th = sqrt(th2), s = sin(th), co = cos(th);
+        c = 1.0 / th2 - 1.0 / (2.0 * th * tan(0.5 * th));
+        c1 = (th - s) / (th2 * th);
+        c2 = (th2 + 2.0 * co - 2.0) / (2.0 * th2 * th2);
+        c3 = (2.0 * th - 3.0 * s + th * co) / (2.0 * th2 * th2 * th);
+    }
+    double W[9], P[9], W2[9], WP[9], PW[9], WPW[9], W2P[9], PW2[9], WPW2[9], W2PW[9], A[9], Q[9], AQ[9], B[9];
+    skew3(w, W);
+    skew3(e + 3, P);
+    mm3(W, W, W2);
+    mm3(W, P, WP);
+    mm3(P, W, PW);
+    mm3(WP, W, WPW);
+    mm3(W, WP, W2P);
+    mm3(PW, W, PW2);
+    mm3(WPW, W, WPW2);
+    mm3(W, WPW, W2PW);
+    for (int k = 0; k < 9; ++k) {
+        A[k] = (k % 4 == 0 ? 1.0 : 0.0) + 0.5 * W[k] + c * W2[k];
+        Q[k] = -0.5 * P[k] + c1 * (WP[k] + PW[k] - WPW[k]) - c2 * (W2P[k] + PW2[k] - 3.0 * WPW[k]) +
+               c3 * (WPW2[k] + W2PW[k]);
+    }
+    mm3(A, Q, AQ);
+    mm3(AQ, A, B);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            Ji[6 * i + j] = A[3 * i + j];
+            Ji[6 * i + 3 + j] = 0.0;
+            Ji[6 * (3 + i) + j] = -B[3 * i + j];
+            Ji[6 * (3 + i) + 3 + j] = A[3 * i + j];
+        }
+}
+
 /* whitened residual r (6) and Jacobian J (6 x 12, columns: X0 then X1) at X */
 static void between_linearize(const between_t* f, const pose_t* X, double* r, double* J) {
     double e[6];
     pose_t hx, hi;
     between_residual(f, X, e, &hx);
-    double ad[36], ad2[36], Ji[36], Ad[36];
-    memset(ad, 0, sizeof(ad));
-    double Ws[9], Vs[9];
-    skew3(e, Ws);
-    skew3(e + 3, Vs);
-    for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-            ad[6 * i + j] = Ws[3 * i + j];
-            ad[6 * (3 + i) + j] = Vs[3 * i + j];
-            ad[6 * (3 + i) + 3 + j] = Ws[3 * i + j];
-        }
-    for (int i = 0; i < 6; ++i)
-        for (int j = 0; j < 6; ++j) {
-            double a = 0;
-            for (int k = 0; k < 6; ++k) a += ad[6 * i + k] * ad[6 * k + j];
-            ad2[6 * i + j] = a;
-        }
-    for (int k = 0; k < 36; ++k) Ji[k] = (k % 7 == 0 ? 1.0 : 0.0) + 0.5 * ad[k] + ad2[k] / 12.0;
+    double Ji[36], Ad[36];
+    se3_jr_inv(e, Ji);
     pose_inv(&hx, &hi);
     memset(Ad, 0, sizeof(Ad));
     double T[9], TR[9];
@@ -546,6 +579,35 @@ static void linearize_point(const pose_t* X, const double* K1, const double* K2,
 /* Returns 0 (BA ran, >= 1 valid track), 1 (no triangulated track), 2 (no track valid after the 0.5 px filter).
  * R_in / t_in: i2Ri1 and the unit i2ti1 of the verifier. R_out / t_out: i2Ri1 and unit i2ti1 after BA (the input
  * pose for statuses 1 and 2). valid[j]: correspondence j survives triangulation + BA + filtering. */
+/* test hook: the between factor (prior value prior_Rt = [R | t] row-major 3x4, isig 6) at cameras X = [R0 | t0, R1 | t1]
+ * (2 x 12) each retracted by d (12, may be NULL): whitened residual r (6) and, when J != NULL, its Jacobian (6 x 12) */
+void oracle_between_eval(const double* prior_Rt, const double* isig, const double* Xrt, const double* d, double* r,
+                         double* J) {
+    between_t f;
+    f.on = 1;
+    for (int i = 0; i < 3; ++i) {
+        for (int j = 0; j < 3; ++j) f.minv.R[3 * i + j] = prior_Rt[4 * i + j];
+        f.minv.t[i] = prior_Rt[4 * i + 3];
+    }
+    for (int k = 0; k < 6; ++k) f.isig[k] = isig[k];
+    pose_t X[2];
+    for (int c = 0; c < 2; ++c) {
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) X[c].R[3 * i + j] = Xrt[12 * c + 4 * i + j];
+            X[c].t[i] = Xrt[12 * c + 4 * i + 3];
+        }
+        if (d) pose_retract(&X[c], d + 6 * c, &X[c]);
+    }
+    if (J) {
+        between_linearize(&f, X, r, J);
+    } else {
+        double e[6];
+        pose_t hx;
+        between_residual(&f, X, e, &hx);
+        for (int k = 0; k < 6; ++k) r[k] = e[k] * f.isig[k];
+    }
+}
+
 int oracle_ba2(const double* uv1, const double* uv2, int n, const double* K1, const double* K2, const double* R_in,
                const double* t_in, int max_iters, double reproj_thresh, double tri_thresh, const double* prior_Rt,
                const double* prior_sigmas, double* R_out, double* t_out, uint8_t* valid, int* iters_out,

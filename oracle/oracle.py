@@ -67,6 +67,8 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_ba2.argtypes = [_f64p, _f64p, ctypes.c_int, _f64p, _f64p, _f64p, _f64p, ctypes.c_int, ctypes.c_double,
                                  ctypes.c_double, ctypes.c_void_p, ctypes.c_void_p, _f64p, _f64p, _u8p,
                                  ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
+        l.oracle_between_eval.restype = None
+        l.oracle_between_eval.argtypes = [_f64p, _f64p, _f64p, ctypes.c_void_p, _f64p, ctypes.c_void_p]
     if hasattr(l, "oracle_ransac_F"):
         l.oracle_ransac_F.restype = ctypes.c_int
         l.oracle_ransac_F.argtypes = [_f32p, _f32p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
