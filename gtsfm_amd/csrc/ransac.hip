@@ -41,6 +41,11 @@ __device__ unsigned long long g_rprof[32];
 #define RPROF_COUNT(k, v) do { } while (0)
 #endif
 
+// The essential-matrix path is compiled without FMA contraction: every fused multiply-add below is an explicit fma()
+// that oracle/ransac.c performs in the same place, so the solver, the refits and recoverPose reproduce the oracle's
+// double arithmetic bit for bit (hypotheses, candidates, scores, the selected model, R and t).
+#pragma clang fp contract(off)
+
 namespace {
 
 constexpr int kBatch = 64;      // hypotheses per chunk: the iteration bound is re-evaluated after each chunk
@@ -87,14 +92,14 @@ __device__ __forceinline__ void mul_ll(const double* a, const double* b, double*
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] += a[i] * b[j];
+        for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] = fma(a[i], b[j], q[kLL2Q[i][j]]);
 }
 
 __device__ __forceinline__ void addmul_ql(const double* q, const double* l, double s, double* c) {
 #pragma unroll
     for (int i = 0; i < 10; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += s * (q[i] * l[j]);
+        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = fma(s, q[i] * l[j], c[kQL2C[i][j]]);
 }
 
 // ------------------------------------------------------------------ lane-private arrays in LDS
@@ -128,7 +133,7 @@ struct LaneArr {
 
 __device__ __forceinline__ double peval(LaneArr<double> p, int deg, double x) {
     double v = p[deg];
-    for (int i = deg - 1; i >= 0; --i) v = v * x + p[i];
+    for (int i = deg - 1; i >= 0; --i) v = fma(v, x, p[i]);
     return v;
 }
 
@@ -137,7 +142,7 @@ __device__ int prem(LaneArr<double> a, int da, LaneArr<double> b, int db, LaneAr
     for (int i = 0; i <= da; ++i) t[i] = a[i];
     for (int k = da; k >= db; --k) {
         const double f = t[k] / b[db];
-        for (int i = 0; i <= db; ++i) t[k - db + i] -= f * b[i];
+        for (int i = 0; i <= db; ++i) t[k - db + i] = fma(-f, b[i], t[k - db + i]);
         t[k] = 0.0;
     }
     int dr = db - 1;
@@ -184,7 +189,7 @@ __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], doubl
         const int len = 11 - k, o = row_off(k);
         double a = R[o + len - 1];
 #pragma unroll
-        for (int i = len - 2; i >= 0; --i) a = a * x + R[o + i];
+        for (int i = len - 2; i >= 0; --i) a = fma(a, x, R[o + i]);
         v[k] = a;
     }
     int c = 0;
@@ -202,14 +207,14 @@ __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], doubl
 __device__ __forceinline__ double peval1(const double (&R)[kChain], double x) {
     double a = R[row_off(1) + 9];
 #pragma unroll
-    for (int i = 8; i >= 0; --i) a = a * x + R[row_off(1) + i];
+    for (int i = 8; i >= 0; --i) a = fma(a, x, R[row_off(1) + i]);
     return a;
 }
 
 __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
     double a = R[10];
 #pragma unroll
-    for (int i = 9; i >= 0; --i) a = a * x + R[i];
+    for (int i = 9; i >= 0; --i) a = fma(a, x, R[i]);
     return a;
 }
 
@@ -236,7 +241,7 @@ __device__ __forceinline__ void sturm_chain_fallback(const double (&row0)[11], i
         for (int i = 0; i <= da; ++i) t[i] = a[i];
         for (int k = da; k >= db; --k) {
             const double f = t[k] / b[db];
-            for (int i = 0; i <= db; ++i) t[k - db + i] -= f * b[i];
+            for (int i = 0; i <= db; ++i) t[k - db + i] = fma(-f, b[i], t[k - db + i]);
             t[k] = 0.0;
         }
         int dr = db - 1;
@@ -296,7 +301,7 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, double (&
             for (int kk = da; kk >= db; --kk) {
                 const double f = t[kk] / R[ob + db];
 #pragma unroll
-                for (int i = 0; i <= db; ++i) t[kk - db + i] -= f * R[ob + i];
+                for (int i = 0; i <= db; ++i) t[kk - db + i] = fma(-f, R[ob + i], t[kk - db + i]);
                 t[kk] = 0.0;
             }
             double scale = 0.0;
@@ -417,7 +422,7 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, double (&
                 flo[k] = go && left ? fx : flo[k];
                 hi[k] = go && !left ? xr[k] : hi[k];
                 const double xn = xr[k] - fx / dfx;
-                const double xs = (xn > lo[k] && xn < hi[k]) ? xn : 0.5 * (lo[k] + hi[k]);
+                const double xs = (xn >= lo[k] && xn <= hi[k]) ? xn : 0.5 * (lo[k] + hi[k]);
                 xr[k] = go ? xs : xr[k];
             }
         }
@@ -457,7 +462,7 @@ __device__ bool nullspace_5x9(const double* x1, const double* x2, SolverMem m, d
         for (int i = 0; i < 5; ++i) {
             if (i == r) continue;
             const double f = q[9 * i + r];
-            for (int j = 0; j < 9; ++j) q[9 * i + j] -= f * q[9 * r + j];
+            for (int j = 0; j < 9; ++j) q[9 * i + j] = fma(-f, q[9 * r + j], q[9 * i + j]);
         }
     }
 #pragma unroll
@@ -467,7 +472,7 @@ __device__ bool nullspace_5x9(const double* x1, const double* x2, SolverMem m, d
         for (int r = 0; r < 5; ++r) v[col[r]] = -q[9 * r + 5 + k];
         double nrm = 0.0;
 #pragma unroll
-        for (int j = 0; j < 9; ++j) nrm += v[j] * v[j];
+        for (int j = 0; j < 9; ++j) nrm = fma(v[j], v[j], nrm);
         nrm = sqrt(nrm);
 #pragma unroll
         for (int j = 0; j < 9; ++j) N[k][j] = v[j] / nrm;
@@ -479,7 +484,7 @@ __device__ __forceinline__ void addmul_ql_lds(const double* q, const double* l, 
 #pragma unroll
     for (int i = 0; i < 10; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] += s * (q[i] * l[j]);
+        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = fma(s, q[i] * l[j], c[kQL2C[i][j]]);
 }
 
 // Lanes 2k and 2k+1 solve one hypothesis together; the even lane holds columns 0..9 of the 10 x 20 matrix, the odd
@@ -627,7 +632,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
             for (int j = 0; j < 10; ++j) row[j] = ld(r, j);
             const double f = pair_lo(row[c]);
 #pragma unroll
-            for (int j = 0; j < 10; ++j) row[j] -= f * prow[j];
+            for (int j = 0; j < 10; ++j) row[j] = fma(-f, prow[j], row[j]);
 #pragma unroll
             for (int j = 0; j < 10; ++j) {
                 if (r < kRegRows) G[r < kRegRows ? r : 0][j] = row[j];
@@ -699,16 +704,16 @@ __device__ int five_point_stage2(const double* in, RootMem m, SolFn&& on_sol) {
 #pragma unroll
             for (int i = 0; i <= deg[c1]; ++i)
 #pragma unroll
-                for (int j = 0; j <= deg[c2]; ++j) mm[i + j] += B[1][c1][i] * B[2][c2][j];
+                for (int j = 0; j <= deg[c2]; ++j) mm[i + j] = fma(B[1][c1][i], B[2][c2][j], mm[i + j]);
 #pragma unroll
             for (int i = 0; i <= deg[c2]; ++i)
 #pragma unroll
-                for (int j = 0; j <= deg[c1]; ++j) mm[i + j] -= B[1][c2][i] * B[2][c1][j];
+                for (int j = 0; j <= deg[c1]; ++j) mm[i + j] = fma(-B[1][c2][i], B[2][c1][j], mm[i + j]);
             const int dm = deg[c1] + deg[c2];
 #pragma unroll
             for (int i = 0; i <= deg[c]; ++i)
 #pragma unroll
-                for (int j = 0; j <= dm; ++j) n[i + j] += B[0][c][i] * mm[j];
+                for (int j = 0; j <= dm; ++j) n[i + j] = fma(B[0][c][i], mm[j], n[i + j]);
         }
     }
     RPROF(6);
@@ -734,7 +739,7 @@ __device__ int five_point_stage2(const double* in, RootMem m, SolFn&& on_sol) {
                 const int dg = c == 2 ? 4 : 3;
                 double v = B[r][c][dg];
 #pragma unroll
-                for (int i = dg - 1; i >= 0; --i) v = v * z + B[r][c][i];
+                for (int i = dg - 1; i >= 0; --i) v = fma(v, z, B[r][c][i]);
                 Bz[r][c] = v;
             }
         double bx = 0, by = 0, bzz = 0, bn = -1.0;
@@ -1012,13 +1017,13 @@ __device__ void svd3(const double* E, double* U, double* s, double* V) {
 }
 
 __device__ __forceinline__ double sampson_sq(const double* E, double2 p1, double2 p2, double* den_out) {
-    const double a0 = E[0] * p1.x + E[1] * p1.y + E[2];
-    const double a1 = E[3] * p1.x + E[4] * p1.y + E[5];
-    const double a2 = E[6] * p1.x + E[7] * p1.y + E[8];
-    const double b0 = E[0] * p2.x + E[3] * p2.y + E[6];
-    const double b1 = E[1] * p2.x + E[4] * p2.y + E[7];
-    const double num = p2.x * a0 + p2.y * a1 + a2;
-    const double den = a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1;
+    const double a0 = fma(E[1], p1.y, fma(E[0], p1.x, E[2]));
+    const double a1 = fma(E[4], p1.y, fma(E[3], p1.x, E[5]));
+    const double a2 = fma(E[7], p1.y, fma(E[6], p1.x, E[8]));
+    const double b0 = fma(E[3], p2.y, fma(E[0], p2.x, E[6]));
+    const double b1 = fma(E[4], p2.y, fma(E[1], p2.x, E[7]));
+    const double num = fma(p2.y, a1, fma(p2.x, a0, a2));
+    const double den = fma(b1, b1, fma(b0, b0, fma(a1, a1, a0 * a0)));
     *den_out = den;
     return den > 0.0 ? num * num / den : 1e300;
 }
@@ -1053,8 +1058,9 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Wave-cooperative Sampson-weighted 8-point refit (see oracle refit_essential). The 45 unique normal-matrix
-// entries are summed per lane, then butterfly-reduced across the wave (fixed order: deterministic).
+// Wave-cooperative Sampson-weighted 8-point refit (oracle/ransac.c refit_essential). The 45 unique normal-matrix
+// entries are summed per lane (point i in lane i mod 64), then reduced across the wave by wave_sum_f64; the oracle
+// forms the same partial sums and restates the reduction order (wave_sum_order), so the sums agree bit for bit.
 __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const double* Esel, double th2,
                            const double* Ew, double* Eout, int lane, double* jac_a, double* jac_v) {
     double acc[45];
@@ -1071,9 +1077,11 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
         const double r[9] = {u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, 1.0};
         int k = 0;
 #pragma unroll
-        for (int a = 0; a < 9; ++a)
+        for (int a = 0; a < 9; ++a) {
+            const double wa = w2 * r[a];
 #pragma unroll
-            for (int b = a; b < 9; ++b) acc[k++] += w2 * r[a] * r[b];
+            for (int b = a; b < 9; ++b, ++k) acc[k] = fma(wa, r[b], acc[k]);
+        }
         ++n;
     }
     for (int m = 32; m >= 1; m >>= 1) n += __shfl_xor(n, m);
@@ -1082,9 +1090,9 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
     for (int k = 0; k < 45; ++k) acc[k] = wave_sum_f64(acc[k]);
     // Smallest eigenvector of the normal matrix: shifted inverse iteration on its Cholesky factor, register-resident
     // and computed redundantly by every lane (no LDS, no barriers). The shift (1e-12 of the trace) keeps the factor
-    // positive definite; 8 iterations contract the other eigen-directions by ((l1 + s) / (l2 + s))^8. Same
-    // eigenvector as the oracle's Jacobi (oracle/ransac.c refit_essential) to rounding; the LDS Jacobi remains the
-    // fallback when the factor breaks down (uniform across the wave: every lane holds identical values).
+    // positive definite; 8 iterations contract the other eigen-directions by ((l1 + s) / (l2 + s))^8. The oracle
+    // runs the same iteration; the LDS Jacobi (oracle jacobi_eig) is the fallback of both when the factor breaks
+    // down (uniform across the wave: every lane holds identical values).
     double E[9];
     {
         auto A = [&](int i, int j) -> double {  // full symmetric entry from the packed upper triangle (static)
@@ -1105,7 +1113,7 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
             for (int j = 0; j <= i; ++j) {
                 double v = A(i, j) + (i == j ? shift : 0.0);
 #pragma unroll
-                for (int k = 0; k < j; ++k) v -= L[i * (i + 1) / 2 + k] * L[j * (j + 1) / 2 + k];
+                for (int k = 0; k < j; ++k) v = fma(-L[i * (i + 1) / 2 + k], L[j * (j + 1) / 2 + k], v);
                 if (i == j) {
                     ok = ok && v > 0.0;
                     L[i * (i + 1) / 2 + i] = 1.0 / sqrt(fmax(v, 1e-300));
@@ -1122,19 +1130,19 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
                 for (int i = 0; i < 9; ++i) {  // L y = x
                     double v = x[i];
 #pragma unroll
-                    for (int k = 0; k < i; ++k) v -= L[i * (i + 1) / 2 + k] * x[k];
+                    for (int k = 0; k < i; ++k) v = fma(-L[i * (i + 1) / 2 + k], x[k], v);
                     x[i] = v * L[i * (i + 1) / 2 + i];
                 }
 #pragma unroll
                 for (int i = 8; i >= 0; --i) {  // L^T z = y
                     double v = x[i];
 #pragma unroll
-                    for (int k = i + 1; k < 9; ++k) v -= L[k * (k + 1) / 2 + i] * x[k];
+                    for (int k = i + 1; k < 9; ++k) v = fma(-L[k * (k + 1) / 2 + i], x[k], v);
                     x[i] = v * L[i * (i + 1) / 2 + i];
                 }
                 double nrm = 0.0;
 #pragma unroll
-                for (int i = 0; i < 9; ++i) nrm += x[i] * x[i];
+                for (int i = 0; i < 9; ++i) nrm = fma(x[i], x[i], nrm);
                 nrm = 1.0 / sqrt(nrm);
 #pragma unroll
                 for (int i = 0; i < 9; ++i) x[i] *= nrm;

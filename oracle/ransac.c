@@ -103,17 +103,17 @@ static void init_tables(void) {
 static void mul_ll(const double* a, const double* b, double* q) { /* q = a*b */
     memset(q, 0, 10 * sizeof(double));
     for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) q[LL2Q[i][j]] += a[i] * b[j];
+        for (int j = 0; j < 4; ++j) q[LL2Q[i][j]] = fma(a[i], b[j], q[LL2Q[i][j]]);
 }
 static void addmul_ql(const double* q, const double* l, double s, double* c) { /* c += s * q*l */
     for (int i = 0; i < 10; ++i)
-        for (int j = 0; j < 4; ++j) c[QL2C[i][j]] += s * (q[i] * l[j]);
+        for (int j = 0; j < 4; ++j) c[QL2C[i][j]] = fma(s, q[i] * l[j], c[QL2C[i][j]]);
 }
 
 /* ------------------------------------------------------------------ univariate polynomials (ascending coeffs) */
 static double peval(const double* p, int deg, double x) {
     double v = p[deg];
-    for (int i = deg - 1; i >= 0; --i) v = v * x + p[i];
+    for (int i = deg - 1; i >= 0; --i) v = fma(v, x, p[i]);
     return v;
 }
 
@@ -123,7 +123,7 @@ static int prem(const double* a, int da, const double* b, int db, double* r) {
     for (int i = 0; i <= da; ++i) t[i] = a[i];
     for (int k = da; k >= db; --k) {
         const double f = t[k] / b[db];
-        for (int i = 0; i <= db; ++i) t[k - db + i] -= f * b[i];
+        for (int i = 0; i <= db; ++i) t[k - db + i] = fma(-f, b[i], t[k - db + i]);
         t[k] = 0.0;
     }
     int dr = db - 1;
@@ -207,7 +207,8 @@ static int real_roots(const double* pin, int deg, double* roots) {
         const int cnt = va - vb;
         if (cnt <= 0) continue;
         if (cnt == 1 || b - a < 1e-10 * fmax(1.0, fabs(a))) {
-            /* refine: bisection down to a relative width of 2^-20, then 4 safeguarded Newton steps (p' is Sturm row 1) */
+            /* refine: bisection down to a relative width of 2^-20, then 4 safeguarded Newton steps (p' is Sturm
+             * row 1; a step landing on a bracket end is kept, so a root within rounding of an end is reached) */
             double lo = a, hi = b;
             double flo = peval(p, deg, lo);
             for (int it = 0; it < 80; ++it) {
@@ -232,7 +233,7 @@ static int real_roots(const double* pin, int deg, double* roots) {
                     hi = x;
                 }
                 const double xn = x - fx / dfx;
-                x = (xn > lo && xn < hi) ? xn : 0.5 * (lo + hi);
+                x = (xn >= lo && xn <= hi) ? xn : 0.5 * (lo + hi);
             }
             roots[nr++] = x;
             continue;
@@ -273,7 +274,7 @@ static int nullspace_5x9(const double q_in[5][9], double N[4][9]) {
         for (int i = 0; i < 5; ++i) {
             if (i == r) continue;
             const double f = q[i][r];
-            for (int j = 0; j < 9; ++j) q[i][j] -= f * q[r][j];
+            for (int j = 0; j < 9; ++j) q[i][j] = fma(-f, q[r][j], q[i][j]);
         }
     }
     for (int k = 0; k < 4; ++k) {
@@ -281,7 +282,7 @@ static int nullspace_5x9(const double q_in[5][9], double N[4][9]) {
         v[col[5 + k]] = 1.0;
         for (int r = 0; r < 5; ++r) v[col[r]] = -q[r][5 + k];
         double nrm = 0.0;
-        for (int j = 0; j < 9; ++j) nrm += v[j] * v[j];
+        for (int j = 0; j < 9; ++j) nrm = fma(v[j], v[j], nrm);
         nrm = sqrt(nrm);
         for (int j = 0; j < 9; ++j) N[k][j] = v[j] / nrm;
     }
@@ -352,7 +353,7 @@ int oracle_five_point(const double* x1, const double* x2, double* Es) {
         for (int r = 0; r < 10; ++r) {
             if (r == c) continue;
             const double f = A[r][c];
-            for (int j = 0; j < NMONO; ++j) A[r][j] -= f * A[c][j];
+            for (int j = 0; j < NMONO; ++j) A[r][j] = fma(-f, A[c][j], A[r][j]);
         }
     }
     /* B(z): rows k = e - z f, l = g - z h, m = i - z j (rows 4..9); columns [x-coef(deg3), y-coef(deg3), 1(deg4)] */
@@ -387,12 +388,12 @@ int oracle_five_point(const double* x1, const double* x2, double* Es) {
             double m[9];
             memset(m, 0, sizeof(m));
             for (int i = 0; i <= deg[c1]; ++i)
-                for (int j = 0; j <= deg[c2]; ++j) m[i + j] += B[1][c1][i] * B[2][c2][j];
+                for (int j = 0; j <= deg[c2]; ++j) m[i + j] = fma(B[1][c1][i], B[2][c2][j], m[i + j]);
             for (int i = 0; i <= deg[c2]; ++i)
-                for (int j = 0; j <= deg[c1]; ++j) m[i + j] -= B[1][c2][i] * B[2][c1][j];
+                for (int j = 0; j <= deg[c1]; ++j) m[i + j] = fma(-B[1][c2][i], B[2][c1][j], m[i + j]);
             const int dm = deg[c1] + deg[c2];
             for (int i = 0; i <= deg[c]; ++i)
-                for (int j = 0; j <= dm; ++j) n[i + j] += B[0][c][i] * m[j];
+                for (int j = 0; j <= dm; ++j) n[i + j] = fma(B[0][c][i], m[j], n[i + j]);
         }
     }
     double roots[MAX_SOL];
@@ -564,23 +565,48 @@ static void svd3(const double* E, double* U, double* s, double* V) {
 
 /* Sampson denominator |Ex1|_xy^2 + |E'x2|_xy^2 and squared Sampson error of one correspondence (double). */
 static double sampson_sq(const double* E, const double* p1, const double* p2, double* den_out) {
-    const double a0 = E[0] * p1[0] + E[1] * p1[1] + E[2];
-    const double a1 = E[3] * p1[0] + E[4] * p1[1] + E[5];
-    const double a2 = E[6] * p1[0] + E[7] * p1[1] + E[8];
-    const double b0 = E[0] * p2[0] + E[3] * p2[1] + E[6];
-    const double b1 = E[1] * p2[0] + E[4] * p2[1] + E[7];
-    const double num = p2[0] * a0 + p2[1] * a1 + a2;
-    const double den = a0 * a0 + a1 * a1 + b0 * b0 + b1 * b1;
+    const double a0 = fma(E[1], p1[1], fma(E[0], p1[0], E[2]));
+    const double a1 = fma(E[4], p1[1], fma(E[3], p1[0], E[5]));
+    const double a2 = fma(E[7], p1[1], fma(E[6], p1[0], E[8]));
+    const double b0 = fma(E[3], p2[1], fma(E[0], p2[0], E[6]));
+    const double b1 = fma(E[4], p2[1], fma(E[1], p2[0], E[7]));
+    const double num = fma(p2[1], a1, fma(p2[0], a0, a2));
+    const double den = fma(b1, b1, fma(b0, b0, fma(a1, a1, a0 * a0)));
     *den_out = den;
     return den > 0.0 ? num * num / den : 1e300;
 }
 
+/* Sum of 64 per-lane partial sums in the order of the device's wave reduction (gtsfm_amd/csrc/ransac.hip
+ * wave_sum_f64): a Hillis-Steele scan inside each row of 16 lanes (lane i adds lane i - 1, i - 2, i - 4, i - 8 of its
+ * row, or +0.0 past the row start), then rows 1 and 3 add lane 15 of the row below, rows 2 and 3 add lane 31; the
+ * total is lane 63. Fixed order, so the CPU and the GPU round identically. */
+static double wave_sum_order(const double* in) {
+    double v[64], t[64];
+    memcpy(v, in, sizeof(v));
+    for (int n = 1; n <= 8; n <<= 1) {
+        memcpy(t, v, sizeof(t));
+        for (int i = 0; i < 64; ++i) v[i] = t[i] + ((i & 15) >= n ? t[i - n] : 0.0);
+    }
+    memcpy(t, v, sizeof(t));
+    for (int i = 0; i < 64; ++i) {
+        const int r = i >> 4;
+        v[i] = t[i] + ((r == 1 || r == 3) ? t[16 * r - 1] : 0.0);
+    }
+    memcpy(t, v, sizeof(t));
+    for (int i = 0; i < 64; ++i) v[i] = t[i] + ((i >> 4) >= 2 ? t[31] : 0.0);
+    return v[63];
+}
+
 /* Sampson-weighted linear 8-point fit (rows scaled by 1/sqrt(den under E_w)) on the points whose squared Sampson
- * error under E_sel is <= th2, projected onto the essential manifold. Returns 0 if fewer than 8 points. */
+ * error under E_sel is <= th2, projected onto the essential manifold. Returns 0 if fewer than 8 points.
+ * The 45 normal-matrix sums are formed as the device forms them (point i into partial sum i mod 64, in index order,
+ * then wave_sum_order). The smallest eigenvector is found by shifted inverse iteration on the Cholesky factor
+ * (shift 1e-12 trace, 8 iterations from the all-ones vector, the factor's diagonal stored as reciprocals), with the
+ * cyclic Jacobi as the fallback when the factor breaks down; both are the device's operations in its order. */
 static int refit_essential(const double* x1, const double* x2, int M, const double* E_sel, double th2,
                            const double* E_w, double* Eout) {
-    double ata[81];
-    memset(ata, 0, sizeof(ata));
+    static __thread double part[64][45];
+    memset(part, 0, sizeof(part));
     int n = 0;
     for (int i = 0; i < M; ++i) {
         double den;
@@ -590,18 +616,70 @@ static int refit_essential(const double* x1, const double* x2, int M, const doub
         const double w2 = dw > 1e-300 ? 1.0 / dw : 0.0;
         const double u1 = x1[2 * i], v1 = x1[2 * i + 1], u2 = x2[2 * i], v2 = x2[2 * i + 1];
         const double r[9] = {u2 * u1, u2 * v1, u2, v2 * u1, v2 * v1, v2, u1, v1, 1.0};
-        for (int a = 0; a < 9; ++a)
-            for (int b = 0; b < 9; ++b) ata[a * 9 + b] += w2 * r[a] * r[b];
+        double* acc = part[i & 63];
+        int k = 0;
+        for (int a = 0; a < 9; ++a) {
+            const double wa = w2 * r[a];
+            for (int b = a; b < 9; ++b, ++k) acc[k] = fma(wa, r[b], acc[k]);
+        }
         ++n;
     }
     if (n < 8) return 0;
-    double w[9], V[81];
-    jacobi_eig(ata, 9, w, V);
-    int imin = 0;
-    for (int i = 1; i < 9; ++i)
-        if (w[i] < w[imin]) imin = i;
+    double ata[45], col[64];
+    for (int k = 0; k < 45; ++k) {
+        for (int l = 0; l < 64; ++l) col[l] = part[l][k];
+        ata[k] = wave_sum_order(col);
+    }
+#define ATA(i, j) ata[((i) < (j) ? (i) : (j)) * 9 - ((i) < (j) ? (i) : (j)) * (((i) < (j) ? (i) : (j)) - 1) / 2 + \
+                      (((i) < (j) ? (j) : (i)) - ((i) < (j) ? (i) : (j)))]
     double E[9];
-    for (int k = 0; k < 9; ++k) E[k] = V[k * 9 + imin];
+    double tr = 0.0;
+    for (int i = 0; i < 9; ++i) tr += ATA(i, i);
+    const double shift = 1e-12 * tr;
+    double L[45]; /* packed lower triangle, row i at i (i + 1) / 2; the diagonal holds 1 / L_ii */
+    int ok = tr > 0.0;
+    for (int i = 0; i < 9; ++i)
+        for (int j = 0; j <= i; ++j) {
+            double v = ATA(i, j) + (i == j ? shift : 0.0);
+            for (int k = 0; k < j; ++k) v = fma(-L[i * (i + 1) / 2 + k], L[j * (j + 1) / 2 + k], v);
+            if (i == j) {
+                ok = ok && v > 0.0;
+                L[i * (i + 1) / 2 + i] = 1.0 / sqrt(fmax(v, 1e-300));
+            } else {
+                L[i * (i + 1) / 2 + j] = v * L[j * (j + 1) / 2 + j];
+            }
+        }
+    if (ok) {
+        double x[9];
+        for (int i = 0; i < 9; ++i) x[i] = 1.0;
+        for (int it = 0; it < 8; ++it) {
+            for (int i = 0; i < 9; ++i) { /* L y = x */
+                double v = x[i];
+                for (int k = 0; k < i; ++k) v = fma(-L[i * (i + 1) / 2 + k], x[k], v);
+                x[i] = v * L[i * (i + 1) / 2 + i];
+            }
+            for (int i = 8; i >= 0; --i) { /* L^T z = y */
+                double v = x[i];
+                for (int k = i + 1; k < 9; ++k) v = fma(-L[k * (k + 1) / 2 + i], x[k], v);
+                x[i] = v * L[i * (i + 1) / 2 + i];
+            }
+            double nrm = 0.0;
+            for (int i = 0; i < 9; ++i) nrm = fma(x[i], x[i], nrm);
+            nrm = 1.0 / sqrt(nrm);
+            for (int i = 0; i < 9; ++i) x[i] *= nrm;
+        }
+        for (int k = 0; k < 9; ++k) E[k] = x[k];
+    } else {
+        double a[81], w[9], V[81];
+        for (int i = 0; i < 9; ++i)
+            for (int j = 0; j < 9; ++j) a[i * 9 + j] = ATA(i, j);
+        jacobi_eig(a, 9, w, V);
+        int imin = 0;
+        for (int i = 1; i < 9; ++i)
+            if (w[i] < w[imin]) imin = i;
+        for (int k = 0; k < 9; ++k) E[k] = V[k * 9 + imin];
+    }
+#undef ATA
     double U[9], s[3], Vv[9];
     svd3(E, U, s, Vv);
     double nrm = 0.0;

@@ -6,11 +6,11 @@ cd "$(dirname "$0")/.."
 SRC=$1; shift
 B=$(basename $SRC .hip)
 make -C gtsfm_amd/csrc -j8 >/dev/null
-mkdir -p build_var
+mkdir -p ${VARDIR:=build_var}
 OBJS=$(ls gtsfm_amd/_lib/obj/*.o | grep -v "/$B.o")
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Igtsfm_amd/csrc $flags -c gtsfm_amd/csrc/$B.hip -o build_var/${B}_$name.o
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build_var/libgtsfm_hip_$name.so $OBJS build_var/${B}_$name.o
-  echo "built build_var/libgtsfm_hip_$name.so ($flags)"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Igtsfm_amd/csrc $flags -c gtsfm_amd/csrc/$B.hip -o $VARDIR/${B}_$name.o
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $VARDIR/libgtsfm_hip_$name.so $OBJS $VARDIR/${B}_$name.o
+  echo "built $VARDIR/libgtsfm_hip_$name.so ($flags)"
 done
