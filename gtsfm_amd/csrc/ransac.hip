@@ -95,11 +95,14 @@ __device__ __forceinline__ void mul_ll(const double* a, const double* b, double*
         for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] = fma(a[i], b[j], q[kLL2Q[i][j]]);
 }
 
+// c += s * q*l (oracle addmul_ql); s is 1, -1 or 2, so s * q[i] is exact and every term is one fused multiply-add
 __device__ __forceinline__ void addmul_ql(const double* q, const double* l, double s, double* c) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i)
+    for (int i = 0; i < 10; ++i) {
+        const double sq = s * q[i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = fma(s, q[i] * l[j], c[kQL2C[i][j]]);
+        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = fma(sq, l[j], c[kQL2C[i][j]]);
+    }
 }
 
 // ------------------------------------------------------------------ lane-private arrays in LDS
@@ -478,13 +481,6 @@ __device__ bool nullspace_5x9(const double* x1, const double* x2, SolverMem m, d
         for (int j = 0; j < 9; ++j) N[k][j] = v[j] / nrm;
     }
     return true;
-}
-
-__device__ __forceinline__ void addmul_ql_lds(const double* q, const double* l, double s, LaneArr<double> c) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = fma(s, q[i] * l[j], c[kQL2C[i][j]]);
 }
 
 // Lanes 2k and 2k+1 solve one hypothesis together; the even lane holds columns 0..9 of the 10 x 20 matrix, the odd

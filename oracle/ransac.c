@@ -105,9 +105,12 @@ static void mul_ll(const double* a, const double* b, double* q) { /* q = a*b */
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) q[LL2Q[i][j]] = fma(a[i], b[j], q[LL2Q[i][j]]);
 }
-static void addmul_ql(const double* q, const double* l, double s, double* c) { /* c += s * q*l */
-    for (int i = 0; i < 10; ++i)
-        for (int j = 0; j < 4; ++j) c[QL2C[i][j]] = fma(s, q[i] * l[j], c[QL2C[i][j]]);
+/* c += s * q*l; s is 1, -1 or 2, so s * q[i] is exact and every term is one fused multiply-add */
+static void addmul_ql(const double* q, const double* l, double s, double* c) {
+    for (int i = 0; i < 10; ++i) {
+        const double sq = s * q[i];
+        for (int j = 0; j < 4; ++j) c[QL2C[i][j]] = fma(sq, l[j], c[QL2C[i][j]]);
+    }
 }
 
 /* ------------------------------------------------------------------ univariate polynomials (ascending coeffs) */
