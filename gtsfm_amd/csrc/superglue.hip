@@ -155,6 +155,215 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
     }
 }
 
+// ------------------------------------------------------------------ batched GEMM, fp32-accurate on bf16 MFMA
+// Every fp32 operand x is split exactly into three bf16 planes, x = x_h + x_m + x_l (each plane the bf16 rounding of
+// what the planes above it leave; the two subtractions are exact), and a product a b is formed from the six largest
+// of its nine plane products: a_h b_h + a_h b_m + a_m b_h + a_m b_m + a_h b_l + a_l b_h. bf16 x bf16 products are
+// exact in the fp32 accumulator, and the dropped terms (a_m b_l, a_l b_m, a_l b_l) are below 2^-23 |a b| together,
+// so each product carries an fp32-level error; the sums are fp32 as on the fp32 matrix cores. Six
+// v_mfma_f32_32x32x16_bf16 (16 k each) replace eight v_mfma_f32_32x32x2_f32 (2 k each): 2.7x the product rate.
+// Weights are split once per layer into [plane][n][k] (sg_split_weights_kernel); activations are split as they are
+// staged into LDS. 128 x 128 output tile per workgroup of four waves (64 x 64 each, four 32 x 32 accumulators),
+// K in chunks of 16 held in LDS as [plane][row][16] bf16 (32-byte rows: a lane's 16-byte fragment read is
+// conflict-free), the next chunk prefetched into registers during the MFMAs.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kG3Tile = 128;
+
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+// eight consecutive fp32 -> three 16-byte planes
+__device__ __forceinline__ void split3x8(const f32x4_t& a, const f32x4_t& b, bf16x8& h, bf16x8& m, bf16x8& l) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        __bf16 hh, mm, ll;
+        split3(j < 4 ? a[j & 3] : b[j & 3], hh, mm, ll);
+        h[j] = hh;
+        m[j] = mm;
+        l[j] = ll;
+    }
+}
+
+struct Gemm3Args {
+    const float* A;  // A[z][m][k] (k < Ksplit), A2[z][m][k - Ksplit] (k >= Ksplit); K a multiple of 16
+    long lda, a_batch;
+    const float* A2;
+    long lda2, a2_batch;
+    int Ksplit;
+    const __bf16* Bp;  // weights: [3][N][K] bf16 planes (batch-invariant), or null
+    const float* Bt;   // activations: Bt[z][n][k] fp32 (ldb, b_batch), split while staging
+    long ldb, b_batch;
+    const float *bias, *bn_scale, *bn_shift;
+    int relu;
+    float alpha;
+    float* C;
+    long ldc, c_batch;
+    int residual;
+    int M, N, K;
+    const int* m_lim;
+    const int* n_lim;
+    int lim_stride;
+    // q/k/v projection only: columns 256..511 (keys) and 512..767 (values) go to bf16 planes for the attention
+    // kernel instead of C: K planes [z][3][head][m][64], then V^T planes [z][3][head][64][M] (kv_batch per z)
+    __bf16* kv;
+    long kv_batch;
+};
+
+__global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
+    __shared__ __attribute__((aligned(16))) __bf16 As[3][kG3Tile][16];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[3][kG3Tile][16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int z = blockIdx.z;
+    const int m0 = blockIdx.y * kG3Tile, n0 = blockIdx.x * kG3Tile;
+    int Mv = g.M, Nv = g.N;
+    if (g.m_lim) Mv = min(Mv, g.m_lim[z * g.lim_stride]);
+    if (g.n_lim) Nv = min(Nv, g.n_lim[z * g.lim_stride + 1]);
+    if (m0 >= Mv || n0 >= Nv) return;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r = lane & 31, hk = lane >> 5;
+    // staging roles: thread t stages row / column t >> 1, k half 8 (t & 1)
+    const int srow = tid >> 1, sk = 8 * (tid & 1);
+    const bool a_ok = m0 + srow < g.M, b_ok = n0 + srow < g.N;
+    const float* Arow = g.A + z * g.a_batch + (long)(m0 + srow) * g.lda + sk;
+    const float* A2row = g.A2 ? g.A2 + z * g.a2_batch + (long)(m0 + srow) * g.lda2 + sk - g.Ksplit : nullptr;
+    f32x4_t pa0, pa1, pb0, pb1;
+    u32x4 pw[3];
+    auto load = [&](int k0) {
+        pa0 = pa1 = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        if (a_ok) {
+            const float* src = k0 < g.Ksplit ? Arow + k0 : A2row + k0;
+            pa0 = *(const f32x4_t*)src;
+            pa1 = *(const f32x4_t*)(src + 4);
+        }
+        if (g.Bp) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+                pw[p] = b_ok ? *(const u32x4*)(g.Bp + ((long)p * g.N + n0 + srow) * g.K + k0 + sk) : u32x4{0, 0, 0, 0};
+        } else {
+            pb0 = pb1 = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            if (b_ok) {
+                const float* src = g.Bt + z * g.b_batch + (long)(n0 + srow) * g.ldb + k0 + sk;
+                pb0 = *(const f32x4_t*)src;
+                pb1 = *(const f32x4_t*)(src + 4);
+            }
+        }
+    };
+    auto store = [&]() {
+        bf16x8 h, m, l;
+        split3x8(pa0, pa1, h, m, l);
+        *(bf16x8*)&As[0][srow][sk] = h;
+        *(bf16x8*)&As[1][srow][sk] = m;
+        *(bf16x8*)&As[2][srow][sk] = l;
+        if (g.Bp) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) *(u32x4*)&Bs[p][srow][sk] = pw[p];
+        } else {
+            split3x8(pb0, pb1, h, m, l);
+            *(bf16x8*)&Bs[0][srow][sk] = h;
+            *(bf16x8*)&Bs[1][srow][sk] = m;
+            *(bf16x8*)&Bs[2][srow][sk] = l;
+        }
+    };
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    load(0);
+    for (int k0 = 0; k0 < g.K; k0 += 16) {
+        __syncthreads();  // the previous chunk's fragments are read
+        store();
+        __syncthreads();
+        if (k0 + 16 < g.K) load(k0 + 16);  // in flight during the MFMAs
+        bf16x8 a[3][2], b[3][2];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                a[p][s] = *(const bf16x8*)&As[p][64 * wm + 32 * s + r][8 * hk];
+                b[p][s] = *(const bf16x8*)&Bs[p][64 * wn + 32 * s + r][8 * hk];
+            }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
+                acc[i][j] = c;
+            }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = n0 + 64 * wn + 32 * j + r;
+        if (n >= Nv) continue;
+        const float bb = g.bias ? g.bias[n] : 0.0f;
+        const float sc = g.bn_scale ? g.bn_scale[n] : 1.0f;
+        const float sh = g.bn_shift ? g.bn_shift[n] : 0.0f;
+        float* C = g.C + z * g.c_batch + n;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int m = m0 + 64 * wm + 32 * i + 4 * hk + (e & 3) + 8 * (e >> 2);
+                if (m >= Mv) continue;
+                float v = acc[i][j][e] + bb;
+                if (g.bn_scale) v = v * sc + sh;
+                if (g.relu) v = v > 0.0f ? v : 0.0f;
+                if (g.alpha != 1.0f) v = v * g.alpha;
+                if (g.kv && n >= kD) {
+                    __bf16 pl[3];
+                    split3(v, pl[0], pl[1], pl[2]);
+                    const int d = (n - kD) & (kD - 1), hh = d / kHd, dd = d % kHd;
+                    __bf16* base = g.kv + z * g.kv_batch;
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+                        if (n < 2 * kD)
+                            base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
+                        else
+                            base[(long)3 * kD * g.M + (((long)q * kHeads + hh) * kHd + dd) * g.M + m] = pl[q];
+                    }
+                    continue;
+                }
+                float* c = C + (long)m * g.ldc;
+                *c = g.residual ? *c + v : v;
+            }
+    }
+}
+
+// W^T[K][N] fp32 (row-major, the packed layout) -> [3][N][K] bf16 planes for sg_gemm3_kernel; up to four matrices
+// per launch (blockIdx.y), one thread per element
+struct SplitJob {
+    const float* W;
+    __bf16* out;
+    int K, N;
+};
+struct SplitJobs {
+    SplitJob j[4];
+};
+
+__global__ void sg_split_weights_kernel(SplitJobs jobs) {
+    const SplitJob jb = jobs.j[blockIdx.y];
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (!jb.W || e >= (long)jb.K * jb.N) return;
+    const int n = (int)(e / jb.K), k = (int)(e % jb.K);
+    __bf16 h, m, l;
+    split3(jb.W[(long)k * jb.N + n], h, m, l);
+    const long plane = (long)jb.K * jb.N;
+    jb.out[e] = h;
+    jb.out[plane + e] = m;
+    jb.out[2 * plane + e] = l;
+}
+
 // ------------------------------------------------------------------ fused multi-head attention
 // superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 64 queries of one
 // (pair, side, head); wave w owns queries 16 w .. +16 and streams the source side's keys in chunks of 64 (online
@@ -265,6 +474,147 @@ __global__ __launch_bounds__(256, 3) void sg_attention_kernel(const float* __res
             for (int s = 0; s < 16; ++s)
                 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pw[lr * (kAttnKeys + 1) + 4 * s + lq],
                                                            Vc[(4 * s + lq) * kKvStride + 16 * u + lr], acc, 0, 0, 0);
+            o[u] = acc;
+        }
+    }
+    float* ob = out + (long)zs * kmax * 256 + h * kHd;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int q = q0 + 4 * lq + j;
+        if (q >= nq) continue;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ob[(long)q * 256 + 16 * u + lr] = l_run[j] > 0.0f ? o[u][j] / l_run[j] : 0.0f;
+    }
+}
+
+// Split-precision attention (the fp32 kernel above, restated on bf16 MFMA with the three-plane products of
+// sg_gemm3_kernel): v_mfma_f32_16x16x32_bf16, A lane l = A[l % 16][8 (l / 16) + j], B lane l = B[8 (l / 16) + j][l % 16],
+// C lane l, j = C[4 (l / 16) + j][l % 16]. Keys arrive as bf16 planes [key][64] and values transposed [64][key] (written
+// by the q/k/v projection's epilogue), so a key chunk is staged by 16-byte copies; Q is split once per wave, P per
+// chunk. Rows of the LDS planes are padded to 72 elements (conflict-free 16-byte fragment reads).
+constexpr int kAttnPad = 72;
+
+__global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
+                                                             const __bf16* __restrict__ kvp, long kv_batch,
+                                                             const int* __restrict__ side_counts, int kmax, int cross,
+                                                             float* __restrict__ out /*(2P, kmax, 256)*/) {
+    __shared__ __attribute__((aligned(16))) __bf16 Ks[3][kAttnKeys][kAttnPad];
+    __shared__ __attribute__((aligned(16))) __bf16 Vs[3][kHd][kAttnPad];
+    __shared__ __attribute__((aligned(16))) float Pw[4][16][kAttnKeys + 4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int zs = blockIdx.z;
+    const int zsrc = cross ? (zs ^ 1) : zs;
+    const int h = blockIdx.y;
+    const int q0 = blockIdx.x * 64 + 16 * wave;
+    const int nkeys = side_counts[zsrc];
+    const int nq = side_counts[zs];
+    if (blockIdx.x * 64 >= nq) return;
+    const int lr = lane & 15, lq = lane >> 4;
+    // Q fragments, planes x k-steps: Q[q0 + lr][32 s + 8 lq + j]
+    bf16x8 qf[3][2];
+    {
+        const float* qrow = qkv + ((long)zs * kmax + min(q0 + lr, kmax - 1)) * 768 + h * kHd + 8 * lq;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            split3x8(*(const f32x4_t*)(qrow + 32 * s), *(const f32x4_t*)(qrow + 32 * s + 4), qf[0][s], qf[1][s],
+                     qf[2][s]);
+    }
+    float m_run[4], l_run[4];
+    f32x4_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        m_run[j] = -INFINITY;
+        l_run[j] = 0.0f;
+        o[j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    const __bf16* kb = kvp + zsrc * kv_batch;                          // [3][head][kmax][64]
+    const __bf16* vb = kvp + zsrc * kv_batch + (long)3 * kD * kmax;    // [3][head][64][kmax]
+    for (int c0 = 0; c0 < nkeys; c0 += kAttnKeys) {
+        __syncthreads();  // previous chunk consumed
+        for (int e = tid; e < 3 * kAttnKeys * 8; e += 256) {
+            const int p = e / (kAttnKeys * 8), row = (e / 8) % kAttnKeys, seg = e % 8;
+            u32x4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
+            if (c0 + row < nkeys) kv = *(const u32x4*)(kb + (((long)p * kHeads + h) * kmax + c0 + row) * kHd + 8 * seg);
+            if (c0 + 8 * seg < nkeys) vv = *(const u32x4*)(vb + (((long)p * kHeads + h) * kHd + row) * kmax + c0 + 8 * seg);
+            *(u32x4*)&Ks[p][row][8 * seg] = kv;
+            *(u32x4*)&Vs[p][row][8 * seg] = vv;
+        }
+        __syncthreads();
+        // S = Q K^T / 8 for 16 queries x 64 keys (4 tiles of 16 keys)
+        f32x4_t s4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const bf16x8 k0 = *(const bf16x8*)&Ks[0][16 * t + lr][32 * s + 8 * lq];
+                const bf16x8 k1 = *(const bf16x8*)&Ks[1][16 * t + lr][32 * s + 8 * lq];
+                const bf16x8 k2 = *(const bf16x8*)&Ks[2][16 * t + lr][32 * s + 8 * lq];
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[0][s], k2, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[2][s], k0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[1][s], k1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[0][s], k1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[1][s], k0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[0][s], k0, acc, 0, 0, 0);
+            }
+            s4[t] = acc;
+        }
+        float cmax[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float mx = -INFINITY;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                float v = s4[t][j] / 8.0f;
+                if (c0 + 16 * t + lr >= nkeys) v = -INFINITY;
+                s4[t][j] = v;
+                mx = fmaxf(mx, v);
+            }
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
+            cmax[j] = mx;
+        }
+        float(*pw)[kAttnKeys + 4] = Pw[wave];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float mnew = fmaxf(m_run[j], cmax[j]);
+            const float corr = expf(m_run[j] - mnew);
+            float rs = 0.0f;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float p = expf(s4[t][j] - mnew);
+                rs = rs + p;
+                pw[4 * lq + j][16 * t + lr] = p;
+            }
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) rs = rs + __shfl_xor(rs, m);
+            l_run[j] = l_run[j] * corr + rs;
+            m_run[j] = mnew;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) o[u][j] = o[u][j] * corr;
+        }
+        __syncthreads();  // P (written in C layout) is read back in A layout
+        // O += P V: A = P (16 queries x 64 keys), B = V (64 keys x 64 dims, 4 tiles of 16)
+        bf16x8 pf[3][2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            split3x8(*(const f32x4_t*)&pw[lr][32 * s + 8 * lq], *(const f32x4_t*)&pw[lr][32 * s + 8 * lq + 4], pf[0][s],
+                     pf[1][s], pf[2][s]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            f32x4_t acc = o[u];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const bf16x8 v0 = *(const bf16x8*)&Vs[0][16 * u + lr][32 * s + 8 * lq];
+                const bf16x8 v1 = *(const bf16x8*)&Vs[1][16 * u + lr][32 * s + 8 * lq];
+                const bf16x8 v2 = *(const bf16x8*)&Vs[2][16 * u + lr][32 * s + 8 * lq];
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[0][s], v2, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[2][s], v0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[1][s], v1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[0][s], v1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[1][s], v0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[0][s], v0, acc, 0, 0, 0);
+            }
             o[u] = acc;
         }
     }
@@ -524,8 +874,11 @@ __global__ __launch_bounds__(256) void sk_final_kernel(const float* __restrict__
 
 // ------------------------------------------------------------------ host-side orchestration
 struct SgLayout {
-    size_t enc_in, X, T1, T2, qkv, att, msg, hid, Z, u, v, max0, idx0, idx1, cnt, total;
+    size_t enc_in, X, T1, T2, qkv, kvp, att, msg, hid, Z, u, v, max0, idx0, idx1, cnt, wsplit, total;
 };
+
+// bf16 planes of one GNN layer's four weight matrices (Wqkv, Wm, W1, W2), reused by the final projection
+constexpr size_t kSplitElems = (size_t)256 * 768 + 256 * 256 + 512 * 512 + 512 * 256;
 
 __host__ SgLayout sg_layout(int P, int kmax) {
     SgLayout L{};
@@ -538,6 +891,7 @@ __host__ SgLayout sg_layout(int P, int kmax) {
     L.T1 = take(S * kD * 4);
     L.T2 = take(S * kD * 4);
     L.qkv = take(S * 768 * 4);
+    L.kvp = take(S * 2 * kD * 3 * sizeof(__bf16));  // key and value planes of the current layer
     L.att = take(S * kD * 4);
     L.msg = take(S * kD * 4);
     L.hid = take(S * 512 * 4);
@@ -548,6 +902,7 @@ __host__ SgLayout sg_layout(int P, int kmax) {
     L.idx0 = take((size_t)P * kmax * 4);
     L.idx1 = take((size_t)P * kmax * 4);
     L.cnt = take((size_t)2 * P * 4);
+    L.wsplit = take(kSplitElems * 3 * sizeof(__bf16));
     L.total = o;
     return L;
 }
@@ -555,6 +910,34 @@ __host__ SgLayout sg_layout(int P, int kmax) {
 hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
     const dim3 grid((unsigned)((g.N + 63) / 64), (unsigned)((g.M + 63) / 64), (unsigned)batches);
     hipLaunchKernelGGL(sg_gemm_kernel, grid, dim3(kGemmThreads), 0, stream, g);
+    return hipGetLastError();
+}
+
+hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
+    const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + kG3Tile - 1) / kG3Tile),
+                    (unsigned)batches);
+    hipLaunchKernelGGL(sg_gemm3_kernel, grid, dim3(256), 0, stream, g);
+    return hipGetLastError();
+}
+
+// Y[z] = A[z] W (+ bias) with W's planes Wp ([3][N][K]) for every (pair, side) block
+Gemm3Args side_gemm3(const float* A, int lda, const __bf16* Wp, int K, int N, const float* bias, float* C, int ldc,
+                     int kmax) {
+    Gemm3Args g{};
+    g.A = A; g.lda = lda; g.a_batch = (long)kmax * lda;
+    g.A2 = nullptr; g.Ksplit = K;
+    g.Bp = Wp;
+    g.bias = bias; g.alpha = 1.0f;
+    g.C = C; g.ldc = ldc; g.c_batch = (long)kmax * ldc;
+    g.M = kmax; g.N = N; g.K = K;
+    return g;
+}
+
+hipError_t split_weights(const SplitJobs& jobs, hipStream_t stream) {
+    long most = 0;
+    for (int i = 0; i < 4; ++i)
+        if (jobs.j[i].W) most = std::max(most, (long)jobs.j[i].K * jobs.j[i].N);
+    hipLaunchKernelGGL(sg_split_weights_kernel, dim3((unsigned)((most + 255) / 256), 4), dim3(256), 0, stream, jobs);
     return hipGetLastError();
 }
 
@@ -600,6 +983,8 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
     float* T1 = (float*)(ws + L.T1);
     float* T2 = (float*)(ws + L.T2);
     float* qkv = (float*)(ws + L.qkv);
+    __bf16* kvp = (__bf16*)(ws + L.kvp);
+    const long kv_batch = (long)2 * 3 * kD * kmax;
     float* att = (float*)(ws + L.att);
     float* msg = (float*)(ws + L.msg);
     float* hid = (float*)(ws + L.hid);
@@ -610,6 +995,11 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
     int* idx0 = (int*)(ws + L.idx0);
     int* idx1 = (int*)(ws + L.idx1);
     int* side_counts = (int*)(ws + L.cnt);
+    __bf16* wsp = (__bf16*)(ws + L.wsplit);
+    __bf16* Pqkv = wsp;                        // [3][768][256]
+    __bf16* Pm = Pqkv + 3 * (size_t)768 * 256;  // [3][256][256]
+    __bf16* P1 = Pm + 3 * (size_t)256 * 256;    // [3][512][512]
+    __bf16* P2 = P1 + 3 * (size_t)512 * 512;    // [3][256][512]
     const int S = 2 * n_pairs;
     hipLaunchKernelGGL(sg_prepare_kernel, dim3((kmax + 255) / 256, S), dim3(256), 0, stream, d_kp, d_scores, d_desc,
                        d_counts, d_image_hw, d_pairs, kmax, enc_in, X, side_counts);
@@ -651,12 +1041,18 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
         const float* W2 = h1 + 512;
         const float* b2 = W2 + 512 * 256;
         w += kLayerFloats;
-        GTSFM_CHECK_HIP(run_gemm(side_gemm(X, kD, Wqkv, kD, 768, bqkv, qkv, 768, kmax), S, stream));
-        hipLaunchKernelGGL(sg_attention_kernel, dim3(kmax / 64, kHeads, S), dim3(256), 0, stream, qkv, side_counts,
-                           kmax, l & 1, att);
+        GTSFM_CHECK_HIP(split_weights(SplitJobs{{{Wqkv, Pqkv, kD, 768}, {Wm, Pm, kD, kD}, {W1, P1, 512, 512},
+                                                 {W2, P2, 512, kD}}},
+                                      stream));
+        Gemm3Args gq = side_gemm3(X, kD, Pqkv, kD, 768, bqkv, qkv, 768, kmax);
+        gq.kv = kvp;
+        gq.kv_batch = kv_batch;
+        GTSFM_CHECK_HIP(run_gemm3(gq, S, stream));
+        hipLaunchKernelGGL(sg_attention3_kernel, dim3(kmax / 64, kHeads, S), dim3(256), 0, stream, qkv, kvp, kv_batch,
+                           side_counts, kmax, l & 1, att);
         GTSFM_CHECK_HIP(hipGetLastError());
-        GTSFM_CHECK_HIP(run_gemm(side_gemm(att, kD, Wm, kD, kD, bm, msg, kD, kmax), S, stream));
-        GemmArgs g1 = side_gemm(X, kD, W1, 512, 512, b1, hid, 512, kmax);
+        GTSFM_CHECK_HIP(run_gemm3(side_gemm3(att, kD, Pm, kD, kD, bm, msg, kD, kmax), S, stream));
+        Gemm3Args g1 = side_gemm3(X, kD, P1, 512, 512, b1, hid, 512, kmax);
         g1.Ksplit = kD;  // cat([x, message])
         g1.A2 = msg;
         g1.lda2 = kD;
@@ -664,27 +1060,28 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
         g1.bn_scale = s1;
         g1.bn_shift = h1;
         g1.relu = 1;
-        GTSFM_CHECK_HIP(run_gemm(g1, S, stream));
-        GemmArgs g2 = side_gemm(hid, 512, W2, 512, kD, b2, X, kD, kmax);
+        GTSFM_CHECK_HIP(run_gemm3(g1, S, stream));
+        Gemm3Args g2 = side_gemm3(hid, 512, P2, 512, kD, b2, X, kD, kmax);
         g2.residual = 1;  // desc + delta
-        GTSFM_CHECK_HIP(run_gemm(g2, S, stream));
+        GTSFM_CHECK_HIP(run_gemm3(g2, S, stream));
     }
     // final projection, scores = mdesc0^T mdesc1 / 16 into the coupling matrix interior
     const float* Wf = w;
     const float* bf = Wf + 256 * 256;
     const float* bin = bf + 256;
-    GTSFM_CHECK_HIP(run_gemm(side_gemm(X, kD, Wf, kD, kD, bf, T1, kD, kmax), S, stream));
+    GTSFM_CHECK_HIP(split_weights(SplitJobs{{{Wf, Pm, kD, kD}, {}, {}, {}}}, stream));
+    GTSFM_CHECK_HIP(run_gemm3(side_gemm3(X, kD, Pm, kD, kD, bf, T1, kD, kmax), S, stream));
     const long ld = kmax + 1;
     {
-        GemmArgs g{};
+        Gemm3Args g{};
         g.A = T1; g.lda = kD; g.a_batch = (long)2 * kmax * kD;
         g.Ksplit = kD;
-        g.B = T1 + (long)kmax * kD; g.ldb = kD; g.b_batch = (long)2 * kmax * kD; g.b_trans = 1;
+        g.Bt = T1 + (long)kmax * kD; g.ldb = kD; g.b_batch = (long)2 * kmax * kD;
         g.alpha = 1.0f / 16.0f;
         g.C = Z; g.ldc = ld; g.c_batch = ld * ld;
         g.M = kmax; g.N = kmax; g.K = kD;
         g.m_lim = side_counts; g.n_lim = side_counts; g.lim_stride = 2;
-        GTSFM_CHECK_HIP(run_gemm(g, n_pairs, stream));
+        GTSFM_CHECK_HIP(run_gemm3(g, n_pairs, stream));
     }
     hipLaunchKernelGGL(sk_init_kernel, dim3((kmax + 256) / 256, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
                        bin, u, v);

@@ -224,6 +224,192 @@ __global__ __launch_bounds__(kConvThreads) void conv_mfma_kernel(ConvArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ implicit-GEMM convolution, fp32-accurate bf16
+// The same tiling as conv_mfma_kernel, restated on v_mfma_f32_32x32x16_bf16 with the three-plane split products of
+// superglue.hip's sg_gemm3_kernel (x = x_h + x_m + x_l in bf16; six plane products per MFMA step; the dropped ones
+// are below 2^-23 |a b|): one 16-channel tap is one MFMA k-step of 16 instead of eight 32x32x2 f32 steps. The input
+// patch is split as it is staged ([plane][pixel][16] bf16); the weights are split once per call into
+// [tap][Cin / 16][plane][cout][16] (sp_split_weights_kernel) and staged as [tap][plane][64 couts][16]. A lane's
+// 16-byte fragment (8 channels) sits in half kh ^ ((row >> 3) & 1) of its 32-byte row, so the 16 rows one ds_read_b128
+// phase touches fall on distinct banks.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void sp_split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+    h = (__bf16)x;
+    const float r = x - (float)h;
+    m = (__bf16)r;
+    l = (__bf16)(r - (float)m);
+}
+
+__device__ __forceinline__ int swz16(int row, int half) { return 8 * (half ^ ((row >> 3) & 1)); }
+
+template <int KS, bool POOL>
+__global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, const __bf16* __restrict__ w3) {
+    constexpr int R = KS / 2;
+    constexpr int PH = 2 + 2 * R, PW = 32 + 2 * R;
+    constexpr int kPU = PH * PW * 2;             // patch staging units (pixel, 8-channel half)
+    constexpr int kWU = KS * KS * 3 * 64 * 2;    // weight staging units (tap, plane, cout, half)
+    constexpr int kNP = (kPU + kConvThreads - 1) / kConvThreads;
+    constexpr int kNW = (kWU + kConvThreads - 1) / kConvThreads;
+    __shared__ __attribute__((aligned(16))) __bf16 patch[3][PH * PW][16];
+    __shared__ __attribute__((aligned(16))) __bf16 wt[KS * KS][3][64][16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ct = blockIdx.y;
+    int t = blockIdx.x;
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    const int ty = t % a.tiles_y;
+    const int img = t / a.tiles_y;
+    const int y0 = 2 * ty, x0 = 32 * tx;
+    const int wx = wave & 1, wn = wave >> 1;
+    const int i = lane & 31, kh = lane >> 5;
+    const int prow = i >> 4, pcol = 16 * wx + (i & 15);
+    const int ncol = (lane & 31) + 32 * wn;
+    const float* inb = a.in + (size_t)img * a.Hi * a.Wi * a.in_cstride + a.in_c0;
+    f32x16 acc = {};
+    f32x4_t pv[kNP][2];
+    u32x4 wv[kNW];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int u = 0; u < kNP; ++u) {
+            const int e = tid + u * kConvThreads;
+            const int pix = e >> 1, hf = e & 1;
+            const int py = pix / PW, px = pix - py * PW;
+            const int gy = y0 - R + py, gx = x0 - R + px;
+            pv[u][0] = pv[u][1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            if (e < kPU && gy >= 0 && gy < a.Hi && gx >= 0 && gx < a.Wi) {
+                const float* src = inb + ((size_t)gy * a.Wi + gx) * a.in_cstride + c0 + 8 * hf;
+                pv[u][0] = *(const f32x4_t*)src;
+                pv[u][1] = *(const f32x4_t*)(src + 4);
+            }
+        }
+        const int chunk = c0 / kCinChunk, nchunk = a.Cin / kCinChunk;
+#pragma unroll
+        for (int u = 0; u < kNW; ++u) {
+            const int e = tid + u * kConvThreads;
+            if (e < kWU) {
+                const int hf = e & 1, co = (e >> 1) & 63, p = (e >> 7) % 3, kk = (e >> 7) / 3;
+                wv[u] = *(const u32x4*)(w3 + ((((size_t)kk * nchunk + chunk) * 3 + p) * a.cout_pad + 64 * ct + co) * 16 +
+                                        8 * hf);
+            }
+        }
+    };
+    auto stash = [&]() {
+#pragma unroll
+        for (int u = 0; u < kNP; ++u) {
+            const int e = tid + u * kConvThreads;
+            if (e < kPU) {
+                const int pix = e >> 1, hf = e & 1;
+                bf16x8 h, m, l;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    __bf16 hh, mm, ll;
+                    sp_split3(pv[u][j >> 2][j & 3], hh, mm, ll);
+                    h[j] = hh;
+                    m[j] = mm;
+                    l[j] = ll;
+                }
+                const int o = swz16(pix, hf);
+                *(bf16x8*)&patch[0][pix][o] = h;
+                *(bf16x8*)&patch[1][pix][o] = m;
+                *(bf16x8*)&patch[2][pix][o] = l;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kNW; ++u) {
+            const int e = tid + u * kConvThreads;
+            if (e < kWU) {
+                const int hf = e & 1, co = (e >> 1) & 63, p = (e >> 7) % 3, kk = (e >> 7) / 3;
+                *(u32x4*)&wt[kk][p][co][swz16(co, hf)] = wv[u];
+            }
+        }
+    };
+    load(0);
+    stash();
+    __syncthreads();
+    for (int c0 = 0; c0 < a.Cin; c0 += kCinChunk) {
+        const bool more = c0 + kCinChunk < a.Cin;
+        if (more) load(c0 + kCinChunk);
+#pragma unroll
+        for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < KS; ++kx) {
+                const int pix = (prow + ky) * PW + pcol + kx, kk = ky * KS + kx;
+                const int po = swz16(pix, kh), wo = swz16(ncol, kh);
+                const bf16x8 a0 = *(const bf16x8*)&patch[0][pix][po];
+                const bf16x8 a1 = *(const bf16x8*)&patch[1][pix][po];
+                const bf16x8 a2 = *(const bf16x8*)&patch[2][pix][po];
+                const bf16x8 b0 = *(const bf16x8*)&wt[kk][0][ncol][wo];
+                const bf16x8 b1 = *(const bf16x8*)&wt[kk][1][ncol][wo];
+                const bf16x8 b2 = *(const bf16x8*)&wt[kk][2][ncol][wo];
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+            }
+        if (!more) break;
+        __syncthreads();
+        stash();
+        __syncthreads();
+    }
+    // epilogue (conv_mfma_kernel's): acc[g] = conv output at tile pixel 4 kh + (g & 3) + 8 (g >> 2), channel ncol
+    const int co = 64 * ct + ncol;
+    if (co >= a.Cout) return;
+    const float b = a.bias[co];
+    float* outb = a.out + a.out_c0 + co;
+    if constexpr (POOL) {
+        const int Ho = a.Hi / 2, Wo = a.Wi / 2;
+        const int py = y0 / 2;
+        if (py >= Ho) return;
+#pragma unroll
+        for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+            for (int rp = 0; rp < 2; ++rp) {
+                const int g0 = 4 * qa + 2 * rp, g1 = 4 * (qa + 2) + 2 * rp;
+                float v = fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g1], acc[g1 + 1]));
+                v = v + b;
+                if (a.relu) v = v > 0.0f ? v : 0.0f;
+                const int px = x0 / 2 + 8 * wx + 4 * qa + 2 * kh + rp;
+                if (px < Wo) outb[(((size_t)img * Ho + py) * Wo + px) * a.out_cstride] = v;
+            }
+    } else {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int ip = 4 * kh + (g & 3) + 8 * (g >> 2);
+            const int y = y0 + (ip >> 4), x = x0 + 16 * wx + (ip & 15);
+            if (y >= a.Hi || x >= a.Wi) continue;
+            float v = acc[g] + b;
+            if (a.relu) v = v > 0.0f ? v : 0.0f;
+            outb[(((size_t)img * a.Hi + y) * a.Wi + x) * a.out_cstride] = v;
+        }
+    }
+}
+
+// fp32 weights [tap][Cin][cout_pad] of layers L1B..LDB -> bf16 planes [tap][Cin / 16][plane][cout_pad][16] at
+// sp_w3_offset(layer); blockIdx.y = layer - 1
+__host__ __device__ constexpr size_t sp_w3_offset(int l) {
+    size_t o = 0;
+    for (int i = 1; i < l; ++i) o += (size_t)3 * kSp[i].k * kSp[i].k * kSp[i].cin * kSp[i].cout_pad;
+    return o;
+}
+
+__global__ void sp_split_weights_kernel(const float* __restrict__ blob, __bf16* __restrict__ w3) {
+    const int l = blockIdx.y + 1;
+    const int KK = kSp[l].k * kSp[l].k, Cin = kSp[l].cin, Cp = kSp[l].cout_pad;
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (size_t)KK * Cin * Cp) return;
+    const int co = (int)(e % Cp), ci = (int)((e / Cp) % Cin), kk = (int)(e / ((size_t)Cp * Cin));
+    __bf16 pl[3];
+    sp_split3(blob[sp_layer_offset(l) + e], pl[0], pl[1], pl[2]);
+    __bf16* out = w3 + sp_w3_offset(l);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+        out[((((size_t)kk * (Cin / kCinChunk) + ci / kCinChunk) * 3 + p) * Cp + co) * 16 + ci % kCinChunk] = pl[p];
+}
+
 // ------------------------------------------------------------------ dense scores: softmax over 65, depth-to-space
 // superpoint.py:168-172: scores = softmax(convPb)[:, :64] reshaped so cell (cy, cx) channel c -> pixel
 // (8 cy + c / 8, 8 cx + c % 8).
@@ -525,7 +711,7 @@ __host__ SpDims sp_dims(int H, int W) {
 }
 
 struct SpLayout {
-    size_t buf0, buf1, logits, maps, cand_idx, cand_score, rowcnt, rowoff, ndet, total;
+    size_t buf0, buf1, logits, maps, cand_idx, cand_score, rowcnt, rowoff, ndet, w3, total;
     size_t map_floats;
     int cap;
 };
@@ -548,13 +734,15 @@ __host__ SpLayout sp_layout(int n, const SpDims& d) {
     L.rowcnt = o; o += gtsfm_align_up((size_t)n * (d.Hs + 1) * 4, 256);
     L.rowoff = o; o += gtsfm_align_up((size_t)n * (d.Hs + 1) * 4, 256);
     L.ndet = o; o += gtsfm_align_up((size_t)n * 4, 256);
+    L.w3 = o; o += gtsfm_align_up(sp_w3_offset(kSpLayers) * sizeof(__bf16), 256);
     L.total = o;
     return L;
 }
 
 template <int KS, bool POOL>
 hipError_t launch_conv(int n, const float* in, int Hi, int Wi, int in_cstride, int in_c0, int Cin, const float* blob,
-                       int layer, float* out, int out_cstride, int out_c0, int Cout, hipStream_t stream) {
+                       const __bf16* w3, int layer, float* out, int out_cstride, int out_c0, int Cout,
+                       hipStream_t stream) {
     ConvArgs a;
     a.in = in; a.Hi = Hi; a.Wi = Wi; a.in_cstride = in_cstride; a.in_c0 = in_c0; a.Cin = Cin;
     a.w = blob + sp_layer_offset(layer);
@@ -566,7 +754,7 @@ hipError_t launch_conv(int n, const float* in, int Hi, int Wi, int in_cstride, i
     if (POOL) a.tiles_y = (Hi / 2);  // pooled rows only (MaxPool2d floors; an odd last conv row is dropped)
     if (a.tiles_x == 0 || a.tiles_y == 0) return hipSuccess;
     const dim3 grid((unsigned)(a.tiles_x * a.tiles_y * n), (unsigned)((Cout + 63) / 64));
-    hipLaunchKernelGGL((conv_mfma_kernel<KS, POOL>), grid, dim3(kConvThreads), 0, stream, a);
+    hipLaunchKernelGGL((conv3_kernel<KS, POOL>), grid, dim3(kConvThreads), 0, stream, a, w3 + sp_w3_offset(layer));
     return hipGetLastError();
 }
 
@@ -605,6 +793,15 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, in
         return GTSFM_OK;
     }
     const float* blob = d_weights;
+    __bf16* w3 = (__bf16*)(ws + L.w3);
+    {
+        size_t most = 0;
+        for (int l = 1; l < kSpLayers; ++l)
+            most = std::max(most, (size_t)kSp[l].k * kSp[l].k * kSp[l].cin * kSp[l].cout_pad);
+        hipLaunchKernelGGL(sp_split_weights_kernel, dim3((unsigned)((most + 255) / 256), kSpLayers - 1), dim3(256), 0,
+                           stream, blob, w3);
+        GTSFM_CHECK_HIP(hipGetLastError());
+    }
     // shared encoder (superpoint.py:147-158)
     {
         const size_t pix = (size_t)n * H * W;
@@ -612,15 +809,15 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, in
                            W, C, blob + sp_layer_offset(L1A), buf0);
         GTSFM_CHECK_HIP(hipGetLastError());
     }
-    GTSFM_CHECK_HIP((launch_conv<3, true>(n, buf0, d.H, d.W, 64, 0, 64, blob, L1B, buf1, 64, 0, 64, stream)));
-    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H2, d.W2, 64, 0, 64, blob, L2A, buf0, 64, 0, 64, stream)));
-    GTSFM_CHECK_HIP((launch_conv<3, true>(n, buf0, d.H2, d.W2, 64, 0, 64, blob, L2B, buf1, 64, 0, 64, stream)));
-    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H4, d.W4, 64, 0, 64, blob, L3A, buf0, 128, 0, 128, stream)));
-    GTSFM_CHECK_HIP((launch_conv<3, true>(n, buf0, d.H4, d.W4, 128, 0, 128, blob, L3B, buf1, 128, 0, 128, stream)));
-    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H8, d.W8, 128, 0, 128, blob, L4A, buf0, 128, 0, 128, stream)));
-    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf0, d.H8, d.W8, 128, 0, 128, blob, L4B, buf1, 128, 0, 128, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, true>(n, buf0, d.H, d.W, 64, 0, 64, blob, w3, L1B, buf1, 64, 0, 64, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H2, d.W2, 64, 0, 64, blob, w3, L2A, buf0, 64, 0, 64, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, true>(n, buf0, d.H2, d.W2, 64, 0, 64, blob, w3, L2B, buf1, 64, 0, 64, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H4, d.W4, 64, 0, 64, blob, w3, L3A, buf0, 128, 0, 128, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, true>(n, buf0, d.H4, d.W4, 128, 0, 128, blob, w3, L3B, buf1, 128, 0, 128, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H8, d.W8, 128, 0, 128, blob, w3, L4A, buf0, 128, 0, 128, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf0, d.H8, d.W8, 128, 0, 128, blob, w3, L4B, buf1, 128, 0, 128, stream)));
     // heads: [convPa | convDa] in one 3x3 (128 -> 512), then the two 1x1s (superpoint.py:161-162, 190-191)
-    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H8, d.W8, 128, 0, 128, blob, LHEAD, buf0, 512, 0, 512, stream)));
+    GTSFM_CHECK_HIP((launch_conv<3, false>(n, buf1, d.H8, d.W8, 128, 0, 128, blob, w3, LHEAD, buf0, 512, 0, 512, stream)));
     // convPb: no ReLU; convDb: no ReLU
     auto conv1x1 = [&](int layer, int in_c0, float* out, int out_cstride, int Cout) -> hipError_t {
         ConvArgs a;
@@ -632,7 +829,7 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, in
         a.tiles_x = (d.W8 + 31) / 32;
         a.tiles_y = (d.H8 + 1) / 2;
         const dim3 grid((unsigned)(a.tiles_x * a.tiles_y * n), (unsigned)((Cout + 63) / 64));
-        hipLaunchKernelGGL((conv_mfma_kernel<1, false>), grid, dim3(kConvThreads), 0, stream, a);
+        hipLaunchKernelGGL((conv3_kernel<1, false>), grid, dim3(kConvThreads), 0, stream, a, w3 + sp_w3_offset(layer));
         return hipGetLastError();
     };
     GTSFM_CHECK_HIP(conv1x1(LPB, 0, logits, 128, 65));
