@@ -109,22 +109,19 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 // The solver's dynamically indexed arrays live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit
 // consecutive words, so every access is bank-conflict free, and nothing spills to scratch. The solver runs in two
 // kernels so each one's workgroup holds only its own phase's arrays:
-//   stage 1 (sample, 5x9 nullspace, 10x20 Gauss-Jordan), two lanes per hypothesis: Q (45) + column permutation
-//       (9 ints) | rows 2..9 of this lane's half of A (8 x 10; rows 0, 1 in registers) = 40 KB per 64-lane
-//       workgroup (four per CU);
+//   stage 1 (sample, 5x9 null space in registers, 10x20 Gauss-Jordan), two lanes per hypothesis: rows 2..9 of this
+//       lane's half of A (8 x 10; rows 0, 1 in registers) = 40 KB per 64-lane workgroup (four per CU);
 //   stage 2 (det B(z), Sturm chain, isolation, bisection, E): the chain is built in registers (generic degrees;
 //       a private-memory fallback for degree drops), the isolating intervals are selected into registers, and LDS
 //       holds only the isolation stack as left ends (24 doubles + 24 count bytes) = 13.5 KB per workgroup, so
 //       with <= 256 registers two waves share a SIMD.
 constexpr int kLanes = 64;
 constexpr int kRegRows = 2;   // rows of the lane's half of A kept in registers (the rest in LDS)
-constexpr int kUnion = 10 * (10 - kRegRows);  // stage-1 doubles per lane: Q (45) + V (9) + perm ints (slot 64) | A rows 2..9
-constexpr int kPermSlot = 64; // double slot where the nullspace's column permutation (9 ints) starts
+constexpr int kUnion = 10 * (10 - kRegRows);  // stage-1 doubles per lane: A rows 2..9 of the lane's half
 constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
 constexpr int kRootDbl = kStack;  // stage-2 doubles per lane: the isolation stack's left ends
 constexpr int kRootB = kStack;    // stage-2 bytes per lane: the stack's Sturm sign-variation counts
 constexpr size_t kSolveLds = (size_t)kUnion * kLanes * sizeof(double);
-static_assert(kPermSlot >= 54 && kPermSlot * 8 + 9 * 4 <= kUnion * 8, "permutation ints overlap Q/V or overflow");
 constexpr size_t kRootLds = (size_t)kRootDbl * kLanes * sizeof(double) + (size_t)kRootB * kLanes;
 
 template <typename T>
@@ -158,13 +155,10 @@ __device__ int prem(LaneArr<double> a, int da, LaneArr<double> b, int db, LaneAr
 
 struct SolverMem {
     LaneArr<double> u;  // kUnion doubles
-    LaneArr<int> iv;    // 9 ints inside u, past Q and V (nullspace only)
 };
 
 __device__ __forceinline__ SolverMem solver_mem(unsigned char* smem, int lane) {
-    double* d = (double*)smem;
-    int* iv = (int*)(smem + (size_t)kPermSlot * kLanes * sizeof(double));
-    return SolverMem{LaneArr<double>{d + lane}, LaneArr<int>{iv + lane}};
+    return SolverMem{LaneArr<double>{(double*)smem + lane}};
 }
 
 struct RootMem {
@@ -436,49 +430,60 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, double (&
 }
 
 // ------------------------------------------------------------------ Nister 5-point (one lane, arrays in LDS)
-__device__ bool nullspace_5x9(const double* x1, const double* x2, SolverMem m, double N[4][9]) {
-    LaneArr<double> q = m.u;     // [5][9]
-    LaneArr<double> v = m.u.at(45);
-    LaneArr<int> col = m.iv;
+// Null space of the 5 x 9 epipolar system (oracle/ransac.c nullspace_5x9): Householder QR of its transpose,
+// M^T = H_0 ... H_4 [R; 0], then columns 5..8 of H_0 ... H_4. Static indices only, so it stays in registers.
+__device__ bool nullspace_5x9(const double* x1, const double* x2, double N[4][9]) {
+    double a[5][9], v[5][9], beta[5];
+#pragma unroll
     for (int i = 0; i < 5; ++i) {
         const double u1 = x1[2 * i], v1 = x1[2 * i + 1], u2 = x2[2 * i], v2 = x2[2 * i + 1];
-        q[9 * i + 0] = u2 * u1; q[9 * i + 1] = u2 * v1; q[9 * i + 2] = u2;
-        q[9 * i + 3] = v2 * u1; q[9 * i + 4] = v2 * v1; q[9 * i + 5] = v2;
-        q[9 * i + 6] = u1; q[9 * i + 7] = v1; q[9 * i + 8] = 1.0;
+        a[i][0] = u2 * u1; a[i][1] = u2 * v1; a[i][2] = u2;
+        a[i][3] = v2 * u1; a[i][4] = v2 * v1; a[i][5] = v2;
+        a[i][6] = u1; a[i][7] = v1; a[i][8] = 1.0;
     }
-    for (int j = 0; j < 9; ++j) col[j] = j;
-    for (int r = 0; r < 5; ++r) {
-        int pr = r, pc = r;
-        double best = -1.0;
-        for (int i = r; i < 5; ++i)
-            for (int j = r; j < 9; ++j)
-                if (fabs(q[9 * i + j]) > best) { best = fabs(q[9 * i + j]); pr = i; pc = j; }
-        if (best < 1e-12) return false;
-        if (pr != r)
-            for (int j = 0; j < 9; ++j) { const double tt = q[9 * r + j]; q[9 * r + j] = q[9 * pr + j]; q[9 * pr + j] = tt; }
-        if (pc != r) {
-            for (int i = 0; i < 5; ++i) { const double tt = q[9 * i + r]; q[9 * i + r] = q[9 * i + pc]; q[9 * i + pc] = tt; }
-            const int tt = col[r]; col[r] = col[pc]; col[pc] = tt;
-        }
-        const double inv = 1.0 / q[9 * r + r];
-        for (int j = 0; j < 9; ++j) q[9 * r + j] *= inv;
-        for (int i = 0; i < 5; ++i) {
-            if (i == r) continue;
-            const double f = q[9 * i + r];
-            for (int j = 0; j < 9; ++j) q[9 * i + j] = fma(-f, q[9 * r + j], q[9 * i + j]);
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        double sq = 0.0;
+#pragma unroll
+        for (int r = k; r < 9; ++r) sq = fma(a[k][r], a[k][r], sq);
+        const double nrm = sqrt(sq);
+        ok = ok && !(nrm < 1e-12);
+        const double alpha = a[k][k] >= 0.0 ? -nrm : nrm;
+#pragma unroll
+        for (int r = k; r < 9; ++r) v[k][r] = a[k][r];
+        v[k][k] = v[k][k] - alpha;
+        double vv = 0.0;
+#pragma unroll
+        for (int r = k; r < 9; ++r) vv = fma(v[k][r], v[k][r], vv);
+        beta[k] = 2.0 / vv;
+#pragma unroll
+        for (int c = k + 1; c < 5; ++c) {
+            double d = 0.0;
+#pragma unroll
+            for (int r = k; r < 9; ++r) d = fma(v[k][r], a[c][r], d);
+            d = d * beta[k];
+#pragma unroll
+            for (int r = k; r < 9; ++r) a[c][r] = fma(-d, v[k][r], a[c][r]);
         }
     }
+    if (!ok) return false;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        for (int j = 0; j < 9; ++j) v[j] = 0.0;
-        v[col[5 + k]] = 1.0;
-        for (int r = 0; r < 5; ++r) v[col[r]] = -q[9 * r + 5 + k];
-        double nrm = 0.0;
+    for (int n = 0; n < 4; ++n) {
+        double y[9];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) nrm = fma(v[j], v[j], nrm);
-        nrm = sqrt(nrm);
+        for (int j = 0; j < 9; ++j) y[j] = j == 5 + n ? 1.0 : 0.0;
 #pragma unroll
-        for (int j = 0; j < 9; ++j) N[k][j] = v[j] / nrm;
+        for (int k = 4; k >= 0; --k) {
+            double d = 0.0;
+#pragma unroll
+            for (int r = k; r < 9; ++r) d = fma(v[k][r], y[r], d);
+            d = d * beta[k];
+#pragma unroll
+            for (int r = k; r < 9; ++r) y[r] = fma(-d, v[k][r], y[r]);
+        }
+#pragma unroll
+        for (int j = 0; j < 9; ++j) N[n][j] = y[j];
     }
     return true;
 }
@@ -502,7 +507,7 @@ constexpr int kStageVals = 6 * 10 + 4 * 9;  // doubles handed from stage 1 to st
 __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem m, int part, double N[4][9],
                                   double Rt[6][10]) {
     RPROF_DECL
-    if (!nullspace_5x9(x1, x2, m, N)) return false;
+    if (!nullspace_5x9(x1, x2, N)) return false;
     RPROF(1);
     double E[9][4];
 #pragma unroll

@@ -253,41 +253,42 @@ static int real_roots(const double* pin, int deg, double* roots) {
 }
 
 /* ------------------------------------------------------------------ 5-point solver */
-/* Gauss-Jordan with full pivoting of the 5x9 system; fills the 4 null-space vectors. Returns 0 if degenerate. */
-static int nullspace_5x9(const double q_in[5][9], double N[4][9]) {
-    double q[5][9];
-    int col[9];
-    memcpy(q, q_in, sizeof(q));
-    for (int j = 0; j < 9; ++j) col[j] = j;
-    for (int r = 0; r < 5; ++r) {
-        int pr = r, pc = r;
-        double best = -1.0;
-        for (int i = r; i < 5; ++i)
-            for (int j = r; j < 9; ++j)
-                if (fabs(q[i][j]) > best) { best = fabs(q[i][j]); pr = i; pc = j; }
-        if (best < 1e-12) return 0;
-        if (pr != r)
-            for (int j = 0; j < 9; ++j) { double t = q[r][j]; q[r][j] = q[pr][j]; q[pr][j] = t; }
-        if (pc != r) {
-            for (int i = 0; i < 5; ++i) { double t = q[i][r]; q[i][r] = q[i][pc]; q[i][pc] = t; }
-            int t = col[r]; col[r] = col[pc]; col[pc] = t;
-        }
-        const double inv = 1.0 / q[r][r];
-        for (int j = 0; j < 9; ++j) q[r][j] *= inv;
-        for (int i = 0; i < 5; ++i) {
-            if (i == r) continue;
-            const double f = q[i][r];
-            for (int j = 0; j < 9; ++j) q[i][j] = fma(-f, q[r][j], q[i][j]);
+/* Null space of the 5 x 9 epipolar system: Householder QR of its transpose, M^T (9 x 5) = H_0 H_1 ... H_4 [R; 0],
+ * H_k = I - beta_k v_k v_k^T acting on entries k..8; columns 5..8 of H_0 ... H_4 (each built by applying H_4 first)
+ * are an orthonormal basis of null(M). Every index is static, so the device keeps the whole factorisation in
+ * registers (gtsfm_amd/csrc/ransac.hip nullspace_5x9, the same operations). Returns 0 when a column's remaining norm
+ * is below 1e-12 (rank < 5: a degenerate sample). */
+static int nullspace_5x9(const double q[5][9], double N[4][9]) {
+    double a[5][9], v[5][9], beta[5];
+    memcpy(a, q, sizeof(a)); /* a[c][r] = M^T[r][c]: column c of M^T is row c of M */
+    for (int k = 0; k < 5; ++k) {
+        double s = 0.0;
+        for (int r = k; r < 9; ++r) s = fma(a[k][r], a[k][r], s);
+        const double nrm = sqrt(s);
+        if (nrm < 1e-12) return 0;
+        const double alpha = a[k][k] >= 0.0 ? -nrm : nrm;
+        for (int r = k; r < 9; ++r) v[k][r] = a[k][r];
+        v[k][k] = v[k][k] - alpha;
+        double vv = 0.0;
+        for (int r = k; r < 9; ++r) vv = fma(v[k][r], v[k][r], vv);
+        beta[k] = 2.0 / vv;
+        for (int c = k + 1; c < 5; ++c) {
+            double d = 0.0;
+            for (int r = k; r < 9; ++r) d = fma(v[k][r], a[c][r], d);
+            d = d * beta[k];
+            for (int r = k; r < 9; ++r) a[c][r] = fma(-d, v[k][r], a[c][r]);
         }
     }
-    for (int k = 0; k < 4; ++k) {
-        double v[9] = {0};
-        v[col[5 + k]] = 1.0;
-        for (int r = 0; r < 5; ++r) v[col[r]] = -q[r][5 + k];
-        double nrm = 0.0;
-        for (int j = 0; j < 9; ++j) nrm = fma(v[j], v[j], nrm);
-        nrm = sqrt(nrm);
-        for (int j = 0; j < 9; ++j) N[k][j] = v[j] / nrm;
+    for (int n = 0; n < 4; ++n) {
+        double y[9] = {0};
+        y[5 + n] = 1.0;
+        for (int k = 4; k >= 0; --k) {
+            double d = 0.0;
+            for (int r = k; r < 9; ++r) d = fma(v[k][r], y[r], d);
+            d = d * beta[k];
+            for (int r = k; r < 9; ++r) y[r] = fma(-d, v[k][r], y[r]);
+        }
+        for (int j = 0; j < 9; ++j) N[n][j] = y[j];
     }
     return 1;
 }
