@@ -41,7 +41,7 @@ __device__ unsigned long long g_rprof[32];
 #define RPROF_COUNT(k, v) do { } while (0)
 #endif
 
-// The essential-matrix path is compiled without FMA contraction: every fused multiply-add below is an explicit fma()
+// The essential-matrix path is compiled without FMA contraction: every fused multiply-add below is an explicit __builtin_fma()
 // that oracle/ransac.c performs in the same place, so the solver, the refits and recoverPose reproduce the oracle's
 // double arithmetic bit for bit (hypotheses, candidates, scores, the selected model, R and t).
 #pragma clang fp contract(off)
@@ -92,7 +92,7 @@ __device__ __forceinline__ void mul_ll(const double* a, const double* b, double*
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] = fma(a[i], b[j], q[kLL2Q[i][j]]);
+        for (int j = 0; j < 4; ++j) q[kLL2Q[i][j]] = __builtin_fma(a[i], b[j], q[kLL2Q[i][j]]);
 }
 
 // c += s * q*l (oracle addmul_ql); s is 1, -1 or 2, so s * q[i] is exact and every term is one fused multiply-add
@@ -101,7 +101,7 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
     for (int i = 0; i < 10; ++i) {
         const double sq = s * q[i];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = fma(sq, l[j], c[kQL2C[i][j]]);
+        for (int j = 0; j < 4; ++j) c[kQL2C[i][j]] = __builtin_fma(sq, l[j], c[kQL2C[i][j]]);
     }
 }
 
@@ -133,7 +133,7 @@ struct LaneArr {
 
 __device__ __forceinline__ double peval(LaneArr<double> p, int deg, double x) {
     double v = p[deg];
-    for (int i = deg - 1; i >= 0; --i) v = fma(v, x, p[i]);
+    for (int i = deg - 1; i >= 0; --i) v = __builtin_fma(v, x, p[i]);
     return v;
 }
 
@@ -142,7 +142,7 @@ __device__ int prem(LaneArr<double> a, int da, LaneArr<double> b, int db, LaneAr
     for (int i = 0; i <= da; ++i) t[i] = a[i];
     for (int k = da; k >= db; --k) {
         const double f = t[k] / b[db];
-        for (int i = 0; i <= db; ++i) t[k - db + i] = fma(-f, b[i], t[k - db + i]);
+        for (int i = 0; i <= db; ++i) t[k - db + i] = __builtin_fma(-f, b[i], t[k - db + i]);
         t[k] = 0.0;
     }
     int dr = db - 1;
@@ -186,7 +186,7 @@ __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], doubl
         const int len = 11 - k, o = row_off(k);
         double a = R[o + len - 1];
 #pragma unroll
-        for (int i = len - 2; i >= 0; --i) a = fma(a, x, R[o + i]);
+        for (int i = len - 2; i >= 0; --i) a = __builtin_fma(a, x, R[o + i]);
         v[k] = a;
     }
     int c = 0;
@@ -204,14 +204,14 @@ __device__ __forceinline__ int sign_changes_reg(const double (&R)[kChain], doubl
 __device__ __forceinline__ double peval1(const double (&R)[kChain], double x) {
     double a = R[row_off(1) + 9];
 #pragma unroll
-    for (int i = 8; i >= 0; --i) a = fma(a, x, R[row_off(1) + i]);
+    for (int i = 8; i >= 0; --i) a = __builtin_fma(a, x, R[row_off(1) + i]);
     return a;
 }
 
 __device__ __forceinline__ double peval0(const double (&R)[kChain], double x) {
     double a = R[10];
 #pragma unroll
-    for (int i = 9; i >= 0; --i) a = fma(a, x, R[i]);
+    for (int i = 9; i >= 0; --i) a = __builtin_fma(a, x, R[i]);
     return a;
 }
 
@@ -238,7 +238,7 @@ __device__ __forceinline__ void sturm_chain_fallback(const double (&row0)[11], i
         for (int i = 0; i <= da; ++i) t[i] = a[i];
         for (int k = da; k >= db; --k) {
             const double f = t[k] / b[db];
-            for (int i = 0; i <= db; ++i) t[k - db + i] = fma(-f, b[i], t[k - db + i]);
+            for (int i = 0; i <= db; ++i) t[k - db + i] = __builtin_fma(-f, b[i], t[k - db + i]);
             t[k] = 0.0;
         }
         int dr = db - 1;
@@ -298,7 +298,7 @@ __device__ int real_roots(const double (&pin)[11], int deg, RootMem m, double (&
             for (int kk = da; kk >= db; --kk) {
                 const double f = t[kk] / R[ob + db];
 #pragma unroll
-                for (int i = 0; i <= db; ++i) t[kk - db + i] = fma(-f, R[ob + i], t[kk - db + i]);
+                for (int i = 0; i <= db; ++i) t[kk - db + i] = __builtin_fma(-f, R[ob + i], t[kk - db + i]);
                 t[kk] = 0.0;
             }
             double scale = 0.0;
@@ -446,7 +446,7 @@ __device__ bool nullspace_5x9(const double* x1, const double* x2, double N[4][9]
     for (int k = 0; k < 5; ++k) {
         double sq = 0.0;
 #pragma unroll
-        for (int r = k; r < 9; ++r) sq = fma(a[k][r], a[k][r], sq);
+        for (int r = k; r < 9; ++r) sq = __builtin_fma(a[k][r], a[k][r], sq);
         const double nrm = sqrt(sq);
         ok = ok && !(nrm < 1e-12);
         const double alpha = a[k][k] >= 0.0 ? -nrm : nrm;
@@ -455,16 +455,16 @@ __device__ bool nullspace_5x9(const double* x1, const double* x2, double N[4][9]
         v[k][k] = v[k][k] - alpha;
         double vv = 0.0;
 #pragma unroll
-        for (int r = k; r < 9; ++r) vv = fma(v[k][r], v[k][r], vv);
+        for (int r = k; r < 9; ++r) vv = __builtin_fma(v[k][r], v[k][r], vv);
         beta[k] = 2.0 / vv;
 #pragma unroll
         for (int c = k + 1; c < 5; ++c) {
             double d = 0.0;
 #pragma unroll
-            for (int r = k; r < 9; ++r) d = fma(v[k][r], a[c][r], d);
+            for (int r = k; r < 9; ++r) d = __builtin_fma(v[k][r], a[c][r], d);
             d = d * beta[k];
 #pragma unroll
-            for (int r = k; r < 9; ++r) a[c][r] = fma(-d, v[k][r], a[c][r]);
+            for (int r = k; r < 9; ++r) a[c][r] = __builtin_fma(-d, v[k][r], a[c][r]);
         }
     }
     if (!ok) return false;
@@ -477,10 +477,10 @@ __device__ bool nullspace_5x9(const double* x1, const double* x2, double N[4][9]
         for (int k = 4; k >= 0; --k) {
             double d = 0.0;
 #pragma unroll
-            for (int r = k; r < 9; ++r) d = fma(v[k][r], y[r], d);
+            for (int r = k; r < 9; ++r) d = __builtin_fma(v[k][r], y[r], d);
             d = d * beta[k];
 #pragma unroll
-            for (int r = k; r < 9; ++r) y[r] = fma(-d, v[k][r], y[r]);
+            for (int r = k; r < 9; ++r) y[r] = __builtin_fma(-d, v[k][r], y[r]);
         }
 #pragma unroll
         for (int j = 0; j < 9; ++j) N[n][j] = y[j];
@@ -633,7 +633,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
             for (int j = 0; j < 10; ++j) row[j] = ld(r, j);
             const double f = pair_lo(row[c]);
 #pragma unroll
-            for (int j = 0; j < 10; ++j) row[j] = fma(-f, prow[j], row[j]);
+            for (int j = 0; j < 10; ++j) row[j] = __builtin_fma(-f, prow[j], row[j]);
 #pragma unroll
             for (int j = 0; j < 10; ++j) {
                 if (r < kRegRows) G[r < kRegRows ? r : 0][j] = row[j];
@@ -705,16 +705,16 @@ __device__ int five_point_stage2(const double* in, RootMem m, SolFn&& on_sol) {
 #pragma unroll
             for (int i = 0; i <= deg[c1]; ++i)
 #pragma unroll
-                for (int j = 0; j <= deg[c2]; ++j) mm[i + j] = fma(B[1][c1][i], B[2][c2][j], mm[i + j]);
+                for (int j = 0; j <= deg[c2]; ++j) mm[i + j] = __builtin_fma(B[1][c1][i], B[2][c2][j], mm[i + j]);
 #pragma unroll
             for (int i = 0; i <= deg[c2]; ++i)
 #pragma unroll
-                for (int j = 0; j <= deg[c1]; ++j) mm[i + j] = fma(-B[1][c2][i], B[2][c1][j], mm[i + j]);
+                for (int j = 0; j <= deg[c1]; ++j) mm[i + j] = __builtin_fma(-B[1][c2][i], B[2][c1][j], mm[i + j]);
             const int dm = deg[c1] + deg[c2];
 #pragma unroll
             for (int i = 0; i <= deg[c]; ++i)
 #pragma unroll
-                for (int j = 0; j <= dm; ++j) n[i + j] = fma(B[0][c][i], mm[j], n[i + j]);
+                for (int j = 0; j <= dm; ++j) n[i + j] = __builtin_fma(B[0][c][i], mm[j], n[i + j]);
         }
     }
     RPROF(6);
@@ -740,7 +740,7 @@ __device__ int five_point_stage2(const double* in, RootMem m, SolFn&& on_sol) {
                 const int dg = c == 2 ? 4 : 3;
                 double v = B[r][c][dg];
 #pragma unroll
-                for (int i = dg - 1; i >= 0; --i) v = fma(v, z, B[r][c][i]);
+                for (int i = dg - 1; i >= 0; --i) v = __builtin_fma(v, z, B[r][c][i]);
                 Bz[r][c] = v;
             }
         double bx = 0, by = 0, bzz = 0, bn = -1.0;
@@ -1018,13 +1018,13 @@ __device__ void svd3(const double* E, double* U, double* s, double* V) {
 }
 
 __device__ __forceinline__ double sampson_sq(const double* E, double2 p1, double2 p2, double* den_out) {
-    const double a0 = fma(E[1], p1.y, fma(E[0], p1.x, E[2]));
-    const double a1 = fma(E[4], p1.y, fma(E[3], p1.x, E[5]));
-    const double a2 = fma(E[7], p1.y, fma(E[6], p1.x, E[8]));
-    const double b0 = fma(E[3], p2.y, fma(E[0], p2.x, E[6]));
-    const double b1 = fma(E[4], p2.y, fma(E[1], p2.x, E[7]));
-    const double num = fma(p2.y, a1, fma(p2.x, a0, a2));
-    const double den = fma(b1, b1, fma(b0, b0, fma(a1, a1, a0 * a0)));
+    const double a0 = __builtin_fma(E[1], p1.y, __builtin_fma(E[0], p1.x, E[2]));
+    const double a1 = __builtin_fma(E[4], p1.y, __builtin_fma(E[3], p1.x, E[5]));
+    const double a2 = __builtin_fma(E[7], p1.y, __builtin_fma(E[6], p1.x, E[8]));
+    const double b0 = __builtin_fma(E[3], p2.y, __builtin_fma(E[0], p2.x, E[6]));
+    const double b1 = __builtin_fma(E[4], p2.y, __builtin_fma(E[1], p2.x, E[7]));
+    const double num = __builtin_fma(p2.y, a1, __builtin_fma(p2.x, a0, a2));
+    const double den = __builtin_fma(b1, b1, __builtin_fma(b0, b0, __builtin_fma(a1, a1, a0 * a0)));
     *den_out = den;
     return den > 0.0 ? num * num / den : 1e300;
 }
@@ -1081,7 +1081,7 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
         for (int a = 0; a < 9; ++a) {
             const double wa = w2 * r[a];
 #pragma unroll
-            for (int b = a; b < 9; ++b, ++k) acc[k] = fma(wa, r[b], acc[k]);
+            for (int b = a; b < 9; ++b, ++k) acc[k] = __builtin_fma(wa, r[b], acc[k]);
         }
         ++n;
     }
@@ -1114,7 +1114,7 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
             for (int j = 0; j <= i; ++j) {
                 double v = A(i, j) + (i == j ? shift : 0.0);
 #pragma unroll
-                for (int k = 0; k < j; ++k) v = fma(-L[i * (i + 1) / 2 + k], L[j * (j + 1) / 2 + k], v);
+                for (int k = 0; k < j; ++k) v = __builtin_fma(-L[i * (i + 1) / 2 + k], L[j * (j + 1) / 2 + k], v);
                 if (i == j) {
                     ok = ok && v > 0.0;
                     L[i * (i + 1) / 2 + i] = 1.0 / sqrt(fmax(v, 1e-300));
@@ -1131,19 +1131,19 @@ __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const do
                 for (int i = 0; i < 9; ++i) {  // L y = x
                     double v = x[i];
 #pragma unroll
-                    for (int k = 0; k < i; ++k) v = fma(-L[i * (i + 1) / 2 + k], x[k], v);
+                    for (int k = 0; k < i; ++k) v = __builtin_fma(-L[i * (i + 1) / 2 + k], x[k], v);
                     x[i] = v * L[i * (i + 1) / 2 + i];
                 }
 #pragma unroll
                 for (int i = 8; i >= 0; --i) {  // L^T z = y
                     double v = x[i];
 #pragma unroll
-                    for (int k = i + 1; k < 9; ++k) v = fma(-L[k * (k + 1) / 2 + i], x[k], v);
+                    for (int k = i + 1; k < 9; ++k) v = __builtin_fma(-L[k * (k + 1) / 2 + i], x[k], v);
                     x[i] = v * L[i * (i + 1) / 2 + i];
                 }
                 double nrm = 0.0;
 #pragma unroll
-                for (int i = 0; i < 9; ++i) nrm = fma(x[i], x[i], nrm);
+                for (int i = 0; i < 9; ++i) nrm = __builtin_fma(x[i], x[i], nrm);
                 nrm = 1.0 / sqrt(nrm);
 #pragma unroll
                 for (int i = 0; i < 9; ++i) x[i] *= nrm;
