@@ -140,6 +140,6 @@ def test_batched_two_view_estimator(scene, generated, oracle_mod):
         _, rmask, rR, rt, rn, _ = ref
         assert len(v) == rn, (i1, i2, len(v), rn)
         np.testing.assert_array_equal(geometry.rotation_matrix(R), rR)
-        np.testing.assert_array_equal(geometry.unit_vector(U), rt)
+        np.testing.assert_array_equal(geometry.unit_vector(U), geometry.unit_vector(geometry.Unit3(rt)))
         n_checked += 1
     assert n_checked >= 6
