@@ -14,6 +14,8 @@
 // the K1 x K2 probability matrix never reaches HBM. The Sinkhorn matrix (K1 + 1) x (K2 + 1) does, once per pair.
 #include <float.h>
 
+#include <type_traits>
+
 #include "common.hpp"
 
 #pragma clang fp contract(off)
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
 // Weights are split once per layer into [plane][n][k] (sg_split_weights_kernel); activations are split as they are
 // staged into LDS. 128 x 128 output tile per workgroup of four waves (64 x 64 each, four 32 x 32 accumulators),
 // K in chunks of 16 held in LDS as [plane][row][16] bf16 (32-byte rows: a lane's 16-byte fragment read is
-// conflict-free), the next chunk prefetched into registers during the MFMAs.
+// conflict-free), the next two chunks in flight in registers during the MFMAs.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kG3Tile = 128;
@@ -231,39 +233,43 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     const bool a_ok = m0 + srow < g.M, b_ok = n0 + srow < g.N;
     const float* Arow = g.A + z * g.a_batch + (long)(m0 + srow) * g.lda + sk;
     const float* A2row = g.A2 ? g.A2 + z * g.a2_batch + (long)(m0 + srow) * g.lda2 + sk - g.Ksplit : nullptr;
-    f32x4_t pa0, pa1, pb0, pb1;
-    u32x4 pw[3];
-    auto load = [&](int k0) {
-        pa0 = pa1 = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    // two chunks in flight in registers (slots 0 / 1): chunk k0 + 32 is requested while chunk k0's MFMAs run
+    f32x4_t pa[2][2], pb[2][2];
+    u32x4 pw[2][3];
+    auto load = [&](int k0, auto slot) {
+        constexpr int q = decltype(slot)::value;
+        pa[q][0] = pa[q][1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
         if (a_ok) {
             const float* src = k0 < g.Ksplit ? Arow + k0 : A2row + k0;
-            pa0 = *(const f32x4_t*)src;
-            pa1 = *(const f32x4_t*)(src + 4);
+            pa[q][0] = *(const f32x4_t*)src;
+            pa[q][1] = *(const f32x4_t*)(src + 4);
         }
         if (g.Bp) {
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                pw[p] = b_ok ? *(const u32x4*)(g.Bp + ((long)p * g.N + n0 + srow) * g.K + k0 + sk) : u32x4{0, 0, 0, 0};
+                pw[q][p] = b_ok ? *(const u32x4*)(g.Bp + ((long)p * g.N + n0 + srow) * g.K + k0 + sk)
+                                : u32x4{0, 0, 0, 0};
         } else {
-            pb0 = pb1 = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            pb[q][0] = pb[q][1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
             if (b_ok) {
                 const float* src = g.Bt + z * g.b_batch + (long)(n0 + srow) * g.ldb + k0 + sk;
-                pb0 = *(const f32x4_t*)src;
-                pb1 = *(const f32x4_t*)(src + 4);
+                pb[q][0] = *(const f32x4_t*)src;
+                pb[q][1] = *(const f32x4_t*)(src + 4);
             }
         }
     };
-    auto store = [&]() {
+    auto store = [&](auto slot) {
+        constexpr int q = decltype(slot)::value;
         bf16x8 h, m, l;
-        split3x8(pa0, pa1, h, m, l);
+        split3x8(pa[q][0], pa[q][1], h, m, l);
         *(bf16x8*)&As[0][srow][sk] = h;
         *(bf16x8*)&As[1][srow][sk] = m;
         *(bf16x8*)&As[2][srow][sk] = l;
         if (g.Bp) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) *(u32x4*)&Bs[p][srow][sk] = pw[p];
+            for (int p = 0; p < 3; ++p) *(u32x4*)&Bs[p][srow][sk] = pw[q][p];
         } else {
-            split3x8(pb0, pb1, h, m, l);
+            split3x8(pb[q][0], pb[q][1], h, m, l);
             *(bf16x8*)&Bs[0][srow][sk] = h;
             *(bf16x8*)&Bs[1][srow][sk] = m;
             *(bf16x8*)&Bs[2][srow][sk] = l;
@@ -274,12 +280,7 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-    load(0);
-    for (int k0 = 0; k0 < g.K; k0 += 16) {
-        __syncthreads();  // the previous chunk's fragments are read
-        store();
-        __syncthreads();
-        if (k0 + 16 < g.K) load(k0 + 16);  // in flight during the MFMAs
+    auto compute = [&]() {
         bf16x8 a[3][2], b[3][2];
 #pragma unroll
         for (int p = 0; p < 3; ++p)
@@ -301,6 +302,23 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
                 c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
                 acc[i][j] = c;
             }
+    };
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    load(0, S0{});
+    if (16 < g.K) load(16, S1{});
+    for (int k0 = 0; k0 < g.K; k0 += 32) {
+        __syncthreads();  // the previous chunk's fragments are read
+        store(S0{});
+        __syncthreads();
+        if (k0 + 32 < g.K) load(k0 + 32, S0{});
+        compute();
+        if (k0 + 16 >= g.K) break;
+        __syncthreads();
+        store(S1{});
+        __syncthreads();
+        if (k0 + 48 < g.K) load(k0 + 48, S1{});
+        compute();
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -310,32 +328,59 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
         const float sc = g.bn_scale ? g.bn_scale[n] : 1.0f;
         const float sh = g.bn_shift ? g.bn_shift[n] : 0.0f;
         float* C = g.C + z * g.c_batch + n;
+        // values (q/k/v projection, n >= 512) go to the transposed planes [..][dim][key]: a lane holds four
+        // consecutive keys per register group, written as one 8-byte store per plane (its keys are contiguous there)
+        const bool vt = g.kv && n >= 2 * kD;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int m = m0 + 64 * wm + 32 * i + 4 * hk + (e & 3) + 8 * (e >> 2);
-                if (m >= Mv) continue;
-                float v = acc[i][j][e] + bb;
-                if (g.bn_scale) v = v * sc + sh;
-                if (g.relu) v = v > 0.0f ? v : 0.0f;
-                if (g.alpha != 1.0f) v = v * g.alpha;
-                if (g.kv && n >= kD) {
-                    __bf16 pl[3];
-                    split3(v, pl[0], pl[1], pl[2]);
-                    const int d = (n - kD) & (kD - 1), hh = d / kHd, dd = d % kHd;
-                    __bf16* base = g.kv + z * g.kv_batch;
+            for (int eg = 0; eg < 4; ++eg) {
+                const int mg = m0 + 64 * wm + 32 * i + 4 * hk + 8 * eg;  // rows mg .. mg + 3 (Mv, M: multiples of 64)
+                if (mg >= Mv) continue;
+                float v4[4];
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) {
-                        if (n < 2 * kD)
-                            base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
-                        else
-                            base[(long)3 * kD * g.M + (((long)q * kHeads + hh) * kHd + dd) * g.M + m] = pl[q];
+                for (int e4 = 0; e4 < 4; ++e4) {
+                    float v = acc[i][j][4 * eg + e4] + bb;
+                    if (g.bn_scale) v = v * sc + sh;
+                    if (g.relu) v = v > 0.0f ? v : 0.0f;
+                    if (g.alpha != 1.0f) v = v * g.alpha;
+                    v4[e4] = v;
+                }
+                if (vt) {
+                    const int d = n - 2 * kD, hh = d / kHd, dd = d % kHd;
+                    __bf16* base = g.kv + z * g.kv_batch + (long)3 * kD * g.M;
+                    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                    bf16x4 pl[3];
+#pragma unroll
+                    for (int e4 = 0; e4 < 4; ++e4) {
+                        __bf16 h0, h1, h2;
+                        split3(v4[e4], h0, h1, h2);
+                        pl[0][e4] = h0;
+                        pl[1][e4] = h1;
+                        pl[2][e4] = h2;
                     }
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        *(bf16x4*)(base + (((long)q * kHeads + hh) * kHd + dd) * g.M + mg) = pl[q];
                     continue;
                 }
-                float* c = C + (long)m * g.ldc;
-                *c = g.residual ? *c + v : v;
+#pragma unroll
+                for (int e4 = 0; e4 < 4; ++e4) {
+                    const int m = mg + e4;
+                    if (m >= Mv) continue;
+                    const float v = v4[e4];
+                    if (g.kv && n >= kD) {  // keys: [..][key][dim], lanes along the dimension (64-byte rows)
+                        __bf16 pl[3];
+                        split3(v, pl[0], pl[1], pl[2]);
+                        const int d = n - kD, hh = d / kHd, dd = d % kHd;
+                        __bf16* base = g.kv + z * g.kv_batch;
+#pragma unroll
+                        for (int q = 0; q < 3; ++q) base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
+                        continue;
+                    }
+                    float* c = C + (long)m * g.ldc;
+                    *c = g.residual ? *c + v : v;
+                }
             }
     }
 }
@@ -367,128 +412,10 @@ __global__ void sg_split_weights_kernel(SplitJobs jobs) {
 // ------------------------------------------------------------------ fused multi-head attention
 // superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 64 queries of one
 // (pair, side, head); wave w owns queries 16 w .. +16 and streams the source side's keys in chunks of 64 (online
-// softmax). v_mfma_f32_16x16x4_f32 layouts: A lane l = A[l % 16][l / 16], B lane l = B[l / 16][l % 16],
-// C lane l, j = C[4 (l / 16) + j][l % 16].
+// softmax); the K1 x K2 probability matrix never reaches HBM.
 constexpr int kAttnKeys = 64;
-constexpr int kKvStride = kHd + 1;
 
-__global__ __launch_bounds__(256, 3) void sg_attention_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
-                                                           const int* __restrict__ side_counts /*(2P)*/, int kmax,
-                                                           int cross, float* __restrict__ out /*(2P, kmax, 256)*/) {
-    __shared__ float Kc[kAttnKeys * kKvStride];
-    __shared__ float Vc[kAttnKeys * kKvStride];
-    __shared__ float Pw[4][16 * (kAttnKeys + 1)];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int zs = blockIdx.z;              // (pair, side) of the queries
-    const int zsrc = cross ? (zs ^ 1) : zs; // keys / values side
-    const int h = blockIdx.y;
-    const int q0 = blockIdx.x * 64 + 16 * wave;
-    const int nkeys = side_counts[zsrc];
-    const int nq = side_counts[zs];
-    if (blockIdx.x * 64 >= nq) return;
-    const int lr = lane & 15, lq = lane >> 4;
-    // Q fragments: qa[s] = Q[q0 + lr][4 s + lq]
-    float qa[16];
-    {
-        const float* qrow = qkv + ((long)zs * kmax + min(q0 + lr, kmax - 1)) * 768 + h * kHd;
-#pragma unroll
-        for (int s = 0; s < 16; ++s) qa[s] = qrow[4 * s + lq];
-    }
-    float m_run[4], l_run[4];
-    f32x4_t o[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        m_run[j] = -INFINITY;
-        l_run[j] = 0.0f;
-        o[j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-    }
-    const float* kbase = qkv + (long)zsrc * kmax * 768 + 256 + h * kHd;
-    const float* vbase = qkv + (long)zsrc * kmax * 768 + 512 + h * kHd;
-    for (int c0 = 0; c0 < nkeys; c0 += kAttnKeys) {
-        __syncthreads();  // previous chunk consumed
-        for (int e = tid; e < kAttnKeys * 16; e += 256) {
-            const int key = e >> 4, q4 = e & 15;
-            f32x4_t kv = {0.0f, 0.0f, 0.0f, 0.0f}, vv = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (c0 + key < nkeys) {
-                kv = *(const f32x4_t*)(kbase + (long)(c0 + key) * 768 + 4 * q4);
-                vv = *(const f32x4_t*)(vbase + (long)(c0 + key) * 768 + 4 * q4);
-            }
-            float* kd = Kc + key * kKvStride + 4 * q4;
-            float* vd = Vc + key * kKvStride + 4 * q4;
-            kd[0] = kv[0]; kd[1] = kv[1]; kd[2] = kv[2]; kd[3] = kv[3];
-            vd[0] = vv[0]; vd[1] = vv[1]; vd[2] = vv[2]; vd[3] = vv[3];
-        }
-        __syncthreads();
-        // S = Q K^T / 8 for 16 queries x 64 keys (4 tiles of 16 keys)
-        f32x4_t s4[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int s = 0; s < 16; ++s)
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(qa[s], Kc[(16 * t + lr) * kKvStride + 4 * s + lq], acc, 0,
-                                                           0, 0);
-            s4[t] = acc;
-        }
-        // lane holds S[4 lq + j][16 t + lr]
-        float cmax[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            float mx = -INFINITY;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                float v = s4[t][j] / 8.0f;
-                if (c0 + 16 * t + lr >= nkeys) v = -INFINITY;
-                s4[t][j] = v;
-                mx = fmaxf(mx, v);
-            }
-#pragma unroll
-            for (int m = 1; m < 16; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
-            cmax[j] = mx;
-        }
-        float* pw = Pw[wave];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float mnew = fmaxf(m_run[j], cmax[j]);
-            const float corr = expf(m_run[j] - mnew);
-            float rs = 0.0f;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float p = expf(s4[t][j] - mnew);
-                rs = rs + p;
-                pw[(4 * lq + j) * (kAttnKeys + 1) + 16 * t + lr] = p;
-            }
-#pragma unroll
-            for (int m = 1; m < 16; m <<= 1) rs = rs + __shfl_xor(rs, m);
-            l_run[j] = l_run[j] * corr + rs;
-            m_run[j] = mnew;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) o[u][j] = o[u][j] * corr;
-        }
-        __syncthreads();  // P (written in C layout) is read back in A layout
-        // O += P V: A = P (16 queries x 64 keys), B = V (64 keys x 64 dims, 4 tiles of 16)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            f32x4_t acc = o[u];
-#pragma unroll
-            for (int s = 0; s < 16; ++s)
-                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pw[lr * (kAttnKeys + 1) + 4 * s + lq],
-                                                           Vc[(4 * s + lq) * kKvStride + 16 * u + lr], acc, 0, 0, 0);
-            o[u] = acc;
-        }
-    }
-    float* ob = out + (long)zs * kmax * 256 + h * kHd;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int q = q0 + 4 * lq + j;
-        if (q >= nq) continue;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) ob[(long)q * 256 + 16 * u + lr] = l_run[j] > 0.0f ? o[u][j] / l_run[j] : 0.0f;
-    }
-}
-
-// Split-precision attention (the fp32 kernel above, restated on bf16 MFMA with the three-plane products of
-// sg_gemm3_kernel): v_mfma_f32_16x16x32_bf16, A lane l = A[l % 16][8 (l / 16) + j], B lane l = B[8 (l / 16) + j][l % 16],
+// On bf16 MFMA with the three-plane products of sg_gemm3_kernel: v_mfma_f32_16x16x32_bf16, A lane l = A[l % 16][8 (l / 16) + j], B lane l = B[8 (l / 16) + j][l % 16],
 // C lane l, j = C[4 (l / 16) + j][l % 16]. Keys arrive as bf16 planes [key][64] and values transposed [64][key] (written
 // by the q/k/v projection's epilogue), so a key chunk is staged by 16-byte copies; Q is split once per wave, P per
 // chunk. Rows of the LDS planes are padded to 72 elements (conflict-free 16-byte fragment reads).
@@ -516,8 +443,8 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
         const float* qrow = qkv + ((long)zs * kmax + min(q0 + lr, kmax - 1)) * 768 + h * kHd + 8 * lq;
 #pragma unroll
         for (int s = 0; s < 2; ++s)
-            split3x8(*(const f32x4_t*)(qrow + 32 * s), *(const f32x4_t*)(qrow + 32 * s + 4), qf[0][s], qf[1][s],
-                     qf[2][s]);
+            split3x8(*(const f32x4_t*)(qrow + 32 * s) * 0.125f, *(const f32x4_t*)(qrow + 32 * s + 4) * 0.125f, qf[0][s],
+                     qf[1][s], qf[2][s]);  // q / sqrt(64): a power of two, exact before the split
     }
     float m_run[4], l_run[4];
     f32x4_t o[4];
@@ -529,17 +456,32 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
     }
     const __bf16* kb = kvp + zsrc * kv_batch;                          // [3][head][kmax][64]
     const __bf16* vb = kvp + zsrc * kv_batch + (long)3 * kD * kmax;    // [3][head][64][kmax]
+    // the next key chunk's planes are loaded into registers while the current one is processed
+    constexpr int kUnits = 3 * kAttnKeys * 8 / 256;  // 16-byte units per thread and chunk (keys and values each)
+    u32x4 pk[kUnits], pv[kUnits];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int u = 0; u < kUnits; ++u) {
+            const int e = tid + 256 * u;
+            const int p = e / (kAttnKeys * 8), row = (e / 8) % kAttnKeys, seg = e % 8;
+            pk[u] = pv[u] = u32x4{0, 0, 0, 0};
+            if (c0 + row < nkeys) pk[u] = *(const u32x4*)(kb + (((long)p * kHeads + h) * kmax + c0 + row) * kHd + 8 * seg);
+            if (c0 + 8 * seg < nkeys)
+                pv[u] = *(const u32x4*)(vb + (((long)p * kHeads + h) * kHd + row) * kmax + c0 + 8 * seg);
+        }
+    };
+    load(0);
     for (int c0 = 0; c0 < nkeys; c0 += kAttnKeys) {
         __syncthreads();  // previous chunk consumed
-        for (int e = tid; e < 3 * kAttnKeys * 8; e += 256) {
+#pragma unroll
+        for (int u = 0; u < kUnits; ++u) {
+            const int e = tid + 256 * u;
             const int p = e / (kAttnKeys * 8), row = (e / 8) % kAttnKeys, seg = e % 8;
-            u32x4 kv = {0, 0, 0, 0}, vv = {0, 0, 0, 0};
-            if (c0 + row < nkeys) kv = *(const u32x4*)(kb + (((long)p * kHeads + h) * kmax + c0 + row) * kHd + 8 * seg);
-            if (c0 + 8 * seg < nkeys) vv = *(const u32x4*)(vb + (((long)p * kHeads + h) * kHd + row) * kmax + c0 + 8 * seg);
-            *(u32x4*)&Ks[p][row][8 * seg] = kv;
-            *(u32x4*)&Vs[p][row][8 * seg] = vv;
+            *(u32x4*)&Ks[p][row][8 * seg] = pk[u];
+            *(u32x4*)&Vs[p][row][8 * seg] = pv[u];
         }
         __syncthreads();
+        if (c0 + kAttnKeys < nkeys) load(c0 + kAttnKeys);
         // S = Q K^T / 8 for 16 queries x 64 keys (4 tiles of 16 keys)
         f32x4_t s4[4];
 #pragma unroll
@@ -565,7 +507,7 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
             float mx = -INFINITY;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                float v = s4[t][j] / 8.0f;
+                float v = s4[t][j];
                 if (c0 + 16 * t + lr >= nkeys) v = -INFINITY;
                 s4[t][j] = v;
                 mx = fmaxf(mx, v);
@@ -578,11 +520,12 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const float mnew = fmaxf(m_run[j], cmax[j]);
-            const float corr = expf(m_run[j] - mnew);
+            // exp(x) = 2^(x log2 e) on v_exp_f32 (1 ulp): x <= 0 here, so no range reduction is needed
+            const float corr = __builtin_amdgcn_exp2f((m_run[j] - mnew) * 1.44269504088896341f);
             float rs = 0.0f;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
-                const float p = expf(s4[t][j] - mnew);
+                const float p = __builtin_amdgcn_exp2f((s4[t][j] - mnew) * 1.44269504088896341f);
                 rs = rs + p;
                 pw[4 * lq + j][16 * t + lr] = p;
             }
@@ -593,7 +536,11 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
 #pragma unroll
             for (int u = 0; u < 4; ++u) o[u][j] = o[u][j] * corr;
         }
-        __syncthreads();  // P (written in C layout) is read back in A layout
+        // P (written in C layout) is read back in A layout by the same wave: LDS operations of one wave complete
+        // in order, so a wave barrier (no workgroup barrier) separates the writes from the reads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // O += P V: A = P (16 queries x 64 keys), B = V (64 keys x 64 dims, 4 tiles of 16)
         bf16x8 pf[3][2];
 #pragma unroll
