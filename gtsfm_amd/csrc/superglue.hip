@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
 // Weights are split once per layer into [plane][n][k] (sg_split_weights_kernel); activations are split as they are
 // staged into LDS. 128 x 128 output tile per workgroup of four waves (64 x 64 each, four 32 x 32 accumulators),
 // K in chunks of 16 held in LDS as [plane][row][16] bf16 (32-byte rows: a lane's 16-byte fragment read is
-// conflict-free), the next two chunks in flight in registers during the MFMAs.
+// conflict-free), the next chunk in flight in registers during the MFMAs.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kG3Tile = 128;
@@ -216,9 +216,18 @@ struct Gemm3Args {
     long kv_batch;
 };
 
+// KC: K per LDS chunk (16 or 32; rows padded to 40 elements at 32 so the fragment reads stay conflict-free);
+// SLOTS: chunks kept in flight in registers. Measured on the C5 slice (qkv / W1 / Wm+W2 launches of 992 sides):
+// <16, 1> 7.05 / 7.57 / 3.45 ms (162 VGPRs, three waves per SIMD), <16, 2> 7.87 / 8.38 / 4.17, <32, 1> 7.40 / 7.76 /
+// 4.04, <32, 2> 10.19 / 10.94 / 5.38: the kernel is bound by LDS fragment traffic (12 16-byte reads per 24 MFMAs per
+// wave), so occupancy beats prefetch depth; <16, 1> is the one launched.
+constexpr int kG3Kc = 16, kG3Slots = 1;
+template <int KC, int SLOTS>
 __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
-    __shared__ __attribute__((aligned(16))) __bf16 As[3][kG3Tile][16];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[3][kG3Tile][16];
+    constexpr int kRow = KC == 16 ? 16 : 40;
+    constexpr int kU = KC / 16;  // 8-float A units / 16-byte B units per thread, plane and chunk
+    __shared__ __attribute__((aligned(16))) __bf16 As[3][kG3Tile][kRow];
+    __shared__ __attribute__((aligned(16))) __bf16 Bs[3][kG3Tile][kRow];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int z = blockIdx.z;
     const int m0 = blockIdx.y * kG3Tile, n0 = blockIdx.x * kG3Tile;
@@ -228,51 +237,57 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     if (m0 >= Mv || n0 >= Nv) return;
     const int wm = wave & 1, wn = wave >> 1;
     const int r = lane & 31, hk = lane >> 5;
-    // staging roles: thread t stages row / column t >> 1, k half 8 (t & 1)
-    const int srow = tid >> 1, sk = 8 * (tid & 1);
+    // staging roles: thread t stages row / column t >> 1, k offset (KC / 2) (t & 1)
+    const int srow = tid >> 1, sk = (KC / 2) * (tid & 1);
     const bool a_ok = m0 + srow < g.M, b_ok = n0 + srow < g.N;
     const float* Arow = g.A + z * g.a_batch + (long)(m0 + srow) * g.lda + sk;
     const float* A2row = g.A2 ? g.A2 + z * g.a2_batch + (long)(m0 + srow) * g.lda2 + sk - g.Ksplit : nullptr;
-    // two chunks in flight in registers (slots 0 / 1): chunk k0 + 32 is requested while chunk k0's MFMAs run
-    f32x4_t pa[2][2], pb[2][2];
-    u32x4 pw[2][3];
+    f32x4_t pa[SLOTS][2 * kU], pb[SLOTS][2 * kU];
+    u32x4 pw[SLOTS][3][kU];
     auto load = [&](int k0, auto slot) {
         constexpr int q = decltype(slot)::value;
-        pa[q][0] = pa[q][1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int u = 0; u < 2 * kU; ++u) pa[q][u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
         if (a_ok) {
             const float* src = k0 < g.Ksplit ? Arow + k0 : A2row + k0;
-            pa[q][0] = *(const f32x4_t*)src;
-            pa[q][1] = *(const f32x4_t*)(src + 4);
+#pragma unroll
+            for (int u = 0; u < 2 * kU; ++u) pa[q][u] = *(const f32x4_t*)(src + 4 * u);
         }
         if (g.Bp) {
 #pragma unroll
             for (int p = 0; p < 3; ++p)
-                pw[q][p] = b_ok ? *(const u32x4*)(g.Bp + ((long)p * g.N + n0 + srow) * g.K + k0 + sk)
-                                : u32x4{0, 0, 0, 0};
+#pragma unroll
+                for (int u = 0; u < kU; ++u)
+                    pw[q][p][u] = b_ok ? *(const u32x4*)(g.Bp + ((long)p * g.N + n0 + srow) * g.K + k0 + sk + 8 * u)
+                                       : u32x4{0, 0, 0, 0};
         } else {
-            pb[q][0] = pb[q][1] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int u = 0; u < 2 * kU; ++u) pb[q][u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
             if (b_ok) {
                 const float* src = g.Bt + z * g.b_batch + (long)(n0 + srow) * g.ldb + k0 + sk;
-                pb[q][0] = *(const f32x4_t*)src;
-                pb[q][1] = *(const f32x4_t*)(src + 4);
+#pragma unroll
+                for (int u = 0; u < 2 * kU; ++u) pb[q][u] = *(const f32x4_t*)(src + 4 * u);
             }
         }
     };
     auto store = [&](auto slot) {
         constexpr int q = decltype(slot)::value;
-        bf16x8 h, m, l;
-        split3x8(pa[q][0], pa[q][1], h, m, l);
-        *(bf16x8*)&As[0][srow][sk] = h;
-        *(bf16x8*)&As[1][srow][sk] = m;
-        *(bf16x8*)&As[2][srow][sk] = l;
-        if (g.Bp) {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) *(u32x4*)&Bs[p][srow][sk] = pw[q][p];
-        } else {
-            split3x8(pb[q][0], pb[q][1], h, m, l);
-            *(bf16x8*)&Bs[0][srow][sk] = h;
-            *(bf16x8*)&Bs[1][srow][sk] = m;
-            *(bf16x8*)&Bs[2][srow][sk] = l;
+        for (int u = 0; u < kU; ++u) {
+            bf16x8 h, m, l;
+            split3x8(pa[q][2 * u], pa[q][2 * u + 1], h, m, l);
+            *(bf16x8*)&As[0][srow][sk + 8 * u] = h;
+            *(bf16x8*)&As[1][srow][sk + 8 * u] = m;
+            *(bf16x8*)&As[2][srow][sk + 8 * u] = l;
+            if (g.Bp) {
+#pragma unroll
+                for (int p = 0; p < 3; ++p) *(u32x4*)&Bs[p][srow][sk + 8 * u] = pw[q][p][u];
+            } else {
+                split3x8(pb[q][2 * u], pb[q][2 * u + 1], h, m, l);
+                *(bf16x8*)&Bs[0][srow][sk + 8 * u] = h;
+                *(bf16x8*)&Bs[1][srow][sk + 8 * u] = m;
+                *(bf16x8*)&Bs[2][srow][sk + 8 * u] = l;
+            }
         }
     };
     f32x16 acc[2][2];
@@ -281,44 +296,51 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
     auto compute = [&]() {
-        bf16x8 a[3][2], b[3][2];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int ks = 0; ks < kU; ++ks) {
+            bf16x8 a[3][2], b[3][2];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                a[p][s] = *(const bf16x8*)&As[p][64 * wm + 32 * s + r][8 * hk];
-                b[p][s] = *(const bf16x8*)&Bs[p][64 * wn + 32 * s + r][8 * hk];
-            }
+            for (int p = 0; p < 3; ++p)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+                for (int s = 0; s < 2; ++s) {
+                    a[p][s] = *(const bf16x8*)&As[p][64 * wm + 32 * s + r][16 * ks + 8 * hk];
+                    b[p][s] = *(const bf16x8*)&Bs[p][64 * wn + 32 * s + r][16 * ks + 8 * hk];
+                }
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                f32x16 c = acc[i][j];
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
-                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
-                acc[i][j] = c;
-            }
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    f32x16 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
+                    acc[i][j] = c;
+                }
+        }
     };
     using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, 1>;
+    using S1 = std::integral_constant<int, SLOTS - 1>;
     load(0, S0{});
-    if (16 < g.K) load(16, S1{});
-    for (int k0 = 0; k0 < g.K; k0 += 32) {
+    if constexpr (SLOTS == 2) {
+        if (KC < g.K) load(KC, S1{});
+    }
+    for (int k0 = 0; k0 < g.K; k0 += KC * SLOTS) {
         __syncthreads();  // the previous chunk's fragments are read
         store(S0{});
         __syncthreads();
-        if (k0 + 32 < g.K) load(k0 + 32, S0{});
+        if (k0 + KC * SLOTS < g.K) load(k0 + KC * SLOTS, S0{});
         compute();
-        if (k0 + 16 >= g.K) break;
-        __syncthreads();
-        store(S1{});
-        __syncthreads();
-        if (k0 + 48 < g.K) load(k0 + 48, S1{});
-        compute();
+        if constexpr (SLOTS == 2) {
+            if (k0 + KC >= g.K) break;
+            __syncthreads();
+            store(S1{});
+            __syncthreads();
+            if (k0 + 3 * KC < g.K) load(k0 + 3 * KC, S1{});
+            compute();
+        }
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -863,7 +885,7 @@ hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
 hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
     const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + kG3Tile - 1) / kG3Tile),
                     (unsigned)batches);
-    hipLaunchKernelGGL(sg_gemm3_kernel, grid, dim3(256), 0, stream, g);
+    hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots>), grid, dim3(256), 0, stream, g);
     return hipGetLastError();
 }
 
