@@ -157,6 +157,19 @@ __global__ __launch_bounds__(kGemmThreads) void sg_gemm_kernel(GemmArgs g) {
     }
 }
 
+// XCD-aware workgroup order: the dispatcher deals workgroup L to XCD L % 8, so workgroup L takes logical tile
+// (L % 8) * (T / 8) + L / 8 and every XCD runs a contiguous range of logical tiles, whose shared operands (one
+// (side, head)'s key / value planes; one row block of A) then stay in that XCD's L2. Identity when 8 does not divide T.
+__device__ __forceinline__ void xcd_tile(int& x, int& y, int& z) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const long T = (long)nx * ny * gridDim.z;
+    const long L = blockIdx.x + (long)nx * (blockIdx.y + (long)ny * blockIdx.z);
+    const long t = T % 8 == 0 ? (L % 8) * (T / 8) + L / 8 : L;
+    x = (int)(t % nx);
+    y = (int)((t / nx) % ny);
+    z = (int)(t / ((long)nx * ny));
+}
+
 // ------------------------------------------------------------------ batched GEMM, fp32-accurate on bf16 MFMA
 // Every fp32 operand x is split exactly into three bf16 planes, x = x_h + x_m + x_l (each plane the bf16 rounding of
 // what the planes above it leave; the two subtractions are exact), and a product a b is formed from the six largest
@@ -229,8 +242,9 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     __shared__ __attribute__((aligned(16))) __bf16 As[3][kG3Tile][kRow];
     __shared__ __attribute__((aligned(16))) __bf16 Bs[3][kG3Tile][kRow];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int z = blockIdx.z;
-    const int m0 = blockIdx.y * kG3Tile, n0 = blockIdx.x * kG3Tile;
+    int bx, by, z;
+    xcd_tile(bx, by, z);
+    const int m0 = by * kG3Tile, n0 = bx * kG3Tile;
     int Mv = g.M, Nv = g.N;
     if (g.m_lim) Mv = min(Mv, g.m_lim[z * g.lim_stride]);
     if (g.n_lim) Nv = min(Nv, g.n_lim[z * g.lim_stride + 1]);
@@ -451,13 +465,13 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
     __shared__ __attribute__((aligned(16))) __bf16 Vs[3][kHd][kAttnPad];
     __shared__ __attribute__((aligned(16))) float Pw[4][16][kAttnKeys + 4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int zs = blockIdx.z;
+    int qb, h, zs;
+    xcd_tile(qb, h, zs);
     const int zsrc = cross ? (zs ^ 1) : zs;
-    const int h = blockIdx.y;
-    const int q0 = blockIdx.x * 64 + 16 * wave;
+    const int q0 = qb * 64 + 16 * wave;
     const int nkeys = side_counts[zsrc];
     const int nq = side_counts[zs];
-    if (blockIdx.x * 64 >= nq) return;
+    if (qb * 64 >= nq) return;
     const int lr = lane & 15, lq = lane >> 4;
     // Q fragments, planes x k-steps: Q[q0 + lr][32 s + 8 lq + j]
     bf16x8 qf[3][2];

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${1:-r04}
 CFG=${2:-c5}
 R=$GRAFT_REPO_ROOT
-if [ "$CFG" = c3 ]; then KS="fl_shortlist_kernel,fl_rerank_kernel,conv_mfma_kernel"; else KS="sg_attention_kernel,sg_gemm_kernel,sk_,conv_mfma_kernel"; fi
+if [ "$CFG" = c3 ]; then KS="fl_shortlist_kernel,fl_rerank_kernel,conv3_kernel"; else KS="sg_attention3_kernel,sg_gemm3_kernel,sg_gemm_kernel,sk_,conv3_kernel"; fi
 dirs=""
 for grp in FETCH_SIZE WRITE_SIZE; do
   (cd /tmp && timeout -s KILL 600 rocprofv3 --pmc $grp --output-format csv -d $R/gpurun_out/pmc_${TAG}_${CFG}_$grp -o run -- python $R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc_${TAG}_${CFG}_$grp.log 2>&1)
