@@ -23,7 +23,8 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 
 def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, ratio: Optional[float],
                 mode: int = native.GTSFM_MATCH_INT_F16, stream: Optional[torch.cuda.Stream] = None,
-                groups: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                groups: Optional[torch.Tensor] = None,
+                out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Mutual-NN + ratio matching of every (i1, i2) row of `pairs`.
 
     Args:
@@ -34,6 +35,8 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
         mode: GTSFM_MATCH_INT_F16 (integer descriptors, MFMA) or GTSFM_MATCH_EXACT_F32.
         groups: optional (n_groups, G) int32 device tensor of pair indices (-1 = empty slot) for the INT_F16 kernel:
             every pair exactly once, the pairs of a group sharing image i1 (pair_groups builds one).
+        out: optional caller-owned (idx (P, kmax, 2) int32, count (P,) int32) to write into (no allocation: a
+            pipelined caller keeps them across steps instead of cycling cross-stream blocks through the allocator).
 
     Returns:
         idx: (P, kmax, 2) int32 tensor holding uint32 keypoint indices, rows [0, count) valid per pair.
@@ -44,8 +47,14 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
     n_img, kmax, dim = desc.shape
     n_pairs = pairs.shape[0]
     L = native.lib()
-    idx = torch.empty((max(n_pairs, 1), kmax, 2), dtype=torch.int32, device=desc.device)
-    cnt = torch.zeros((max(n_pairs, 1),), dtype=torch.int32, device=desc.device)
+    if out is not None:
+        idx, cnt = out
+        assert idx.dtype == torch.int32 and idx.is_contiguous() and tuple(idx.shape) == (n_pairs, kmax, 2)
+        assert cnt.dtype == torch.int32 and cnt.is_contiguous() and tuple(cnt.shape) == (n_pairs,)
+        cnt.zero_()
+    else:
+        idx = torch.empty((max(n_pairs, 1), kmax, 2), dtype=torch.int32, device=desc.device)
+        cnt = torch.zeros((max(n_pairs, 1),), dtype=torch.int32, device=desc.device)
     if n_pairs == 0:
         return idx[:0], cnt[:0]
     ws_bytes = L.gtsfm_match_workspace_bytes(n_img, kmax, dim, n_pairs, mode)
