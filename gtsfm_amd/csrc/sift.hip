@@ -171,12 +171,6 @@ __host__ __device__ constexpr size_t blur_lds_bytes(int r, bool u8) {
            sizeof(float);
 }
 
-__device__ __forceinline__ float gray_at(const uint8_t* __restrict__ s, int C, int W, int yy, int xx) {
-    const uint8_t* p = s + ((size_t)yy * W + xx) * C;
-    if (C == 1) return (float)p[0];
-    return (float)((p[0] * 4899 + p[1] * 9617 + p[2] * 1868 + (1 << 13)) >> 14);
-}
-
 // INTER_LINEAR 2x source coordinate of output index x (cv::resize, half-pixel centres, clamped at the border)
 __device__ __forceinline__ void up_coord(int x, int W, int& s0, int& s1, float& f) {
     float fx = (float)((x + 0.5) * 0.5 - 0.5);
@@ -227,13 +221,33 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
         const int gx0 = max((xlo - 1) / 2, 0), gx1 = min(xhi / 2 + 1, W0 - 1);
         const uint8_t* s8 = img8 + (size_t)b * H0 * W0 * C;
         {
+            // gray = cv::cvtColor's fixed point (R 4899 + G 9617 + B 1868 + 2^13) >> 14; every byte load of the tile is
+            // issued before any is converted (one HBM round trip per block instead of one per pixel row)
             constexpr int NGR = (blur_gh(R) + kBlurTYT - 1) / kBlurTYT;
             float gv[NGR];
             const int gx = gx0 + tx;
+            if (C == 1) {
+                uint32_t b0[NGR];
 #pragma unroll
-            for (int i = 0; i < NGR; ++i) {
-                const int gy = gy0 + ty + i * kBlurTYT;
-                gv[i] = (gy <= gy1 && gx <= gx1) ? gray_at(s8, C, W0, gy, gx) : 0.f;
+                for (int i = 0; i < NGR; ++i) {
+                    const int gy = min(gy0 + ty + i * kBlurTYT, gy1);
+                    b0[i] = s8[(size_t)gy * W0 + min(gx, gx1)];
+                }
+#pragma unroll
+                for (int i = 0; i < NGR; ++i) gv[i] = (float)b0[i];
+            } else {
+                uint32_t b0[NGR], b1[NGR], b2[NGR];
+#pragma unroll
+                for (int i = 0; i < NGR; ++i) {
+                    const int gy = min(gy0 + ty + i * kBlurTYT, gy1);
+                    const uint8_t* px = s8 + ((size_t)gy * W0 + min(gx, gx1)) * 3;
+                    b0[i] = px[0];
+                    b1[i] = px[1];
+                    b2[i] = px[2];
+                }
+#pragma unroll
+                for (int i = 0; i < NGR; ++i)
+                    gv[i] = (float)((b0[i] * 4899 + b1[i] * 9617 + b2[i] * 1868 + (1 << 13)) >> 14);
             }
 #pragma unroll
             for (int i = 0; i < NGR; ++i) {
@@ -1120,19 +1134,34 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             __syncthreads();
             // lane l takes the contiguous run [l nit, (l + 1) nit) of the chunk's samples: one instruction's 64 atomics
             // spread over the whole chunk's rows (and bins) instead of one or two raster rows
+            // software-pipelined: the next sample's four gradient taps are in flight while this one is binned (lanes
+            // past the chunk's end load the last valid sample's taps, in bounds, and skip the binning)
             const int nit = (nv + 63) >> 6;
+            auto taps = [&](int t, float (&g)[4], int& sv) {
+                sv = slist[min(t, nv - 1)];
+                const int r = py + (sv >> 16), c = px + (short)(sv & 0xffff);
+                const float* p = img_p + (size_t)r * W + c;
+                g[0] = p[1];
+                g[1] = p[-1];
+                g[2] = p[-W];
+                g[3] = p[W];
+            };
+            float gn[4];
+            int svn = 0;
+            if (nit > 0) taps(lane * nit, gn, svn);
             for (int it = 0; it < nit; ++it) {
             const int t = lane * nit + it;
+            const float g0 = gn[0], g1 = gn[1], g2 = gn[2], g3 = gn[3];
+            const int sv = svn;
+            if (it + 1 < nit) taps(t + 1, gn, svn);
             if (t >= nv) continue;
-            const int sv = slist[t];
             const int i = sv >> 16, j = (short)(sv & 0xffff);
             const float c_rot = j * cos_t - i * sin_t;
             const float r_rot = j * sin_t + i * cos_t;
             float rbin = r_rot + d / 2 - 0.5f;
             float cbin = c_rot + d / 2 - 0.5f;
-            const int r = py + i, c = px + j;
-            const float dx = img_p[(size_t)r * W + c + 1] - img_p[(size_t)r * W + c - 1];
-            const float dy = img_p[(size_t)(r - 1) * W + c] - img_p[(size_t)(r + 1) * W + c];
+            const float dx = g0 - g1;
+            const float dy = g2 - g3;
             const float wexp = (c_rot * c_rot + r_rot * r_rot) * exp_scale;
             const float o = fast_atan2(dy, dx);
             const float mag0 = sqrtf(fmaf(dx, dx, dy * dy));
