@@ -446,49 +446,60 @@ __global__ void sg_split_weights_kernel(SplitJobs jobs) {
 }
 
 // ------------------------------------------------------------------ fused multi-head attention
-// superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 64 queries of one
-// (pair, side, head); wave w owns queries 16 w .. +16 and streams the source side's keys in chunks of 64 (online
-// softmax); the K1 x K2 probability matrix never reaches HBM.
+// superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 128 queries of one
+// (pair, side, head); wave w owns queries 32 w .. +32 (two 16-query tiles) and streams the source side's keys in chunks
+// of 64 (online softmax); the K1 x K2 probability matrix never reaches HBM.
 constexpr int kAttnKeys = 64;
+constexpr int kAttnQT = 2;                    // 16-query tiles per wave: each staged K / V fragment feeds both
+constexpr int kAttnQ = 4 * 16 * kAttnQT;      // queries per workgroup
 
-// On bf16 MFMA with the three-plane products of sg_gemm3_kernel: v_mfma_f32_16x16x32_bf16, A lane l = A[l % 16][8 (l / 16) + j], B lane l = B[8 (l / 16) + j][l % 16],
-// C lane l, j = C[4 (l / 16) + j][l % 16]. Keys arrive as bf16 planes [key][64] and values transposed [64][key] (written
-// by the q/k/v projection's epilogue), so a key chunk is staged by 16-byte copies; Q is split once per wave, P per
-// chunk. Rows of the LDS planes are padded to 72 elements (conflict-free 16-byte fragment reads).
+// On bf16 MFMA with the three-plane products of sg_gemm3_kernel (v_mfma_f32_16x16x32_bf16: A lane l = A[l % 16][8 (l /
+// 16) + j], B lane l = B[8 (l / 16) + j][l % 16], C lane l, j = C[4 (l / 16) + j][l % 16]). Both products run
+// transposed so that a lane keeps one query throughout:
+// - S^T = K Q^T: lane (lr, lq) of key tile t holds S[query lr][key 16 t + 4 lq + j], so the softmax max / sum of a
+//   query are lane-local plus two shuffles, and its running max / sum / rescale factor never leave the lane;
+// - O^T = V^T P^T over 32-key slabs whose k index runs through the keys in the order the lane already holds them
+//   (k = 8 lq + j' -> key 32 s + 4 lq + j' for j' < 4, 32 s + 16 + 4 lq + j' - 4 otherwise): P^T's operand is the
+//   lane's own probabilities (no LDS round trip) and V^T's is read with that key order.
+// Keys arrive as bf16 planes [key][64] and values transposed [64][key] (written by the q/k/v projection's epilogue),
+// staged by 16-byte copies; Q is split once per wave, P per chunk. LDS rows are padded to 72 elements.
 constexpr int kAttnPad = 72;
 
 __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
                                                              const __bf16* __restrict__ kvp, long kv_batch,
                                                              const int* __restrict__ side_counts, int kmax, int cross,
                                                              float* __restrict__ out /*(2P, kmax, 256)*/) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     __shared__ __attribute__((aligned(16))) __bf16 Ks[3][kAttnKeys][kAttnPad];
     __shared__ __attribute__((aligned(16))) __bf16 Vs[3][kHd][kAttnPad];
-    __shared__ __attribute__((aligned(16))) float Pw[4][16][kAttnKeys + 4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int qb, h, zs;
     xcd_tile(qb, h, zs);
     const int zsrc = cross ? (zs ^ 1) : zs;
-    const int q0 = qb * 64 + 16 * wave;
+    const int q0 = qb * kAttnQ + 16 * kAttnQT * wave;
     const int nkeys = side_counts[zsrc];
     const int nq = side_counts[zs];
-    if (qb * 64 >= nq) return;
+    if (qb * kAttnQ >= nq) return;
     const int lr = lane & 15, lq = lane >> 4;
-    // Q fragments, planes x k-steps: Q[q0 + lr][32 s + 8 lq + j]
-    bf16x8 qf[3][2];
-    {
-        const float* qrow = qkv + ((long)zs * kmax + min(q0 + lr, kmax - 1)) * 768 + h * kHd + 8 * lq;
+    // Q fragments (the B operand of S^T), per tile, plane and k-step: Q[q0 + 16 qt + lr][32 s + 8 lq + j]
+    bf16x8 qf[kAttnQT][3][2];
+#pragma unroll
+    for (int qt = 0; qt < kAttnQT; ++qt) {
+        const float* qrow = qkv + ((long)zs * kmax + min(q0 + 16 * qt + lr, kmax - 1)) * 768 + h * kHd + 8 * lq;
 #pragma unroll
         for (int s = 0; s < 2; ++s)
-            split3x8(*(const f32x4_t*)(qrow + 32 * s) * 0.125f, *(const f32x4_t*)(qrow + 32 * s + 4) * 0.125f, qf[0][s],
-                     qf[1][s], qf[2][s]);  // q / sqrt(64): a power of two, exact before the split
+            split3x8(*(const f32x4_t*)(qrow + 32 * s) * 0.125f, *(const f32x4_t*)(qrow + 32 * s + 4) * 0.125f,
+                     qf[qt][0][s], qf[qt][1][s], qf[qt][2][s]);  // q / sqrt(64): a power of two, exact before the split
     }
-    float m_run[4], l_run[4];
-    f32x4_t o[4];
+    // per tile: the lane's query's running max / sum; o[qt][u][j] = O[q0 + 16 qt + lr][16 u + 4 lq + j]
+    float m_run[kAttnQT], l_run[kAttnQT];
+    f32x4_t o[kAttnQT][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        m_run[j] = -INFINITY;
-        l_run[j] = 0.0f;
-        o[j] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    for (int qt = 0; qt < kAttnQT; ++qt) {
+        m_run[qt] = -INFINITY;
+        l_run[qt] = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[qt][u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
     }
     const __bf16* kb = kvp + zsrc * kv_batch;                          // [3][head][kmax][64]
     const __bf16* vb = kvp + zsrc * kv_batch + (long)3 * kD * kmax;    // [3][head][64][kmax]
@@ -518,96 +529,105 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
         }
         __syncthreads();
         if (c0 + kAttnKeys < nkeys) load(c0 + kAttnKeys);
-        // S = Q K^T / 8 for 16 queries x 64 keys (4 tiles of 16 keys)
-        f32x4_t s4[4];
+        // S^T = K Q^T / 8 for 64 keys (4 tiles of 16) x the wave's query tiles
+        f32x4_t s4[kAttnQT][4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-            f32x4_t acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int qt = 0; qt < kAttnQT; ++qt) s4[qt][t] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const bf16x8 k0 = *(const bf16x8*)&Ks[0][16 * t + lr][32 * s + 8 * lq];
                 const bf16x8 k1 = *(const bf16x8*)&Ks[1][16 * t + lr][32 * s + 8 * lq];
                 const bf16x8 k2 = *(const bf16x8*)&Ks[2][16 * t + lr][32 * s + 8 * lq];
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[0][s], k2, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[2][s], k0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[1][s], k1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[0][s], k1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[1][s], k0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[0][s], k0, acc, 0, 0, 0);
-            }
-            s4[t] = acc;
-        }
-        float cmax[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+                for (int qt = 0; qt < kAttnQT; ++qt) {
+                    f32x4_t acc = s4[qt][t];
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k2, qf[qt][0][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[qt][2][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[qt][1][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k1, qf[qt][0][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[qt][1][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(k0, qf[qt][0][s], acc, 0, 0, 0);
+                    s4[qt][t] = acc;
+                }
+            }
+        }
+        // online softmax per query (lane-local; the 4 lanes sharing lr hold the chunk's other keys), then P's planes
+        bf16x8 pf[kAttnQT][3][2];
+#pragma unroll
+        for (int qt = 0; qt < kAttnQT; ++qt) {
             float mx = -INFINITY;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                float v = s4[t][j];
-                if (c0 + 16 * t + lr >= nkeys) v = -INFINITY;
-                s4[t][j] = v;
-                mx = fmaxf(mx, v);
-            }
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int m = 1; m < 16; m <<= 1) mx = fmaxf(mx, __shfl_xor(mx, m));
-            cmax[j] = mx;
-        }
-        float(*pw)[kAttnKeys + 4] = Pw[wave];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const float mnew = fmaxf(m_run[j], cmax[j]);
+                for (int j = 0; j < 4; ++j) {
+                    float v = s4[qt][t][j];
+                    if (c0 + 16 * t + 4 * lq + j >= nkeys) v = -INFINITY;
+                    s4[qt][t][j] = v;
+                    mx = fmaxf(mx, v);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16));
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float mnew = fmaxf(m_run[qt], mx);
             // exp(x) = 2^(x log2 e) on v_exp_f32 (1 ulp): x <= 0 here, so no range reduction is needed
-            const float corr = __builtin_amdgcn_exp2f((m_run[j] - mnew) * 1.44269504088896341f);
+            const float corr = __builtin_amdgcn_exp2f((m_run[qt] - mnew) * 1.44269504088896341f);
             float rs = 0.0f;
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const float p = __builtin_amdgcn_exp2f((s4[t][j] - mnew) * 1.44269504088896341f);
-                rs = rs + p;
-                pw[4 * lq + j][16 * t + lr] = p;
-            }
+            for (int t = 0; t < 4; ++t)
 #pragma unroll
-            for (int m = 1; m < 16; m <<= 1) rs = rs + __shfl_xor(rs, m);
-            l_run[j] = l_run[j] * corr + rs;
-            m_run[j] = mnew;
+                for (int j = 0; j < 4; ++j) {
+                    const float p = __builtin_amdgcn_exp2f((s4[qt][t][j] - mnew) * 1.44269504088896341f);
+                    rs = rs + p;
+                    s4[qt][t][j] = p;
+                }
+            rs = rs + __shfl_xor(rs, 16);
+            rs = rs + __shfl_xor(rs, 32);
+            l_run[qt] = l_run[qt] * corr + rs;
+            m_run[qt] = mnew;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) o[u][j] = o[u][j] * corr;
+            for (int u = 0; u < 4; ++u) o[qt][u] = o[qt][u] * corr;
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                split3x8(s4[qt][2 * s], s4[qt][2 * s + 1], pf[qt][0][s], pf[qt][1][s], pf[qt][2][s]);
         }
-        // P (written in C layout) is read back in A layout by the same wave: LDS operations of one wave complete
-        // in order, so a wave barrier (no workgroup barrier) separates the writes from the reads
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // O += P V: A = P (16 queries x 64 keys), B = V (64 keys x 64 dims, 4 tiles of 16)
-        bf16x8 pf[3][2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-            split3x8(*(const f32x4_t*)&pw[lr][32 * s + 8 * lq], *(const f32x4_t*)&pw[lr][32 * s + 8 * lq + 4], pf[0][s],
-                     pf[1][s], pf[2][s]);
+        // O^T += V^T P^T: A = V^T (16 dims x 32 keys of slab s, in the lane's key order), B = P^T
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            f32x4_t acc = o[u];
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const bf16x8 v0 = *(const bf16x8*)&Vs[0][16 * u + lr][32 * s + 8 * lq];
-                const bf16x8 v1 = *(const bf16x8*)&Vs[1][16 * u + lr][32 * s + 8 * lq];
-                const bf16x8 v2 = *(const bf16x8*)&Vs[2][16 * u + lr][32 * s + 8 * lq];
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[0][s], v2, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[2][s], v0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[1][s], v1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[0][s], v1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[1][s], v0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[0][s], v0, acc, 0, 0, 0);
+                bf16x8 v[3];
+#pragma unroll
+                for (int pl = 0; pl < 3; ++pl) {
+                    const bf16x4 a = *(const bf16x4*)&Vs[pl][16 * u + lr][32 * s + 4 * lq];
+                    const bf16x4 b = *(const bf16x4*)&Vs[pl][16 * u + lr][32 * s + 16 + 4 * lq];
+                    v[pl] = bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+                }
+#pragma unroll
+                for (int qt = 0; qt < kAttnQT; ++qt) {
+                    f32x4_t acc = o[qt][u];
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v[2], pf[qt][0][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v[0], pf[qt][2][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v[1], pf[qt][1][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v[1], pf[qt][0][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v[0], pf[qt][1][s], acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(v[0], pf[qt][0][s], acc, 0, 0, 0);
+                    o[qt][u] = acc;
+                }
             }
-            o[u] = acc;
         }
     }
     float* ob = out + (long)zs * kmax * 256 + h * kHd;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int q = q0 + 4 * lq + j;
+    for (int qt = 0; qt < kAttnQT; ++qt) {
+        const int q = q0 + 16 * qt + lr;
         if (q >= nq) continue;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) ob[(long)q * 256 + 16 * u + lr] = l_run[j] > 0.0f ? o[u][j] / l_run[j] : 0.0f;
+        for (int u = 0; u < 4; ++u) {
+            f32x4_t r = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            if (l_run[qt] > 0.0f) r = o[qt][u] / l_run[qt];
+            *(f32x4_t*)(ob + (long)q * 256 + 16 * u + 4 * lq) = r;
+        }
     }
 }
 
@@ -1031,8 +1051,8 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
         gq.kv = kvp;
         gq.kv_batch = kv_batch;
         GTSFM_CHECK_HIP(run_gemm3(gq, S, stream));
-        hipLaunchKernelGGL(sg_attention3_kernel, dim3(kmax / 64, kHeads, S), dim3(256), 0, stream, qkv, kvp, kv_batch,
-                           side_counts, kmax, l & 1, att);
+        hipLaunchKernelGGL(sg_attention3_kernel, dim3((kmax + kAttnQ - 1) / kAttnQ, kHeads, S), dim3(256), 0, stream,
+                           qkv, kvp, kv_batch, side_counts, kmax, l & 1, att);
         GTSFM_CHECK_HIP(hipGetLastError());
         GTSFM_CHECK_HIP(run_gemm3(side_gemm3(att, kD, Pm, kD, kD, bm, msg, kD, kmax), S, stream));
         Gemm3Args g1 = side_gemm3(X, kD, P1, 512, 512, b1, hid, 512, kmax);
