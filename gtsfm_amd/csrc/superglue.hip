@@ -7,11 +7,12 @@
 //   -> log-space optimal transport with a dustbin -> mutual argmax + threshold.
 //
 // Layout: every (pair, side) owns a kmax x C row-major (point-major) feature block, so each 1x1 Conv1d is a
-// batched GEMM  Y[n][co] = sum_ci X[n][ci] W^T[ci][co]  on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, exact
-// fp32 products and sums: the network matches the fp32 torch reference up to summation order). Heads are stored
-// head-major (channel h * 64 + d; the reference's view(b, 64, 4, n) interleaves them as 4 d + h — the host packs
-// the q/k/v/merge weights accordingly). Attention is one fused kernel (online softmax, v_mfma_f32_16x16x4_f32):
-// the K1 x K2 probability matrix never reaches HBM. The Sinkhorn matrix (K1 + 1) x (K2 + 1) does, once per pair.
+// batched GEMM  Y[n][co] = sum_ci X[n][ci] W^T[ci][co]  on the bf16 matrix cores at fp32 accuracy (three-plane
+// split, six products: sg_gemm3_kernel; the network matches the fp32 torch reference up to summation order). Heads
+// are stored head-major (channel h * 64 + d; the reference's view(b, 64, 4, n) interleaves them as 4 d + h — the
+// host packs the q/k/v/merge weights accordingly). Attention is one fused kernel (online softmax on the same split
+// products): the K1 x K2 probability matrix never reaches HBM. The Sinkhorn matrix (K1 + 1) x (K2 + 1) does, once
+// per pair.
 #include <float.h>
 
 #include <type_traits>
@@ -178,7 +179,7 @@ __device__ __forceinline__ void xcd_tile(int& x, int& y, int& z) {
 // so each product carries an fp32-level error; the sums are fp32 as on the fp32 matrix cores. Six
 // v_mfma_f32_32x32x16_bf16 (16 k each) replace eight v_mfma_f32_32x32x2_f32 (2 k each): 2.7x the product rate.
 // Weights are split once per layer into [plane][n][k] (sg_split_weights_kernel); activations are split as they are
-// staged into LDS. 128 x 128 output tile per workgroup of four waves (64 x 64 each, four 32 x 32 accumulators),
+// staged into LDS. TM x 128 output tile per workgroup of four waves (TM / 2 x 64 each, 32 x 32 accumulators),
 // K in chunks of 16 held in LDS as [plane][row][16] bf16 (32-byte rows: a lane's 16-byte fragment read is
 // conflict-free), the next chunk in flight in registers during the MFMAs.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -234,38 +235,56 @@ struct Gemm3Args {
 // <16, 1> 7.05 / 7.57 / 3.45 ms (162 VGPRs, three waves per SIMD), <16, 2> 7.87 / 8.38 / 4.17, <32, 1> 7.40 / 7.76 /
 // 4.04, <32, 2> 10.19 / 10.94 / 5.38: the kernel is bound by LDS fragment traffic (12 16-byte reads per 24 MFMAs per
 // wave), so occupancy beats prefetch depth; <16, 1> is the one launched.
+// TM: output rows per workgroup (128 or 256; waves 2 x 2, each TM / 2 x 64). Measured on the C5 slice (992 sides):
+// TM = 256 runs the N = 768 / 512 launches (q/k/v, W1) at 7.21 / 7.02 ms against 7.53 / 7.42 for 128, the N = 256 ones
+// (Wm, W2) at 3.69 against 3.53, so run_gemm3 takes 256 for N >= 512.
 constexpr int kG3Kc = 16, kG3Slots = 1;
-template <int KC, int SLOTS>
+constexpr int kG3EpiRow = 72;  // epilogue tile row stride (floats): 4 rows apart = 32 banks apart
+template <int KC, int SLOTS, int TM>
 __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     constexpr int kRow = KC == 16 ? 16 : 40;
-    constexpr int kU = KC / 16;  // 8-float A units / 16-byte B units per thread, plane and chunk
-    __shared__ __attribute__((aligned(16))) __bf16 As[3][kG3Tile][kRow];
-    __shared__ __attribute__((aligned(16))) __bf16 Bs[3][kG3Tile][kRow];
+    constexpr int kU = KC / 16;   // 8-float A units / 16-byte B units per thread, plane and chunk
+    constexpr int RA = TM / 128;  // A rows staged per thread
+    constexpr int WI = TM / 64;   // 32-row accumulator tiles per wave (2 x 2 waves over TM x 128)
+    // staging planes As [3][TM][kRow] | Bs [3][128][kRow], reused by the epilogue's per-wave 32 x 72 fp32 tiles
+    constexpr int kStage = 3 * (TM + kG3Tile) * kRow, kEpi = 4 * 32 * kG3EpiRow * 2;
+    __shared__ __attribute__((aligned(16))) __bf16 smem[kStage > kEpi ? kStage : kEpi];
+    __bf16(*As)[TM][kRow] = reinterpret_cast<__bf16(*)[TM][kRow]>(smem);
+    __bf16(*Bs)[kG3Tile][kRow] = reinterpret_cast<__bf16(*)[kG3Tile][kRow]>(smem + 3 * TM * kRow);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int bx, by, z;
     xcd_tile(bx, by, z);
-    const int m0 = by * kG3Tile, n0 = bx * kG3Tile;
+    const int m0 = by * TM, n0 = bx * kG3Tile;
     int Mv = g.M, Nv = g.N;
     if (g.m_lim) Mv = min(Mv, g.m_lim[z * g.lim_stride]);
     if (g.n_lim) Nv = min(Nv, g.n_lim[z * g.lim_stride + 1]);
     if (m0 >= Mv || n0 >= Nv) return;
     const int wm = wave & 1, wn = wave >> 1;
     const int r = lane & 31, hk = lane >> 5;
-    // staging roles: thread t stages row / column t >> 1, k offset (KC / 2) (t & 1)
+    // staging roles: thread t stages A rows (t >> 1) + 128 ra and B column t >> 1, k offset (KC / 2) (t & 1)
     const int srow = tid >> 1, sk = (KC / 2) * (tid & 1);
-    const bool a_ok = m0 + srow < g.M, b_ok = n0 + srow < g.N;
-    const float* Arow = g.A + z * g.a_batch + (long)(m0 + srow) * g.lda + sk;
-    const float* A2row = g.A2 ? g.A2 + z * g.a2_batch + (long)(m0 + srow) * g.lda2 + sk - g.Ksplit : nullptr;
-    f32x4_t pa[SLOTS][2 * kU], pb[SLOTS][2 * kU];
+    const bool b_ok = n0 + srow < g.N;
+    bool a_ok[RA];
+    const float *Arow[RA], *A2row[RA];
+#pragma unroll
+    for (int ra = 0; ra < RA; ++ra) {
+        a_ok[ra] = m0 + srow + 128 * ra < g.M;
+        Arow[ra] = g.A + z * g.a_batch + (long)(m0 + srow + 128 * ra) * g.lda + sk;
+        A2row[ra] = g.A2 ? g.A2 + z * g.a2_batch + (long)(m0 + srow + 128 * ra) * g.lda2 + sk - g.Ksplit : nullptr;
+    }
+    f32x4_t pa[SLOTS][RA][2 * kU], pb[SLOTS][2 * kU];
     u32x4 pw[SLOTS][3][kU];
     auto load = [&](int k0, auto slot) {
         constexpr int q = decltype(slot)::value;
 #pragma unroll
-        for (int u = 0; u < 2 * kU; ++u) pa[q][u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
-        if (a_ok) {
-            const float* src = k0 < g.Ksplit ? Arow + k0 : A2row + k0;
+        for (int ra = 0; ra < RA; ++ra) {
 #pragma unroll
-            for (int u = 0; u < 2 * kU; ++u) pa[q][u] = *(const f32x4_t*)(src + 4 * u);
+            for (int u = 0; u < 2 * kU; ++u) pa[q][ra][u] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+            if (a_ok[ra]) {
+                const float* src = k0 < g.Ksplit ? Arow[ra] + k0 : A2row[ra] + k0;
+#pragma unroll
+                for (int u = 0; u < 2 * kU; ++u) pa[q][ra][u] = *(const f32x4_t*)(src + 4 * u);
+            }
         }
         if (g.Bp) {
 #pragma unroll
@@ -289,10 +308,13 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             bf16x8 h, m, l;
-            split3x8(pa[q][2 * u], pa[q][2 * u + 1], h, m, l);
-            *(bf16x8*)&As[0][srow][sk + 8 * u] = h;
-            *(bf16x8*)&As[1][srow][sk + 8 * u] = m;
-            *(bf16x8*)&As[2][srow][sk + 8 * u] = l;
+#pragma unroll
+            for (int ra = 0; ra < RA; ++ra) {
+                split3x8(pa[q][ra][2 * u], pa[q][ra][2 * u + 1], h, m, l);
+                *(bf16x8*)&As[0][srow + 128 * ra][sk + 8 * u] = h;
+                *(bf16x8*)&As[1][srow + 128 * ra][sk + 8 * u] = m;
+                *(bf16x8*)&As[2][srow + 128 * ra][sk + 8 * u] = l;
+            }
             if (g.Bp) {
 #pragma unroll
                 for (int p = 0; p < 3; ++p) *(u32x4*)&Bs[p][srow][sk + 8 * u] = pw[q][p][u];
@@ -304,35 +326,37 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
             }
         }
     };
-    f32x16 acc[2][2];
+    f32x16 acc[WI][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
     auto compute = [&]() {
 #pragma unroll
         for (int ks = 0; ks < kU; ++ks) {
-            bf16x8 a[3][2], b[3][2];
+            // B fragments for the chunk, then A one row tile at a time (fewer fragments live beside the accumulators)
+            bf16x8 b[3][2];
 #pragma unroll
             for (int p = 0; p < 3; ++p)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    a[p][s] = *(const bf16x8*)&As[p][64 * wm + 32 * s + r][16 * ks + 8 * hk];
-                    b[p][s] = *(const bf16x8*)&Bs[p][64 * wn + 32 * s + r][16 * ks + 8 * hk];
-                }
+                for (int s = 0; s < 2; ++s) b[p][s] = *(const bf16x8*)&Bs[p][64 * wn + 32 * s + r][16 * ks + 8 * hk];
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < WI; ++i) {
+                bf16x8 a[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) a[p] = *(const bf16x8*)&As[p][(TM / 2) * wm + 32 * i + r][16 * ks + 8 * hk];
 #pragma unroll
                 for (int j = 0; j < 2; ++j) {
                     f32x16 c = acc[i][j];
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
-                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0][j], c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0][j], c, 0, 0, 0);
                     acc[i][j] = c;
                 }
+            }
         }
     };
     using S0 = std::integral_constant<int, 0>;
@@ -356,41 +380,50 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
             compute();
         }
     }
+    // epilogue through LDS, one 32-row accumulator tile at a time: the wave parks tile i (32 x 64 fp32, rows padded
+    // to 72 floats: conflict-free both ways) in the staging buffers and then walks it with lane = column, so no
+    // unrolled per-register epilogue sits beside the live accumulators
+    __syncthreads();  // every wave is done with As / Bs
+    float* T = (float*)smem + wave * 32 * kG3EpiRow;
+    const int col = lane, n = n0 + 64 * wn + col;
+    const bool n_ok = n < Nv;
+    const float bb = n_ok && g.bias ? g.bias[n] : 0.0f;
+    const float sc = n_ok && g.bn_scale ? g.bn_scale[n] : 1.0f;
+    const float sh = n_ok && g.bn_shift ? g.bn_shift[n] : 0.0f;
+    // values (q/k/v projection, n >= 512) go to the transposed planes [..][dim][key] (four consecutive keys per
+    // 8-byte store); keys (256 <= n < 512) to [..][key][dim] (lanes along the dimension)
+    const bool vt = g.kv && n >= 2 * kD, kt = g.kv && n >= kD && n < 2 * kD;
+    auto post = [&](float v) {
+        v = v + bb;
+        if (g.bn_scale) v = v * sc + sh;
+        if (g.relu) v = v > 0.0f ? v : 0.0f;
+        if (g.alpha != 1.0f) v = v * g.alpha;
+        return v;
+    };
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = n0 + 64 * wn + 32 * j + r;
-        if (n >= Nv) continue;
-        const float bb = g.bias ? g.bias[n] : 0.0f;
-        const float sc = g.bn_scale ? g.bn_scale[n] : 1.0f;
-        const float sh = g.bn_shift ? g.bn_shift[n] : 0.0f;
-        float* C = g.C + z * g.c_batch + n;
-        // values (q/k/v projection, n >= 512) go to the transposed planes [..][dim][key]: a lane holds four
-        // consecutive keys per register group, written as one 8-byte store per plane (its keys are contiguous there)
-        const bool vt = g.kv && n >= 2 * kD;
+    for (int i = 0; i < WI; ++i) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int eg = 0; eg < 4; ++eg) {
-                const int mg = m0 + 64 * wm + 32 * i + 4 * hk + 8 * eg;  // rows mg .. mg + 3 (Mv, M: multiples of 64)
-                if (mg >= Mv) continue;
-                float v4[4];
-#pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                    float v = acc[i][j][4 * eg + e4] + bb;
-                    if (g.bn_scale) v = v * sc + sh;
-                    if (g.relu) v = v > 0.0f ? v : 0.0f;
-                    if (g.alpha != 1.0f) v = v * g.alpha;
-                    v4[e4] = v;
-                }
-                if (vt) {
-                    const int d = n - 2 * kD, hh = d / kHd, dd = d % kHd;
-                    __bf16* base = g.kv + z * g.kv_batch + (long)3 * kD * g.M;
-                    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            for (int k = 0; k < 16; ++k) T[(8 * (k >> 2) + 4 * hk + (k & 3)) * kG3EpiRow + 32 * j + r] = acc[i][j][k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int mt = m0 + (TM / 2) * wm + 32 * i;  // the tile's first row (Mv, M: multiples of 64)
+        if (n_ok && mt < Mv) {
+            if (vt) {
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                const int d = n - 2 * kD, hh = d / kHd, dd = d % kHd;
+                __bf16* base = g.kv + z * g.kv_batch + (long)3 * kD * g.M;
+#pragma unroll 2
+                for (int rg = 0; rg < 8; ++rg) {
+                    const int mg = mt + 4 * rg;
+                    if (mg >= Mv) break;
                     bf16x4 pl[3];
 #pragma unroll
                     for (int e4 = 0; e4 < 4; ++e4) {
                         __bf16 h0, h1, h2;
-                        split3(v4[e4], h0, h1, h2);
+                        split3(post(T[(4 * rg + e4) * kG3EpiRow + col]), h0, h1, h2);
                         pl[0][e4] = h0;
                         pl[1][e4] = h1;
                         pl[2][e4] = h2;
@@ -398,26 +431,34 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
 #pragma unroll
                     for (int q = 0; q < 3; ++q)
                         *(bf16x4*)(base + (((long)q * kHeads + hh) * kHd + dd) * g.M + mg) = pl[q];
-                    continue;
                 }
+            } else if (kt) {
+                const int d = n - kD, hh = d / kHd, dd = d % kHd;
+                __bf16* base = g.kv + z * g.kv_batch;
+#pragma unroll 4
+                for (int row = 0; row < 32; ++row) {
+                    const int m = mt + row;
+                    if (m >= Mv) break;
+                    __bf16 pl[3];
+                    split3(post(T[row * kG3EpiRow + col]), pl[0], pl[1], pl[2]);
 #pragma unroll
-                for (int e4 = 0; e4 < 4; ++e4) {
-                    const int m = mg + e4;
-                    if (m >= Mv) continue;
-                    const float v = v4[e4];
-                    if (g.kv && n >= kD) {  // keys: [..][key][dim], lanes along the dimension (64-byte rows)
-                        __bf16 pl[3];
-                        split3(v, pl[0], pl[1], pl[2]);
-                        const int d = n - kD, hh = d / kHd, dd = d % kHd;
-                        __bf16* base = g.kv + z * g.kv_batch;
-#pragma unroll
-                        for (int q = 0; q < 3; ++q) base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
-                        continue;
-                    }
+                    for (int q = 0; q < 3; ++q) base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
+                }
+            } else {
+                float* C = g.C + z * g.c_batch + n;
+#pragma unroll 4
+                for (int row = 0; row < 32; ++row) {
+                    const int m = mt + row;
+                    if (m >= Mv) break;
+                    const float v = post(T[row * kG3EpiRow + col]);
                     float* c = C + (long)m * g.ldc;
                     *c = g.residual ? *c + v : v;
                 }
             }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the tile is read before the next one overwrites it
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -917,9 +958,13 @@ hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
 }
 
 hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
-    const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + kG3Tile - 1) / kG3Tile),
-                    (unsigned)batches);
-    hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots>), grid, dim3(256), 0, stream, g);
+    if (g.N >= 512) {
+        const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + 255) / 256), (unsigned)batches);
+        hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 256>), grid, dim3(256), 0, stream, g);
+    } else {
+        const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + 127) / 128), (unsigned)batches);
+        hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 128>), grid, dim3(256), 0, stream, g);
+    }
     return hipGetLastError();
 }
 
