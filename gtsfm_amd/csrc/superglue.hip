@@ -722,21 +722,24 @@ __global__ void sk_init_kernel(float* __restrict__ Z, const int* __restrict__ si
     if (t <= n) v[(long)p * ld + t] = 0.0f;
 }
 
-__device__ __forceinline__ void lse_push(float x, float& mx, float& s) {
-    if (x > mx) {
-        s = s * expf(mx - x) + 1.0f;
-        mx = x;
-    } else {
-        s = s + expf(x - mx);
-    }
+// exp(x) = 2^(x log2 e) on v_exp_f32 (1 ulp; arguments <= 0 here)
+__device__ __forceinline__ float sk_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
+// online log-sum-exp over four values at a time: one running-max update and no divergent branch per element, and the
+// four loads behind it are issued together (the passes stream Z from HBM: 8.3 GB each on the C5 slice)
+__device__ __forceinline__ void lse_push4(const float (&x)[4], float& mx, float& s) {
+    const float nm = fmaxf(fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])), mx);
+    if (nm == -INFINITY) return;  // nothing seen yet (padding lanes)
+    s = s * sk_exp(mx - nm) + ((sk_exp(x[0] - nm) + sk_exp(x[1] - nm)) + (sk_exp(x[2] - nm) + sk_exp(x[3] - nm)));
+    mx = nm;
 }
 
 __device__ __forceinline__ void lse_merge(float& mx, float& s, float mo, float so) {
     if (mo > mx) {
-        s = s * expf(mx - mo) + so;
+        s = s * sk_exp(mx - mo) + so;
         mx = mo;
     } else if (so > 0.0f) {
-        s = s + so * expf(mo - mx);
+        s = s + so * sk_exp(mo - mx);
     }
 }
 
@@ -753,7 +756,15 @@ __global__ __launch_bounds__(256) void sk_rows_kernel(const float* __restrict__ 
     const float* row = Z + (long)p * ld * ld + (long)i * ld;
     const float* vp = v + (long)p * ld;
     float mx = -INFINITY, s = 0.0f;
-    for (int j = lane; j <= n; j += 64) lse_push(row[j] + vp[j], mx, s);
+    for (int j0 = lane; j0 <= n; j0 += 256) {
+        float x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int j = j0 + 64 * k;
+            x[k] = j <= n ? row[j] + vp[j] : -INFINITY;
+        }
+        lse_push4(x, mx, s);
+    }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
         const float mo = __shfl_xor(mx, o), so = __shfl_xor(s, o);
@@ -780,7 +791,15 @@ __global__ __launch_bounds__(256) void sk_cols_kernel(const float* __restrict__ 
     const float* up = u + (long)p * ld;
     float mx = -INFINITY, s = 0.0f;
     if (j <= n)
-        for (int i = g; i <= m; i += 4) lse_push(Zp[(long)i * ld + j] + up[i], mx, s);
+        for (int i0 = g; i0 <= m; i0 += 16) {
+            float x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + 4 * k;
+                x[k] = i <= m ? Zp[(long)i * ld + j] + up[i] : -INFINITY;
+            }
+            lse_push4(x, mx, s);
+        }
     pm[g][c] = mx;
     ps[g][c] = s;
     __syncthreads();
