@@ -10,5 +10,5 @@ for v in prod "$@"; do
   timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/${TAG}_$v -o run -- python -u bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_${v}_c5.json 2> gpurun_out/${TAG}_${v}_c5.err
   rc=$?; echo "== $v rc=$rc"; [ $rc -eq 0 ] || { tail -20 gpurun_out/${TAG}_${v}_c5.err; exit $rc; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['stage_ms'], d['roofline']['frac'])" gpurun_out/${TAG}_${v}_c5.json
-  f=$(find gpurun_out/${TAG}_$v -name "*kernel_trace.csv" | head -1); python tools/kgrid.py $f sg_ > gpurun_out/${TAG}_${v}_grid.txt; head -8 gpurun_out/${TAG}_${v}_grid.txt; rm -rf gpurun_out/${TAG}_$v
+  f=$(find gpurun_out/${TAG}_$v -name "*kernel_trace.csv" | head -1); python tools/kgrid.py $f sg_ sk_ > gpurun_out/${TAG}_${v}_grid.txt; head -12 gpurun_out/${TAG}_${v}_grid.txt; rm -rf gpurun_out/${TAG}_$v
 done
