@@ -487,12 +487,16 @@ __global__ void sg_split_weights_kernel(SplitJobs jobs) {
 }
 
 // ------------------------------------------------------------------ fused multi-head attention
-// superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 128 queries of one
+// superglue.py:84-103: prob = softmax(q k / sqrt(64)) over keys; out = prob v. One workgroup = 256 queries of one
 // (pair, side, head); wave w owns queries 32 w .. +32 (two 16-query tiles) and streams the source side's keys in chunks
 // of 64 (online softmax); the K1 x K2 probability matrix never reaches HBM.
 constexpr int kAttnKeys = 64;
 constexpr int kAttnQT = 2;                    // 16-query tiles per wave: each staged K / V fragment feeds both
-constexpr int kAttnQ = 4 * 16 * kAttnQT;      // queries per workgroup
+// eight waves (256 queries) per workgroup share each staged key / value chunk: 21.5 ms per C5 launch against 22.1 for
+// four (`profiles/r04o_c5_kernel_grid_aw*.txt`)
+constexpr int kAttnWaves = 8;
+constexpr int kAttnThreads = 64 * kAttnWaves;
+constexpr int kAttnQ = kAttnWaves * 16 * kAttnQT;  // queries per workgroup
 
 // On bf16 MFMA with the three-plane products of sg_gemm3_kernel (v_mfma_f32_16x16x32_bf16: A lane l = A[l % 16][8 (l /
 // 16) + j], B lane l = B[8 (l / 16) + j][l % 16], C lane l, j = C[4 (l / 16) + j][l % 16]). Both products run
@@ -506,7 +510,7 @@ constexpr int kAttnQ = 4 * 16 * kAttnQT;      // queries per workgroup
 // staged by 16-byte copies; Q is split once per wave, P per chunk. LDS rows are padded to 72 elements.
 constexpr int kAttnPad = 72;
 
-__global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
+__global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
                                                              const __bf16* __restrict__ kvp, long kv_batch,
                                                              const int* __restrict__ side_counts, int kmax, int cross,
                                                              float* __restrict__ out /*(2P, kmax, 256)*/) {
@@ -545,12 +549,12 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
     const __bf16* kb = kvp + zsrc * kv_batch;                          // [3][head][kmax][64]
     const __bf16* vb = kvp + zsrc * kv_batch + (long)3 * kD * kmax;    // [3][head][64][kmax]
     // the next key chunk's planes are loaded into registers while the current one is processed
-    constexpr int kUnits = 3 * kAttnKeys * 8 / 256;  // 16-byte units per thread and chunk (keys and values each)
+    constexpr int kUnits = 3 * kAttnKeys * 8 / kAttnThreads;  // 16-byte units per thread and chunk (keys, values each)
     u32x4 pk[kUnits], pv[kUnits];
     auto load = [&](int c0) {
 #pragma unroll
         for (int u = 0; u < kUnits; ++u) {
-            const int e = tid + 256 * u;
+            const int e = tid + kAttnThreads * u;
             const int p = e / (kAttnKeys * 8), row = (e / 8) % kAttnKeys, seg = e % 8;
             pk[u] = pv[u] = u32x4{0, 0, 0, 0};
             if (c0 + row < nkeys) pk[u] = *(const u32x4*)(kb + (((long)p * kHeads + h) * kmax + c0 + row) * kHd + 8 * seg);
@@ -563,7 +567,7 @@ __global__ __launch_bounds__(256, 2) void sg_attention3_kernel(const float* __re
         __syncthreads();  // previous chunk consumed
 #pragma unroll
         for (int u = 0; u < kUnits; ++u) {
-            const int e = tid + 256 * u;
+            const int e = tid + kAttnThreads * u;
             const int p = e / (kAttnKeys * 8), row = (e / 8) % kAttnKeys, seg = e % 8;
             *(u32x4*)&Ks[p][row][8 * seg] = pk[u];
             *(u32x4*)&Vs[p][row][8 * seg] = pv[u];
@@ -1115,8 +1119,8 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
         gq.kv = kvp;
         gq.kv_batch = kv_batch;
         GTSFM_CHECK_HIP(run_gemm3(gq, S, stream));
-        hipLaunchKernelGGL(sg_attention3_kernel, dim3((kmax + kAttnQ - 1) / kAttnQ, kHeads, S), dim3(256), 0, stream,
-                           qkv, kvp, kv_batch, side_counts, kmax, l & 1, att);
+        hipLaunchKernelGGL(sg_attention3_kernel, dim3((kmax + kAttnQ - 1) / kAttnQ, kHeads, S), dim3(kAttnThreads), 0,
+                           stream, qkv, kvp, kv_batch, side_counts, kmax, l & 1, att);
         GTSFM_CHECK_HIP(hipGetLastError());
         GTSFM_CHECK_HIP(run_gemm3(side_gemm3(att, kD, Pm, kD, kD, bm, msg, kD, kmax), S, stream));
         Gemm3Args g1 = side_gemm3(X, kD, P1, 512, 512, b1, hid, 512, kmax);
