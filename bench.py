@@ -340,10 +340,14 @@ def deep_weights(dev, superglue: bool, head=True):
     1x1 descriptor layer is the whitening of its seeded encoder's activations over the benchmark scene
     (tests/golden/make_superpoint_whitening.py), so descriptors of the scene behave like trained ones (unrelated
     keypoints near-orthogonal, repeated points similar); SuperGlue's final projection gain is 24 (see
-    superglue_state_dict), which gives ~1000 matches on adjacent views. Weights change what is matched, never how
-    much work a step does. C3 (TwoWayMatcher: mutual NN + ratio test, no context) uses the head fitted to its strafe
-    scene, head="c3" (32 leading principal directions whitened, the rest at a quarter weight: ~185 putatives per
-    pair, 95 % of the pairs verified)."""
+    superglue_state_dict), which gives ~1000 matches on adjacent views. For SuperPoint + SuperGlue the weights change
+    what is matched, not the work of a step (every kernel's size is set by the keypoint counts). For C3's
+    F16_RERANK matcher they DO change the work: how clustered the descriptors are decides how many keypoints the fp16
+    shortlist certifies and how many go to the exact rescans (0.75 s per step with the C3 head against 4.5 s with the
+    rank-32 head). C3 (TwoWayMatcher: mutual NN + ratio test, no context) uses the head fitted to its strafe scene,
+    head="c3" (32 leading principal directions whitened, the rest at a quarter weight: ~185 putatives per pair, 95 %
+    of the pairs verified); since round 4 C3 is that strafe scene with that head, a different workload from round
+    3's orbit scene."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from superpoint_weights import superglue_state_dict, superpoint_state_dict
 

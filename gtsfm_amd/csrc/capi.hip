@@ -5,7 +5,9 @@ extern "C" {
 
 // 2.00: gtsfm_ransac_E_batched gained d_n_models; gtsfm_compact_verified added
 // 3.01: gtsfm_ba2_batched gained the relative-pose prior inputs d_prior_Rt / d_prior_sigmas
-int gtsfm_hip_abi_version(void) { return 301; }
+// 4.00: gtsfm_superpoint_batched gained d_masks (SuperPoint image masks); gtsfm_ransac_E_batched / _F_batched
+//       reject more argument shapes with GTSFM_ERR_ARG
+int gtsfm_hip_abi_version(void) { return GTSFM_HIP_ABI_VERSION; }
 
 const char* gtsfm_hip_target(void) { return "gfx950"; }
 

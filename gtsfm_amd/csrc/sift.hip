@@ -1067,7 +1067,7 @@ constexpr int kDescChunk = 512;
 
 __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict__ kps, int kp_cap,
                                                         const int* __restrict__ sel, const int* __restrict__ n_sel,
-                                                        int n_img, int max_kpts, LevelTable L,
+                                                        int n_img, int max_kpts, LevelTable L, float narrow_below,
                                                         float* __restrict__ out_xy, float* __restrict__ out_attr,
                                                         float* __restrict__ out_desc) {
     constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
@@ -1199,7 +1199,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
                 put(idx + (d + 3) * (n + 2), v_rco110, small);
                 put(idx + (d + 3) * (n + 2) + 1, v_rco111, small);
             };
-            if (__all(mag < 255.0f))
+            if (__all(mag < narrow_below))  // narrow_below <= 255 (0: the wide path for every sample, a test hook)
                 put8(true);
             else
                 put8(false);
@@ -1455,9 +1455,14 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         T.W[o] = L.Wo[o];
         T.img_stride[o] = (size_t)L.Ho[o] * L.Wo[o];
     }
+    // Weighted gradient magnitudes of a u8 image stay far below 255 (the Gaussian levels bound every difference of
+    // two pixels two apart by about 2 * 255 / (1.25 sqrt(2 pi)) ~ 163), so the wide fixed-point conversion never runs on
+    // real inputs; GTSFM_SIFT_DESC_WIDE=1 forces it for every sample so that tests can pin it against the oracle.
+    const char* wide = getenv("GTSFM_SIFT_DESC_WIDE");
+    const float narrow_below = (wide && wide[0] == '1') ? 0.f : 255.f;
     hipLaunchKernelGGL(descriptor_kernel, dim3(min(B * max_kpts, 16384)), dim3(64), 0, stream,
                        (const KeyRec*)(ws + L.kps), kKpCapPerImg, (const int*)(ws + L.sel), d_counts, B, max_kpts, T,
-                       d_xy, d_attr, d_desc);
+                       narrow_below, d_xy, d_attr, d_desc);
     GTSFM_CHECK_HIP(hipGetLastError());
     if (d_n_detected) GTSFM_CHECK_HIP(hipMemcpyAsync(d_n_detected, kp_counts, (size_t)B * sizeof(int),
                                                      hipMemcpyDeviceToDevice, stream));

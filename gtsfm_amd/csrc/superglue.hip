@@ -7,8 +7,11 @@
 //   -> log-space optimal transport with a dustbin -> mutual argmax + threshold.
 //
 // Layout: every (pair, side) owns a kmax x C row-major (point-major) feature block, so each 1x1 Conv1d is a
-// batched GEMM  Y[n][co] = sum_ci X[n][ci] W^T[ci][co]  on the bf16 matrix cores at fp32 accuracy (three-plane
-// split, six products: sg_gemm3_kernel; the network matches the fp32 torch reference up to summation order). Heads
+// batched GEMM  Y[n][co] = sum_ci X[n][ci] W^T[ci][co]  on the bf16 matrix cores at near-fp32 accuracy (three-plane
+// split, six products: sg_gemm3_kernel). Differences from the fp32 torch reference come from: summation order; the
+// three dropped plane products (each below 2^-23 |a b|); exp taken as v_exp_f32 of x log2(e) in the attention and
+// Sinkhorn kernels (the product's rounding gives a relative error of about |x| 2^-24). tests/test_superglue_gpu.py
+// bounds the result: log-assignment within 2e-3 of the reference module, matches equal up to near-ties. Heads
 // are stored head-major (channel h * 64 + d; the reference's view(b, 64, 4, n) interleaves them as 4 d + h — the
 // host packs the q/k/v/merge weights accordingly). Attention is one fused kernel (online softmax on the same split
 // products): the K1 x K2 probability matrix never reaches HBM. The Sinkhorn matrix (K1 + 1) x (K2 + 1) does, once
@@ -409,7 +412,9 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int mt = m0 + (TM / 2) * wm + 32 * i;  // the tile's first row (Mv, M: multiples of 64)
+        // the tile's first row. M is a multiple of 64; Mv is M unless m_lim is set (the score GEMM), which kv mode
+        // never sets (run_gemm3 rejects it): the V^T path's four-key stores below assume Mv == M
+        const int mt = m0 + (TM / 2) * wm + 32 * i;
         if (n_ok && mt < Mv) {
             if (vt) {
                 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
@@ -510,7 +515,7 @@ constexpr int kAttnQ = kAttnWaves * 16 * kAttnQT;  // queries per workgroup
 // staged by 16-byte copies; Q is split once per wave, P per chunk. LDS rows are padded to 72 elements.
 constexpr int kAttnPad = 72;
 
-__global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float* __restrict__ qkv /*(2P, kmax, 768)*/,
+__global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float* __restrict__ qkv /*q: (2P, kmax, 256)*/,
                                                              const __bf16* __restrict__ kvp, long kv_batch,
                                                              const int* __restrict__ side_counts, int kmax, int cross,
                                                              float* __restrict__ out /*(2P, kmax, 256)*/) {
@@ -530,7 +535,7 @@ __global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float
     bf16x8 qf[kAttnQT][3][2];
 #pragma unroll
     for (int qt = 0; qt < kAttnQT; ++qt) {
-        const float* qrow = qkv + ((long)zs * kmax + min(q0 + 16 * qt + lr, kmax - 1)) * 768 + h * kHd + 8 * lq;
+        const float* qrow = qkv + ((long)zs * kmax + min(q0 + 16 * qt + lr, kmax - 1)) * kD + h * kHd + 8 * lq;
 #pragma unroll
         for (int s = 0; s < 2; ++s)
             split3x8(*(const f32x4_t*)(qrow + 32 * s) * 0.125f, *(const f32x4_t*)(qrow + 32 * s + 4) * 0.125f,
@@ -957,7 +962,7 @@ __host__ SgLayout sg_layout(int P, int kmax) {
     L.X = take(S * kD * 4);
     L.T1 = take(S * kD * 4);
     L.T2 = take(S * kD * 4);
-    L.qkv = take(S * 768 * 4);
+    L.qkv = take(S * kD * 4);  // q only: keys and values go straight to the bf16 planes (kvp)
     L.kvp = take(S * 2 * kD * 3 * sizeof(__bf16));  // key and value planes of the current layer
     L.att = take(S * kD * 4);
     L.msg = take(S * kD * 4);
@@ -981,6 +986,7 @@ hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
 }
 
 hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
+    if (g.kv && (g.m_lim || g.M % 64 != 0)) return hipErrorInvalidValue;  // kv stores write whole 4-key groups
     if (g.N >= 512) {
         const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + 255) / 256), (unsigned)batches);
         hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 256>), grid, dim3(256), 0, stream, g);
@@ -1115,7 +1121,7 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
         GTSFM_CHECK_HIP(split_weights(SplitJobs{{{Wqkv, Pqkv, kD, 768}, {Wm, Pm, kD, kD}, {W1, P1, 512, 512},
                                                  {W2, P2, 512, kD}}},
                                       stream));
-        Gemm3Args gq = side_gemm3(X, kD, Pqkv, kD, 768, bqkv, qkv, 768, kmax);
+        Gemm3Args gq = side_gemm3(X, kD, Pqkv, kD, 768, bqkv, qkv, kD, kmax);  // C = q (columns < 256), ldc 256
         gq.kv = kvp;
         gq.kv_batch = kv_batch;
         GTSFM_CHECK_HIP(run_gemm3(gq, S, stream));

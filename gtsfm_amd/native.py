@@ -28,6 +28,7 @@ c_size_t = ctypes.c_size_t
 c_uint64 = ctypes.c_uint64
 
 # Mirrors include/gtsfm_hip.h
+ABI_VERSION = 400  # GTSFM_HIP_ABI_VERSION: lib() refuses a library built for another ABI
 GTSFM_OK = 0
 GTSFM_ERR_ARG = -1
 GTSFM_ERR_HIP = -2
@@ -139,6 +140,12 @@ def lib() -> ctypes.CDLL:
                 "(the gtsfm_amd product path has no CPU fallback)"
             )
         handle = ctypes.CDLL(LIB_PATH)
+        ver = getattr(handle, "gtsfm_hip_abi_version", None)
+        if ver is None:
+            raise NativeError(f"{LIB_PATH} does not export gtsfm_hip_abi_version")
+        ver.restype, ver.argtypes = c_int, []
+        if ver() != ABI_VERSION:
+            raise NativeError(f"{LIB_PATH} implements ABI {ver()}, this binding expects {ABI_VERSION}: rebuild it")
         for name, (restype, argtypes) in SIGNATURES.items():
             fn = getattr(handle, name, None)
             if fn is None:

@@ -37,7 +37,9 @@ extern "C" {
 /* ----------------------------------------------------------------------------------------------
  * Library
  * ---------------------------------------------------------------------------------------------- */
-/* ABI version (major*100 + minor). */
+/* ABI version (major*100 + minor); a binding built against this header checks that the library
+ * returns GTSFM_HIP_ABI_VERSION before binding anything else. */
+#define GTSFM_HIP_ABI_VERSION 400
 int gtsfm_hip_abi_version(void);
 /* Name of the offload target the kernels were compiled for (e.g. "gfx950"). */
 const char* gtsfm_hip_target(void);

@@ -8,10 +8,18 @@ import re
 from tests.conftest import REPO
 
 
+def _header_abi_version() -> int:
+    text = open(os.path.join(REPO, "include", "gtsfm_hip.h")).read()
+    return int(re.search(r"#define GTSFM_HIP_ABI_VERSION (\d+)", text).group(1))
+
+
 class _Fn:
     def __init__(self):
         self.argtypes = None
         self.restype = "unset"
+
+    def __call__(self):  # only the version query is called at bind time
+        return _header_abi_version()
 
 
 class _RecordingLib:
@@ -66,3 +74,13 @@ def test_native_signatures_match_header_arity():
     for name, (_, argtypes) in native.SIGNATURES.items():
         assert name in arity, f"{name} is not declared in include/gtsfm_hip.h"
         assert len(argtypes) == arity[name], f"{name}: native.py has {len(argtypes)} args, header {arity[name]}"
+
+
+def test_abi_version_agrees_everywhere():
+    """header #define == native.ABI_VERSION == INTEGRATION.md's check == what the library returns."""
+    from gtsfm_amd import native
+
+    v = _header_abi_version()
+    assert native.ABI_VERSION == v
+    assert f"GTSFM_HIP_ABI_VERSION = {v}" in _binding_block()
+    assert native.lib().gtsfm_hip_abi_version() == v

@@ -176,3 +176,43 @@ def test_msac_selects_lower_truncated_cost(oracle_mod):
         assert np.array_equal(im, mm.astype(bool))
         wins += sm <= sr
     assert wins >= 5
+
+
+def test_oracle_pinned_to_round2_oracle_on_lund_c1(oracle_mod):
+    """The E-path oracle vs its round-2 version (tests/golden/make_prev_oracle_c1.py: Gauss-Jordan null space, Jacobi
+    LO, compiler-placed FMAs), which nothing of the kernel shaped: on all 66 C1 pairs the stored results agree (equal
+    inlier counts and masks, R and t within 2e-3 deg), and the current oracle recomputes three of them from its own
+    SIFT + matcher."""
+    from tests.test_lund_door_c1_gpu import LUND, _images
+
+    cur = np.load(os.path.join(LUND, "oracle_c1.npz"))
+    prev = np.load(os.path.join(LUND, "oracle_c1_prev.npz"))
+    np.testing.assert_array_equal(prev["pairs"], cur["pairs"])
+    np.testing.assert_array_equal(prev["match_count"], cur["match_count"])
+    np.testing.assert_array_equal(prev["status"], cur["status"])
+    np.testing.assert_array_equal(prev["n_inliers"], cur["n_inliers"])
+    masks = np.unpackbits(prev["masks"])[: len(cur["masks"])]
+    np.testing.assert_array_equal(masks, cur["masks"])
+
+    def close(R, t, p):
+        dR = np.rad2deg(np.linalg.norm(Rotation.from_matrix(R @ prev["R"][p].T).as_rotvec()))
+        dt = scenes.direction_angle_deg(t, prev["t"][p])
+        assert dR < 2e-3 and dt < 2e-3, (p, dR, dt)
+
+    for p in range(len(cur["pairs"])):
+        close(cur["R"][p], cur["t"][p], p)
+    gt, imgs = _images()
+    f, u0, v0 = gt["fx_u0_v0"]
+    kps = [oracle_mod.sift(oracle_mod.rgb_to_gray(imgs[i]), 5000)[:2] for i in range(3)]
+    off = np.concatenate([[0], np.cumsum(cur["match_count"])])
+    pairs = [tuple(map(int, q)) for q in cur["pairs"]]
+    for i1, i2 in ((0, 1), (0, 2), (1, 2)):
+        p = pairs.index((i1, i2))
+        m = oracle_mod.twoway_match(kps[i1][1], kps[i2][1], 0.8).reshape(-1, 2).astype(np.int64)
+        np.testing.assert_array_equal(m, cur["matches"][off[p]: off[p + 1]])
+        x1 = (kps[i1][0][m[:, 0], :2].astype(np.float64) - [u0, v0]) / f
+        x2 = (kps[i2][0][m[:, 1], :2].astype(np.float64) - [u0, v0]) / f
+        _, mask, R, t, n, _ = oracle_mod.ransac_E(x1, x2, 4.0 / f, pair_id=0)
+        assert n == prev["n_inliers"][p]
+        np.testing.assert_array_equal(mask, masks[off[p]: off[p + 1]])
+        close(R, t, p)

@@ -141,6 +141,32 @@ def test_topk_many_ties_periodic_texture(dev, oracle_mod):
         np.testing.assert_array_equal(desc, rdesc)
 
 
+def _hard_edges(H, W):
+    """0/255 checkerboard of 7-px squares plus a diagonal step: the steepest gradients a u8 image can give."""
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = np.where(((yy // 7) + (xx // 7)) % 2 == 0, 0, 255)
+    img[(xx + yy) > (H + W) // 2] = 255 - img[(xx + yy) > (H + W) // 2]
+    img[yy > xx * 3] = 255
+    return np.ascontiguousarray(img.astype(np.uint8))
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_descriptor_fixed_point_paths_hard_edges(dev, oracle_mod, monkeypatch, wide):
+    """The descriptor's 2^24 fixed-point histogram has a one-conversion path (every weighted magnitude of the wave
+    below 255, where each contribution is below 2^32) and the split 64-bit conversion beside it. u8 images never reach
+    255 (the blur bounds the gradient), so the wide path is forced through GTSFM_SIFT_DESC_WIDE=1: both paths must be
+    bit-exact vs the oracle on the hardest edges a u8 image has."""
+    if wide:
+        monkeypatch.setenv("GTSFM_SIFT_DESC_WIDE", "1")
+    for H, W, k in ((120, 160, 300), (240, 320, 1000)):
+        gray = _hard_edges(H, W)
+        kp, desc, nd = _gpu_sift(gray, k)
+        rkp, rdesc, rnd = oracle_mod.sift(gray, k)
+        assert nd == rnd and nd > 50
+        np.testing.assert_array_equal(kp, rkp)
+        np.testing.assert_array_equal(desc, rdesc)
+
+
 def test_image_mask_bit_exact_vs_oracle(dev, oracle_mod):
     """detectAndCompute(gray, image.mask) (reference sift.py:47): keypoints on zero mask pixels are dropped before the
     top-k; through the drop-in and the batched generator, mixed masked / unmasked images of one size."""

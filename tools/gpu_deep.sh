@@ -1,6 +1,6 @@
 #!/bin/bash
 # Deep configs on one GPU call: the C3 and C5 bench lines (with their CPU baselines), then the per-kernel PMC passes
-# whose summaries bench.py reads for their roofline "traffic".   tools/gpu_deep_r04.sh TAG
+# whose summaries bench.py reads for their roofline "traffic".   tools/gpu_deep.sh TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=${1:-r04}

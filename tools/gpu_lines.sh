@@ -1,5 +1,5 @@
 #!/bin/bash
-# The other BASELINE configs' bench lines with their CPU baselines.   tools/gpu_r04_lines.sh TAG cfg...
+# The other BASELINE configs' bench lines with their CPU baselines.   tools/gpu_lines.sh TAG cfg...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 TAG=$1; shift
