@@ -430,6 +430,14 @@ def main_frontend(args, info, config: str):
     rank, world, dev = info.rank, info.world, info.device
     native.lib()
     deep = config in ("c3", "c5")
+    emulate = args.emulate_world > 1
+    if emulate:
+        # one process runs rank `emulate_rank`'s share of an `emulate_world`-rank job on this GPU (not a scaling run)
+        if world != 1:
+            raise SystemExit("--emulate-world runs in a single process (--gpus 1)")
+        if not 0 <= args.emulate_rank < args.emulate_world:
+            raise SystemExit("--emulate-rank must be in [0, --emulate-world)")
+        rank, world = args.emulate_rank, args.emulate_world
     want_baseline = rank == 0 and world == 1 and not args.no_cpu_baseline
     if config == "c1":
         all_imgs, intrinsics = lund_door_c1()
@@ -454,8 +462,8 @@ def main_frontend(args, info, config: str):
         kpts = args.kpts if not (config == "c3" and args.kpts == 2048) else 4096
         mine = sharding.local_images(n_img, world, rank)
         # every rank renders (seeded, identical cameras) only the images it extracts; rendering is data generation
-        scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine,
-                                       path="strafe" if config == "c3" else "orbit")
+        path = "strafe" if config == "c3" else "orbit"
+        scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine, path=path)
         host_images = scene.images.cpu().pin_memory()
         intrinsics = scene.intrinsics
         del scene.images
@@ -480,12 +488,38 @@ def main_frontend(args, info, config: str):
     if deep:
         sp_sd, sp_w, sg_sd, sg_w = deep_weights(dev, config == "c5", head=True if config == "c5" else "c3")
         kernels = HipSuperPointKernels(sp_w, "superglue" if config == "c5" else "twoway", sg_w)
-    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg, kernels=kernels)
+    exchange, kc_all = None, np.zeros(n_img)
+    if emulate:
+        # untimed: the other ranks' extraction and packed exchange blocks, produced here one rank at a time
+        blocks = {}
+        for r in range(world):
+            if r == rank:
+                continue
+            idx_r = sharding.local_images(n_img, world, r)
+            if config == "c1":
+                imgs_r = all_imgs[torch.from_numpy(idx_r)].contiguous()
+            else:
+                imgs_r = synthetic.render_scene(n_img, H, W, device=str(dev), indices=idx_r, path=path).images.cpu()
+            fe_r = AllPairsFrontEnd(imgs_r, intrinsics, n_img, r, world, dev, cfg, kernels=kernels,
+                                    image_pairs=np.zeros((0, 2), np.int64))
+            fe_r._extract(resident=False)
+            blocks[r] = fe_r.packed_features()
+            kc_all[idx_r] = fe_r.feats.count.cpu().numpy()
+            del fe_r, imgs_r
+            torch.cuda.empty_cache()
+        nbytes = next(iter(blocks.values())).numel()
+        others = torch.zeros((world, nbytes), dtype=torch.uint8, device=dev)
+        for r, b in blocks.items():
+            others[r].copy_(b)
+        del blocks
+        exchange = sharding.EmulatedAllGather(others, rank)
+    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg, kernels=kernels, exchange=exchange)
 
     for _ in range(args.warmup):
         res = fe.step()
-    elapsed = timed_steps(fe, args.steps, False, world, dev)
-    elapsed_res = timed_steps(fe, args.steps, True, world, dev)
+    tworld = 1 if emulate else world  # the emulated job has one process
+    elapsed = timed_steps(fe, args.steps, False, tworld, dev)
+    elapsed_res = timed_steps(fe, args.steps, True, tworld, dev)
     # `value` is the device-resident figure (inputs in HBM when the timed region starts); the host-to-host figure of
     # SURVEY.md §8(d) (PCIe copies inside the step) is reported beside it, never as value
     ms_per_step = elapsed_res / args.steps * 1e3
@@ -519,10 +553,10 @@ def main_frontend(args, info, config: str):
     n_ok = torch.tensor([float(res.isp_ok.sum())], dtype=torch.float64, device=dev)
     n_inl_rows = torch.tensor([float(len(res.v_corr))], dtype=torch.float64, device=dev)
     # per-stage algorithmic work of this rank
-    kc = np.zeros(n_img)
+    kc = kc_all
     kc[mine] = res.kp_count
     stats = {k: v.double() for k, v in fe.stats.items()}
-    if world > 1:
+    if world > 1 and not emulate:
         t = torch.from_numpy(kc).to(dev)
         torch.distributed.all_reduce(t)
         kc = t.cpu().numpy()
@@ -660,12 +694,25 @@ def main_frontend(args, info, config: str):
         "stage_ms_host_to_host": st_host,
         "roofline": roof,
     }
+    if emulate:
+        # a per-rank measurement, not a scaling curve: value = this rank's pairs per second of its own step
+        out["metric"] = "per-rank verified image-pairs/sec (one rank's share of an N-GPU job, emulated on one GPU)"
+        out["value"] = round(fe.P / (elapsed_res / args.steps), 2)
+        out["n_gpus"] = 1
+        out["scaling"] = "per-rank"
+        out["emulated"] = {
+            "rank": rank, "world": world, "rank_images": fe.n_local, "rank_pairs": fe.P, "job_pairs": fe.total_pairs,
+            "implied_job_pairs_per_s_if_ranks_equal": round(fe.total_pairs / (elapsed_res / args.steps), 2),
+            "note": "rank `rank` of a `world`-rank job run alone on one GPU: its images extracted, the exchange's "
+                    "packing + the gathered buffer's write (the other ranks' blocks extracted untimed beforehand; "
+                    "the xGMI transfer of the all-gather is NOT included), its contiguous pair block matched, "
+                    "verified and compacted"}
     if want_baseline:
         if deep:
             out["cpu_baseline"] = deep_cpu_baseline(baseline_images, intrinsics, n_img, kpts, sp_sd, sg_sd)
         else:
             out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts)
-    if rank == 0:
+    if rank == 0 or emulate:
         print(json.dumps(out), flush=True)
 
 
@@ -686,6 +733,9 @@ def main():
     ap.add_argument("--ba", action="store_true",
                     help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2-weak", "c4", "c3-match", "c3", "c5"])
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="run ONE rank's share of an N-rank job on this GPU (per-rank step time; not a scaling run)")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--launch-probe", action="store_true",
                     help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")
     args = ap.parse_args()

@@ -131,6 +131,10 @@ __global__ void pack_code_kernel(const float* __restrict__ desc, const int* __re
 // min, so its timing does not matter), by when the C1 return has long arrived.
 // Rows: value-only top-2 in registers across a pass; at the pass's last unit one 5-step halving exchange leaves lane
 // l of each half-wave with row l's top-2, stored to rowres.
+// Pass split (n_split > 1): a group's passes are cut into n_split contiguous ranges, one workgroup each, when there
+// are too few groups to fill the CUs (e.g. one rank's share of C2 at 8 GPUs: 619 pairs, ~155 groups of 4). Rows are
+// per pass, so they need nothing; each workgroup's column state then folds into colres (preset to kNoKey) with the
+// same pair of returning atomics as inside the workgroup, on global memory: min on C1, min(max(old, k1), k2) on C2.
 // ---------------------------------------------------------------------------------------------
 constexpr int kPpGroupWaves = 4;
 constexpr int kPpWaves = 2 * kPpGroupWaves;
@@ -231,8 +235,8 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
                                                                const int* __restrict__ counts,
                                                                const int* __restrict__ pairs, int n_pairs,
                                                                const int* __restrict__ groups, int n_groups,
-                                                               int group_size, int kpad, int kmax, int kmax64, int ib,
-                                                               uint2* __restrict__ rowres,
+                                                               int group_size, int n_split, int kpad, int kmax,
+                                                               int kmax64, int ib, uint2* __restrict__ rowres,
                                                                uint2* __restrict__ colres) {
     using Cfg = PpCfg<NK>;
     __shared__ __attribute__((aligned(1024))) unsigned char ring[2 * Cfg::kUnitBytes];
@@ -241,9 +245,12 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
 
     const int tid = threadIdx.x, wave = uniform(tid >> 6), lane = tid & 63;
     const int lrow = lane & 31, half = lane >> 5, grp = wave >> 2;
-    // bijective XCD remap (blocks b, b + 8, ... share an XCD and take consecutive groups)
-    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_groups >> 3, r8 = n_groups & 7;
-    const int grp_idx = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
+    // bijective XCD remap (blocks b, b + 8, ... share an XCD and take consecutive (group, split) units: the splits
+    // of one group stream the same B images through that XCD's L2)
+    const int n_blk = n_groups * n_split;
+    const int blk = blockIdx.x, xcd = blk & 7, q8 = n_blk >> 3, r8 = n_blk & 7;
+    const int flat = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blk >> 3);
+    const int grp_idx = flat / n_split, split = flat - grp_idx * n_split;
     const int G = groups ? group_size : 1;
 
     if (tid < kMaxGroup) {
@@ -271,8 +278,11 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         r.na = uniform(si[3]); r.nb = uniform(si[4]); r.nsup = uniform(si[5]);
         return r;
     };
-    int npass = 0;
-    for (int s = 0; s < G; ++s) npass = max(npass, (slot_info(s).na + kPpRowsPerPass - 1) / kPpRowsPerPass);
+    int npass_all = 0;
+    for (int s = 0; s < G; ++s) npass_all = max(npass_all, (slot_info(s).na + kPpRowsPerPass - 1) / kPpRowsPerPass);
+    // this workgroup's passes [pass_lo, npass)
+    const int pass_per = (npass_all + n_split - 1) / n_split;
+    const int pass_lo = min(npass_all, split * pass_per), npass = min(npass_all, pass_lo + pass_per);
     auto seek = [&](PpIter& it) {  // from (pass, slot) onwards to the first active (pass, slot)
         while (it.pass < npass) {
             it.cur = slot_info(it.slot);
@@ -289,7 +299,8 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         seek(it);
     };
     PpIter first;
-    first.pass = first.slot = first.sc = first.seq = 0;
+    first.slot = first.sc = first.seq = 0;
+    first.pass = pass_lo;
     seek(first);
     int n_units = 0;
     for (PpIter it = first; it.valid; ) {  // whole slots at a time
@@ -508,7 +519,17 @@ __global__ __launch_bounds__(kPpThreads, 1) void mnn_pp_kernel(const _Float16* _
         if (si.pair < 0 || si.na == 0) continue;
         const uint32_t* c1s = colstate + s * 2 * kmax64;
         const uint32_t* c2s = c1s + kmax64;
-        for (int c = tid; c < si.nb; c += kPpThreads) colres[(size_t)si.pair * kmax + c] = make_uint2(c1s[c], c2s[c]);
+        if (n_split == 1) {
+            for (int c = tid; c < si.nb; c += kPpThreads)
+                colres[(size_t)si.pair * kmax + c] = make_uint2(c1s[c], c2s[c]);
+        } else if (pass_lo * kPpRowsPerPass < si.na) {  // this workgroup saw rows of the pair
+            for (int c = tid; c < si.nb; c += kPpThreads) {
+                uint32_t* g = (uint32_t*)(colres + (size_t)si.pair * kmax + c);
+                const uint32_t k1 = c1s[c], k2 = c2s[c];
+                const uint32_t old = __hip_atomic_fetch_min(g, k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_min(g + 1, umin(umax(old, k1), k2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 }
 
@@ -790,6 +811,31 @@ int pp_max_group(int kmax, int dim) {
     return 0;
 }
 
+// Pass split of a launch: the n_split in {1, 2, 4} (at most the passes of kmax rows) that minimises the estimated
+// time ceil(n_groups * n_split / CUs) * (passes / n_split) of one workgroup per CU; ties keep fewer workgroups.
+// gtsfm_amd.device.match_plan mirrors this to choose the group size.
+int pp_split(int n_groups, int kmax, int n_cu) {
+    const int npass = (kmax + kPpRowsPerPass - 1) / kPpRowsPerPass;
+    int best = 1;
+    double best_t = 1e300;
+    for (int s = 1; s <= 4 && s <= npass; s *= 2) {
+        const double t = (double)((n_groups * s + n_cu - 1) / n_cu) * ((npass + s - 1) / s);
+        if (t < best_t) { best_t = t; best = s; }
+    }
+    return best;
+}
+
+int device_cu_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+    }
+    return n;
+}
+
 template <int NK, bool kClamp>
 int launch_pp_t(const _Float16* a_form, const _Float16* b_form, const int* counts, const int* pairs, int n_pairs,
                 const int* groups, int n_groups, int group_size, int kpad, int kmax, int ib, int dim, uint2* rowres,
@@ -797,10 +843,18 @@ int launch_pp_t(const _Float16* a_form, const _Float16* b_form, const int* count
     const int gs = groups ? group_size : 1;
     if (pp_lds_bytes<NK>(kmax, gs) > (size_t)kPpLdsBudget) return GTSFM_ERR_ARG;
     const size_t lds = pp_dyn_lds_bytes(kmax, gs);
+    int n_split = pp_split(n_groups, kmax, device_cu_count());
+    // test hook: GTSFM_MATCH_PASS_SPLIT=1|2|4 forces the split, so tests can pin every path against the oracle
+    if (const char* f = getenv("GTSFM_MATCH_PASS_SPLIT")) {
+        const int v = atoi(f);
+        if (v == 1 || v == 2 || v == 4) n_split = v;
+    }
+    if (n_split > 1)  // the workgroups fold their column state into colres with atomics
+        GTSFM_CHECK_HIP(hipMemsetAsync(colres, 0xFF, (size_t)n_pairs * kmax * sizeof(uint2), stream));
     GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)mnn_pp_kernel<NK, kClamp>, (int)lds));
-    hipLaunchKernelGGL((mnn_pp_kernel<NK, kClamp>), dim3(n_groups), dim3(kPpThreads), lds, stream, a_form, b_form,
-                       counts, pairs, n_pairs, groups, n_groups, group_size, kpad, kmax, pp_kmax64(kmax), ib, rowres,
-                       colres);
+    hipLaunchKernelGGL((mnn_pp_kernel<NK, kClamp>), dim3(n_groups * n_split), dim3(kPpThreads), lds, stream, a_form,
+                       b_form, counts, pairs, n_pairs, groups, n_groups, group_size, n_split, kpad, kmax,
+                       pp_kmax64(kmax), ib, rowres, colres);
     return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
 }
 

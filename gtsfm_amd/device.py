@@ -77,6 +77,39 @@ def match_group_size(kmax: int, dim: int) -> int:
     return int(native.lib().gtsfm_match_max_group(int(kmax), int(dim)))
 
 
+def _split_cost(n_groups: int, group_size: int, kmax: int, n_cu: int) -> float:
+    """Estimated time (in pair-passes of one workgroup) of a grouped distance-GEMM launch, with the pass split the
+    library picks for it (matcher.hip pp_split: n_split in {1, 2, 4} minimising ceil(n_groups * n_split / CUs) *
+    (passes / n_split))."""
+    npass = -(-kmax // 512)
+    best = None
+    s = 1
+    while s <= 4 and s <= npass:
+        t = -(-(n_groups * s) // n_cu) * -(-npass // s)
+        best = t if best is None or t < best else best
+        s *= 2
+    return float(best) * group_size
+
+
+def match_plan(pairs: np.ndarray, kmax: int, dim: int, n_cu: Optional[int] = None) -> Optional[np.ndarray]:
+    """Pair groups for the INT_F16 distance GEMM (gtsfm_match_batched_grouped), sized to fill the GPU: the largest
+    group size (most reuse of the register operand) is kept unless a smaller one, together with the library's pass
+    split, finishes in fewer estimated workgroup rounds. A rank's share of C2 at 8 GPUs (619 pairs) has ~155 groups of
+    4 for 256 CUs: groups of 1 split into 2 pass ranges (1238 workgroups) take 10 pair-passes of time instead of 16."""
+    gmax = match_group_size(kmax, dim)
+    if gmax <= 1:
+        return None
+    if n_cu is None:
+        n_cu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+            if torch.cuda.is_available() else 256
+    plans = [(g, pair_groups(pairs, g)) for g in range(gmax, 0, -1)]
+    cost = [_split_cost(len(groups), g, kmax, n_cu) for g, groups in plans]
+    # the estimate ignores what a smaller group loses (the register operand re-read per pair, more workgroups):
+    # a smaller group must win by more than 10 %
+    best = min(cost)
+    return next(groups for (g, groups), t in zip(plans, cost) if t <= 1.1 * best)
+
+
 def pair_groups(pairs: np.ndarray, group_size: int) -> np.ndarray:
     """Tile an (P, 2) pair list into groups for the INT_F16 distance GEMM: each group = up to `group_size` pairs
     (i1, i2) sharing i1 (the register operand) with i2 in one block of `group_size` consecutive image ids, ordered

@@ -79,9 +79,8 @@ class HipKernels:
         self._dev.sift_extract(images, kpts, out=out, workspace=workspace)
 
     def match_groups(self, pairs: np.ndarray, kmax: int, dim: int) -> Optional[np.ndarray]:
-        """Block-tiled pair groups for the distance GEMM (gtsfm_match_batched_grouped), or None."""
-        g = self._dev.match_group_size(kmax, dim)
-        return self._dev.pair_groups(pairs, g) if g > 1 else None
+        """Block-tiled pair groups for the distance GEMM (gtsfm_match_batched_grouped), sized to fill the GPU, or None."""
+        return self._dev.match_plan(pairs, kmax, dim)
 
     def match(self, f: "Features", pairs, ratio, groups=None, image_hw=None, out=None):
         return self._dev.match_pairs(f.desc, f.count, pairs, ratio, self._native.GTSFM_MATCH_INT_F16, groups=groups,
@@ -196,10 +195,13 @@ class AllPairsFrontEnd:
 
     def __init__(self, host_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, rank: int, world: int,
                  device: torch.device, cfg: Optional[FrontEndConfig] = None, kernels=None,
-                 image_pairs: Optional[np.ndarray] = None):
+                 image_pairs: Optional[np.ndarray] = None, exchange=None):
         """image_pairs: (P, 2) global (i1, i2) pairs to match and verify, e.g. a retriever's output
-        (gtsfm_amd.retriever; image_pairs_generator.py:29-47); None = every pair (ExhaustiveRetriever)."""
+        (gtsfm_amd.retriever; image_pairs_generator.py:29-47); None = every pair (ExhaustiveRetriever).
+        exchange: None (the collective over torch.distributed), or a sharding.EmulatedAllGather when one process runs
+        rank `rank`'s share of a `world`-rank job (bench.py --emulate-world)."""
         self.cfg = cfg or FrontEndConfig()
+        self.exchange = exchange
         self.kern = kernels if kernels is not None else HipKernels()
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
@@ -339,6 +341,12 @@ class AllPairsFrontEnd:
         if self.cuda and not resident:
             self._mark("h2d_end", self.copy_stream)
 
+    def packed_features(self) -> torch.Tensor:
+        """This rank's packed exchange block of the last extraction (what it contributes to the all-gather)."""
+        fields = getattr(self.kern, "gather", (("xy", None), ("desc", torch.uint8), ("count", None)))
+        return sharding.pack_features([getattr(self.feats, n) for n, _ in fields], self.n_per,
+                                      wire=[w for _, w in fields])[0]
+
     def step(self, resident: bool = False) -> Optional[HostResults]:
         """One pass of the front-end over this rank's share.
 
@@ -354,7 +362,7 @@ class AllPairsFrontEnd:
         # the one exchange: the fields the pair stages read, each in the kernel set's wire dtype (one collective)
         fields = getattr(self.kern, "gather", (("xy", None), ("desc", torch.uint8), ("count", None)))
         got = sharding.allgather_features([getattr(self.feats, n) for n, _ in fields], self.n_per,
-                                          wire=[w for _, w in fields])
+                                          wire=[w for _, w in fields], exchange=self.exchange)
         f_all = Features(**{n: None for n in ("xy", "attr", "desc", "count", "n_detected")})
         for (n, _), t in zip(fields, got):
             setattr(f_all, n, t)

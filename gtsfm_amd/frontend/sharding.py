@@ -51,20 +51,10 @@ def rank_pairs(pairs: np.ndarray, world: int, rank: int) -> np.ndarray:
     return np.arange(min(rank * per, len(pairs)), min((rank + 1) * per, len(pairs)), dtype=np.int64)
 
 
-def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
-                       group: Optional[torch.distributed.ProcessGroup] = None,
-                       wire: Optional[Sequence[Optional[torch.dtype]]] = None) -> Tuple[torch.Tensor, ...]:
-    """Pads each rank's (n_local, ...) feature tensors to n_per rows and all-gathers them rank-major, in ONE
-    collective: the tensors are packed byte-wise into a single per-rank block (each field 16-byte aligned), gathered
-    with one all_gather_into_tensor, and unpacked as views of the gathered buffer.
-
-    wire[i] (optional) is the dtype tensor i travels in; it is cast back afterwards, so the caller must only name a
-    lossless one: SIFT descriptors are integers in [0, 255], so u8 carries them exactly (2048 x 128 B per image
-    instead of 4x that in f32). With world == 1 the inputs are returned unchanged.
-    """
-    world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
-    if world == 1:
-        return tuple(tensors)
+def pack_features(tensors: Sequence[torch.Tensor], n_per: int,
+                  wire: Optional[Sequence[Optional[torch.dtype]]] = None) -> Tuple[torch.Tensor, list]:
+    """One rank's feature tensors padded to n_per rows and packed byte-wise into a single block (each field 16-byte
+    aligned, in its wire dtype). Returns (block (off,) uint8, layout) for unpack_features."""
     fields, layout, off = [], [], 0
     for i, t in enumerate(tensors):
         dtype = t.dtype
@@ -80,18 +70,66 @@ def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
         layout.append((off, nbytes, t.dtype, tuple(t.shape), dtype))
         fields.append(raw)
         off += -(-nbytes // 16) * 16
-    dev = tensors[0].device
-    block = torch.zeros(off, dtype=torch.uint8, device=dev)
+    block = torch.zeros(off, dtype=torch.uint8, device=tensors[0].device)
     for raw, (o, nb, _, _, _) in zip(fields, layout):
         block[o: o + nb] = raw
-    g = torch.empty(world * off, dtype=torch.uint8, device=dev)
-    torch.distributed.all_gather_into_tensor(g, block, group=group)
-    g = g.view(world, off)
+    return block, layout
+
+
+def unpack_features(g: torch.Tensor, layout: list) -> Tuple[torch.Tensor, ...]:
+    """(world, off) gathered blocks -> the rank-major (world * n_per, ...) feature tensors, cast back."""
+    world = g.shape[0]
     out = []
     for o, nb, wdt, shape, dtype in layout:
         f = g[:, o: o + nb].contiguous().view(wdt).view((world * shape[0],) + shape[1:])
         out.append(f if f.dtype == dtype else f.to(dtype))
     return tuple(out)
+
+
+def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
+                       group: Optional[torch.distributed.ProcessGroup] = None,
+                       wire: Optional[Sequence[Optional[torch.dtype]]] = None,
+                       exchange=None) -> Tuple[torch.Tensor, ...]:
+    """Pads each rank's (n_local, ...) feature tensors to n_per rows and all-gathers them rank-major, in ONE
+    collective: the tensors are packed byte-wise into a single per-rank block (each field 16-byte aligned), gathered
+    with one all_gather_into_tensor, and unpacked as views of the gathered buffer.
+
+    wire[i] (optional) is the dtype tensor i travels in; it is cast back afterwards, so the caller must only name a
+    lossless one: SIFT descriptors are integers in [0, 255], so u8 carries them exactly (2048 x 128 B per image
+    instead of 4x that in f32). With world == 1 the inputs are returned unchanged.
+
+    exchange (optional): an EmulatedAllGather standing in for the collective (one process running one rank's share
+    of a larger job on one GPU); the packing and unpacking around it are the real ones.
+    """
+    if exchange is not None:
+        block, layout = pack_features(tensors, n_per, wire)
+        return unpack_features(exchange(block), layout)
+    world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
+    if world == 1:
+        return tuple(tensors)
+    block, layout = pack_features(tensors, n_per, wire)
+    off = block.numel()
+    g = torch.empty(world * off, dtype=torch.uint8, device=block.device)
+    torch.distributed.all_gather_into_tensor(g, block, group=group)
+    return unpack_features(g.view(world, off), layout)
+
+
+class EmulatedAllGather:
+    """The all-gather of rank `rank` in a `world`-rank job, emulated in one process on one GPU: the other ranks'
+    packed blocks were produced beforehand (their extraction, untimed) and sit in `others` (world, off); a call copies
+    them and this rank's fresh block into the gathered buffer, i.e. the bytes the collective would write here. The
+    xGMI transfer itself is not included (bench.py --emulate-world reports that)."""
+
+    def __init__(self, others: torch.Tensor, rank: int):
+        self.others, self.rank = others, rank
+
+    def __call__(self, block: torch.Tensor) -> torch.Tensor:
+        if block.numel() != self.others.shape[1]:
+            raise ValueError(f"block of {block.numel()} bytes, the emulated job packs {self.others.shape[1]}")
+        g = torch.empty_like(self.others)
+        g.copy_(self.others)
+        g[self.rank].copy_(block)
+        return g
 
 
 def gather_pair_results(local: torch.Tensor, n_pairs: int,

@@ -201,6 +201,33 @@ def test_grouped_workgroups_vs_oracle(dev, oracle_mod):
             np.testing.assert_array_equal(idx[p, : cnt[p]], refs[p], err_msg=f"pair {tuple(pairs[p])}")
 
 
+@pytest.mark.parametrize("split", ["1", "2", "4"])
+def test_pass_split_vs_oracle(dev, oracle_mod, monkeypatch, split):
+    """A group's 512-row passes cut over 1, 2 or 4 workgroups (the split the library picks when a launch has too few
+    groups to fill the CUs, forced here through GTSFM_MATCH_PASS_SPLIT): rows per pass, columns folded into colres
+    by global atomics. Ragged counts leave some splits with no rows of a pair; every pair equals the oracle."""
+    from gtsfm_amd import device, native
+
+    monkeypatch.setenv("GTSFM_MATCH_PASS_SPLIT", split)
+    rng = np.random.default_rng(47)
+    counts = [2048, 1300, 2048, 700, 1999, 513, 1537, 1]
+    descs = [_sift_like(rng, n) for n in counts]
+    for i in range(1, len(counts)):
+        k = min(counts[i], counts[0]) // 3
+        descs[i][:k] = np.clip(descs[0][:k] + rng.integers(-6, 7, size=(k, 128)), 0, 255)
+    d, c = _batch(dev, descs)
+    pairs = np.array([(i, j) for i in range(len(counts)) for j in range(len(counts)) if i != j], np.int32)
+    pt = torch.from_numpy(pairs).to(dev)
+    refs = [oracle_mod.twoway_match(descs[i], descs[j], 0.8) for i, j in pairs]
+    G = device.match_group_size(max(counts), 128)
+    for groups in (None, torch.from_numpy(device.pair_groups(pairs, G)).to(dev)):
+        idx, cnt = device.match_pairs(d, c, pt, 0.8, native.GTSFM_MATCH_INT_F16, groups=groups)
+        idx = idx.cpu().numpy().view(np.uint32)
+        cnt = cnt.cpu().numpy()
+        for p in range(len(pairs)):
+            np.testing.assert_array_equal(idx[p, : cnt[p]], refs[p], err_msg=f"pair {tuple(pairs[p])}")
+
+
 def test_contract_edge_norms_exact(dev, oracle_mod):
     """Descriptors at the INT_F16 contract's edge (values up to 1023, squared norms just under 2^19): the folded
     accumulator d2 + code/16 stays exact, so the matches equal the oracle's."""

@@ -103,3 +103,50 @@ def test_gloo_sharded_front_end_matches_single_process(world, tmp_path, oracle_m
     for r in range(world):
         got = np.load(tmp_path / f"counts_{world}_{r}.npy")
         assert np.array_equal(got, np.array(ref))
+
+
+def test_match_plan_fills_the_gpu():
+    """match_plan keeps groups of 4 at C2 (4950 pairs: 1238 groups, 5 full rounds) and, for one rank's share of C2 at
+    8 GPUs (619 pairs), picks smaller groups whose pass-split workgroups take 10 instead of 16 pair-passes."""
+    from gtsfm_amd import device, native
+    from gtsfm_amd.frontend import sharding
+
+    native.lib()
+    pairs = sharding.all_pairs(100)
+    g = device.match_plan(pairs, 2048, 128, n_cu=256)
+    assert g.shape[1] == 4
+    share = pairs[sharding.rank_pairs(pairs, 8, 0)]
+    g8 = device.match_plan(share, 2048, 128, n_cu=256)
+    assert g8.shape[1] < 4
+    assert device._split_cost(len(g8), g8.shape[1], 2048, 256) <= 10
+    assert sorted(g8[g8 >= 0].tolist()) == list(range(len(share)))
+
+
+def test_emulated_allgather_equals_rank_major_gather():
+    """One process emulating rank r of a 3-rank job (bench.py --emulate-world): the other ranks' packed blocks plus
+    this rank's fresh block unpack to exactly the tensors the real all-gather produces (rank-major, padded to n_per,
+    u8 wire for the descriptors)."""
+    from gtsfm_amd.frontend import sharding
+
+    n_img, world = 7, 3
+    n_per = sharding.images_per_rank(n_img, world)
+    g = torch.Generator().manual_seed(3)
+    full_xy = torch.rand((n_img, 5, 2), generator=g)
+    full_desc = torch.randint(0, 256, (n_img, 5, 8), generator=g).float()
+    full_cnt = torch.randint(1, 6, (n_img,), generator=g, dtype=torch.int32)
+    wire = [None, torch.uint8, None]
+
+    def local(r):
+        i = torch.from_numpy(sharding.local_images(n_img, world, r))
+        return [full_xy[i], full_desc[i], full_cnt[i]]
+
+    blocks = [sharding.pack_features(local(r), n_per, wire)[0] for r in range(world)]
+    for rank in range(world):
+        others = torch.stack(blocks)
+        others[rank].zero_()
+        got = sharding.allgather_features(local(rank), n_per, wire=wire,
+                                          exchange=sharding.EmulatedAllGather(others, rank))
+        slot = sharding.global_slots(n_img, world)
+        for t, ref in zip(got, (full_xy, full_desc, full_cnt)):
+            assert t.shape[0] == world * n_per and t.dtype == ref.dtype
+            assert torch.equal(t[torch.from_numpy(slot)], ref)
