@@ -21,7 +21,8 @@ busy = collections.defaultdict(lambda: [0, 0.0])
 gap, last_end = 0.0, t0
 for r in step:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    name = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")[:60]
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    name = name.split("(")[0][:60]
     busy[name][0] += 1
     busy[name][1] += (e - s) / 1e6
     if s > last_end:
