@@ -363,8 +363,14 @@ def deep_weights(dev, superglue: bool, head=True):
     return sd, sp, sgd, torch.from_numpy(pack_superglue_weights(sgd)).to(dev)
 
 
+def deep_sample(config: str) -> int:
+    """Images in the deep configs' CPU-baseline sample: 7 for C3 (21 pairs, ~25 s on 16 threads), 6 for C5 (15
+    SuperGlue pairs at ~1.9 s each, ~45 s)."""
+    return 7 if config == "c3" else 6
+
+
 def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_sd, sg_sd, threads: int = 16,
-                      n_img_sample: int = 5) -> dict:
+                      n_img_sample: int = 6) -> dict:
     """CPU restatement of the deep front-end timed on `threads` host threads over a bounded sample, scaled to n_img
     images / all their pairs: oracle/deep.py's SuperPoint (torch fp32 on the host, `threads` intra-op threads, as the
     reference's torch modules run on a CPU) on n_img_sample images spread over the scene, then for every pair among
@@ -470,7 +476,7 @@ def main_frontend(args, info, config: str):
         torch.cuda.empty_cache()
         baseline_images = None
         if want_baseline:
-            baseline_images = host_images.numpy()[sample_images(n_img, 5 if deep else 16)]
+            baseline_images = host_images.numpy()[sample_images(n_img, deep_sample(config) if deep else 16)]
     cfg = FrontEndConfig(kpts=kpts, ratio=RATIO, thresh_px=THRESH_PX, min_inliers=MIN_INLIERS,
                          min_inlier_ratio=MIN_INLIER_RATIO)
     if deep:
@@ -709,7 +715,8 @@ def main_frontend(args, info, config: str):
                     "verified and compacted"}
     if want_baseline:
         if deep:
-            out["cpu_baseline"] = deep_cpu_baseline(baseline_images, intrinsics, n_img, kpts, sp_sd, sg_sd)
+            out["cpu_baseline"] = deep_cpu_baseline(baseline_images, intrinsics, n_img, kpts, sp_sd, sg_sd,
+                                                    n_img_sample=deep_sample(config))
         else:
             out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts)
     if rank == 0 or emulate:

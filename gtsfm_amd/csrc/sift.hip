@@ -527,20 +527,19 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 
 // DoG levels are never stored: DoG_l = G_{l+1} - G_l is recomputed from the Gaussian levels (the same fp32
 // subtraction cv::subtract performs), which removes 5 level writes per octave.
-// Extrema scan: each wave sweeps a strip of kExStrip rows down 64 consecutive columns starting at a multiple of 64
-// (every lane produces an output; a wave's row of one level is two whole 128-B lines), one image row per step. Per
-// row a lane loads Gaussian levels 1..4 at its pixel (coalesced 256-B rows, saddr + 32-bit offset) plus one halo
-// column (c0 - 1 for lanes 0..31, c0 + 64 for lanes 32..63: two addresses per wave, lines the neighbouring windows
-// read anyway), forms DoG 1..3, gets its horizontal neighbours by wave-wide DPP shifts (lanes 0 and 63 take the
-// halo's DoG instead), and keeps per DoG level the 3-wide row max/min of the last three rows in registers (rolling slots, the loop
+// Extrema scan: each wave sweeps a strip of kExStrip rows down 64 consecutive columns (lanes 1..62 produce outputs,
+// lanes 0 and 63 are the left/right halo), one image row per step. Per row a lane loads Gaussian levels 1..4 at its
+// pixel (coalesced 256-B rows, saddr + 32-bit offset), forms DoG 1..3, gets its horizontal neighbours by wave-wide DPP
+// shifts, and keeps per DoG level the 3-wide row max/min of the last three rows in registers (rolling slots, the loop
 // unrolled by three so no register moves). The 27-neighbourhood test "val >= every neighbour" is val == max over the
 // 3x3x3 block (the centre included), from those max3/min3 partials. The outer DoG levels 0 and 4 only matter for a
 // layer-1 / layer-3 pixel that already passed the threshold and beats its two in-register levels (a few per
 // thousand): they are queued in LDS and their 3x3 blocks gathered after the sweep, all lanes at once. Each pixel's
 // levels 1..4 are read once (plus 2 halo rows per strip and 2 halo lanes per wave): 16 B per pixel instead of all six
-// levels' 24. (Round 4's windows were 62 outputs wide with lanes 0 and 63 as halo: misaligned by one column, so
-// every wave row touched three 128-B lines for two lines of data.)
-constexpr int kExWaves = 4, kExOut = 64, kExStrip = 64;
+// levels' 24. Measured in round 5 and not kept: windows of 64 outputs aligned to 128-B lines, the halo columns
+// loaded separately (lanes 0 / 63 take them through the DPP's old operand): bit-exact, but 366 vs 367 us per launch
+// with the same FETCH_SIZE (the straddled lines are L2 hits) and 103 instead of 79 VGPRs (profiles/r05d_*).
+constexpr int kExWaves = 4, kExOut = 62, kExStrip = 64;
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
@@ -565,7 +564,7 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     __shared__ ExPend pend[kExPend];
     __shared__ int n_list, n_pend, gbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, b = blockIdx.z;
-    const int c0 = (blockIdx.x * kExWaves + wave) * kExOut, c = c0 + lane;  // this lane's column
+    const int c = (blockIdx.x * kExWaves + wave) * kExOut + lane - 1;  // this lane's column
     const int y0 = blockIdx.y * kExStrip;
     const int shard = (int)((blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z)) %
                             kCandShards);  // cap is per shard
@@ -578,8 +577,7 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
 #pragma unroll
     for (int l = 0; l < kLevels; ++l) gl[l] = G.g[l] + (size_t)b * H * W;
     const int cx = min(max(c, 0), W - 1);
-    const int hx = min(max(lane < 32 ? c0 - 1 : c0 + kExOut, 0), W - 1);  // halo column (lanes 0 / 63 use it)
-    const bool col_ok = c >= kBorder && c < W - kBorder;
+    const bool col_ok = lane >= 1 && lane <= kExOut && c >= kBorder && c < W - kBorder;
     const float threshold = floorf(0.5f * kContrast / kLayers * 255.f);
 
     // in registers: DoG levels 1..kLayers (index l - 1), from Gaussian levels 1..kLayers + 1
@@ -587,22 +585,17 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     float hmax[kIn][3], hmin[kIn][3], ctr[kLayers][3];
     // Row y (clamped) of Gaussian levels 1..4 -> g; then into slot s: DoG 1..3, their 3-wide row extrema, and the
     // centre values of layers 1..3.
-    // a row buffer: levels 1..4 at the lane's column, then at its halo column
-    constexpr int kBuf = 2 * kInLv;
-    auto fetch = [&](int y, float (&g)[kBuf]) {
-        const uint32_t row = (uint32_t)(min(max(y, 0), H - 1) * W);
+    auto fetch = [&](int y, float (&g)[kInLv]) {
+        const uint32_t off = (uint32_t)(min(max(y, 0), H - 1) * W + cx);
 #pragma unroll
-        for (int l = 0; l < kInLv; ++l) g[l] = gl[l + 1][row + cx];
-#pragma unroll
-        for (int l = 0; l < kInLv; ++l) g[kInLv + l] = gl[l + 1][row + hx];
+        for (int l = 0; l < kInLv; ++l) g[l] = gl[l + 1][off];
     };
-    auto finish = [&](const float (&g)[kBuf], auto slot) {
+    auto finish = [&](const float (&g)[kInLv], auto slot) {
         constexpr int s = decltype(slot)::value;
 #pragma unroll
         for (int l = 0; l < kIn; ++l) {
             const float d = g[l + 1] - g[l];
-            const float dh = g[kInLv + l + 1] - g[kInLv + l];  // the halo column's DoG (same fp32 subtraction)
-            const float lf = lane == 0 ? dh : dpp_from_left(d), rt = lane == 63 ? dh : dpp_from_right(d);
+            const float lf = dpp_from_left(d), rt = dpp_from_right(d);
             hmax[l][s] = fmaxf(fmaxf(lf, d), rt);
             hmin[l][s] = fminf(fminf(lf, d), rt);
             ctr[l][s] = d;
@@ -688,13 +681,13 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     // has been consumed (rows past the strip's last needed row y_end re-read row y_end, an L2 hit).
     const int y_end = min(y0 + kExStrip, H);
     {
-        float ga[kBuf], gb[kBuf];
+        float ga[kInLv], gb[kInLv];
         fetch(y0 - 1, ga);
         fetch(y0, gb);
         finish(ga, S0{});
         finish(gb, S1{});
     }
-    float g1[kBuf], g2[kBuf], g3[kBuf], g4[kBuf], g5[kBuf], g6[kBuf];
+    float g1[kInLv], g2[kInLv], g3[kInLv], g4[kInLv], g5[kInLv], g6[kInLv];
     fetch(y0 + 1, g1);
     fetch(y0 + 2, g2);
     fetch(y0 + 3, g3);
