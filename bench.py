@@ -444,6 +444,8 @@ def main_frontend(args, info, config: str):
         if not 0 <= args.emulate_rank < args.emulate_world:
             raise SystemExit("--emulate-rank must be in [0, --emulate-world)")
         rank, world = args.emulate_rank, args.emulate_world
+    elif args.pair_limit:
+        raise SystemExit("--pair-limit only applies to --emulate-world runs")
     want_baseline = rank == 0 and world == 1 and not args.no_cpu_baseline
     if config == "c1":
         all_imgs, intrinsics = lund_door_c1()
@@ -519,7 +521,8 @@ def main_frontend(args, info, config: str):
             others[r].copy_(b)
         del blocks
         exchange = sharding.EmulatedAllGather(others, rank)
-    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg, kernels=kernels, exchange=exchange)
+    fe = AllPairsFrontEnd(host_images, intrinsics, n_img, rank, world, dev, cfg, kernels=kernels, exchange=exchange,
+                          pair_limit=args.pair_limit or None)
 
     for _ in range(args.warmup):
         res = fe.step()
@@ -708,7 +711,9 @@ def main_frontend(args, info, config: str):
         out["scaling"] = "per-rank"
         out["emulated"] = {
             "rank": rank, "world": world, "rank_images": fe.n_local, "rank_pairs": fe.P, "job_pairs": fe.total_pairs,
-            "implied_job_pairs_per_s_if_ranks_equal": round(fe.total_pairs / (elapsed_res / args.steps), 2),
+            "implied_job_pairs_per_s_if_ranks_equal": None if args.pair_limit else
+            round(fe.total_pairs / (elapsed_res / args.steps), 2),
+            "pair_limit": args.pair_limit or None,
             "note": "rank `rank` of a `world`-rank job run alone on one GPU: its images extracted, the exchange's "
                     "packing + the gathered buffer's write (the other ranks' blocks extracted untimed beforehand; "
                     "the xGMI transfer of the all-gather is NOT included), its contiguous pair block matched, "
@@ -743,6 +748,8 @@ def main():
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="run ONE rank's share of an N-rank job on this GPU (per-rank step time; not a scaling run)")
     ap.add_argument("--emulate-rank", type=int, default=0)
+    ap.add_argument("--pair-limit", type=int, default=0,
+                    help="with --emulate-world: only the first K pairs of the rank's block (a bounded partial run)")
     ap.add_argument("--launch-probe", action="store_true",
                     help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")
     args = ap.parse_args()

@@ -195,11 +195,13 @@ class AllPairsFrontEnd:
 
     def __init__(self, host_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, rank: int, world: int,
                  device: torch.device, cfg: Optional[FrontEndConfig] = None, kernels=None,
-                 image_pairs: Optional[np.ndarray] = None, exchange=None):
+                 image_pairs: Optional[np.ndarray] = None, exchange=None, pair_limit: Optional[int] = None):
         """image_pairs: (P, 2) global (i1, i2) pairs to match and verify, e.g. a retriever's output
         (gtsfm_amd.retriever; image_pairs_generator.py:29-47); None = every pair (ExhaustiveRetriever).
         exchange: None (the collective over torch.distributed), or a sharding.EmulatedAllGather when one process runs
-        rank `rank`'s share of a `world`-rank job (bench.py --emulate-world)."""
+        rank `rank`'s share of a `world`-rank job (bench.py --emulate-world).
+        pair_limit: keep only the first pair_limit pairs of this rank's block (a bounded partial run of a job whose
+        full block would take minutes per step; bench.py --pair-limit)."""
         self.cfg = cfg or FrontEndConfig()
         self.exchange = exchange
         self.kern = kernels if kernels is not None else HipKernels()
@@ -247,6 +249,8 @@ class AllPairsFrontEnd:
                 raise ValueError("image_pairs must hold distinct image indices in [0, n_img)")
         self.total_pairs = len(pairs)
         block = sharding.rank_pairs(pairs, world, rank)
+        if pair_limit is not None:
+            block = block[: max(0, int(pair_limit))]
         self.pair_id_base = int(block[0]) if len(block) else 0  # global pair index keys the RANSAC sampler
         self.my_pairs = pairs[block]
         P = len(block)
