@@ -54,6 +54,15 @@ def _register_optional(l: ctypes.CDLL) -> None:
         l.oracle_ransac_E.argtypes = [_f64p, _f64p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                       ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _f64p, _u8p, _f64p, _f64p,
                                       ctypes.POINTER(ctypes.c_int)]
+        l.oracle_ransac_E_gc.restype = ctypes.c_int
+        l.oracle_ransac_E_gc.argtypes = [_f64p, _f64p, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                         ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                         ctypes.c_int, ctypes.c_int, _f64p, _u8p, _f64p, _f64p,
+                                         ctypes.POINTER(ctypes.c_int)]
+        l.oracle_gc_label_q.restype = ctypes.c_int
+        l.oracle_gc_label_q.argtypes = [np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS"),
+                                        np.ctypeslib.ndpointer(np.int64, flags="C_CONTIGUOUS"), ctypes.c_int,
+                                        ctypes.c_int64, ctypes.c_int64, _u8p]
         l.oracle_five_point.restype = ctypes.c_int
         l.oracle_five_point.argtypes = [_f64p, _f64p, _f64p]
         l.oracle_sample5.restype = ctypes.c_int
@@ -154,6 +163,34 @@ def ransac_E(x1n: np.ndarray, x2n: np.ndarray, thr: float, prob: float = 0.99999
     if n < 0:
         return None
     return E.reshape(3, 3), mask[:M].copy(), R.reshape(3, 3), t, n, nh.value
+
+
+def ransac_E_gc(x1n: np.ndarray, x2n: np.ndarray, thr: float, gc_iters: int, gc_cell: float, gc_lambda=(39, 40),
+                prob: float = 0.999999, max_iters: int = 1000, seed: int = RANSAC_SEED, pair_id: int = 0,
+                scoring: int = SCORING_MSAC):
+    """ransac_E followed by the graph-cut LO stage (oracle/ransac.c gc_label): gc_cell in normalised units,
+    gc_lambda = (num, den) of the spatial-coherence weight. Same return tuple as ransac_E."""
+    x1n = np.ascontiguousarray(x1n, np.float64)
+    x2n = np.ascontiguousarray(x2n, np.float64)
+    M = x1n.shape[0]
+    E, R, t = np.zeros(9), np.zeros(9), np.zeros(3)
+    mask = np.zeros(max(M, 1), np.uint8)
+    nh = ctypes.c_int(0)
+    n = lib().oracle_ransac_E_gc(x1n.ravel(), x2n.ravel(), M, thr, prob, max_iters, seed, pair_id, int(scoring),
+                                 int(gc_iters), float(gc_cell), int(gc_lambda[0]), int(gc_lambda[1]), E, mask, R, t,
+                                 ctypes.byref(nh))
+    if n < 0:
+        return None
+    return E.reshape(3, 3), mask[:M].copy(), R.reshape(3, 3), t, n, nh.value
+
+
+def gc_label_q(q: np.ndarray, key: np.ndarray, lam=(39, 40)) -> np.ndarray:
+    """Graph-cut labelling (oracle/ransac.c oracle_gc_label_q) of points with MSAC terms q and cell keys."""
+    q = np.ascontiguousarray(q, np.uint32)
+    key = np.ascontiguousarray(key, np.int64)
+    lab = np.zeros(max(len(q), 1), np.uint8)
+    lib().oracle_gc_label_q(q, key, len(q), int(lam[0]), int(lam[1]), lab)
+    return lab[: len(q)].astype(bool)
 
 
 def sampson_sq(F: np.ndarray, x1: np.ndarray, x2: np.ndarray, precision: int = 0) -> np.ndarray:

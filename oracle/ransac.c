@@ -608,13 +608,13 @@ static double wave_sum_order(const double* in) {
  * (shift 1e-12 trace, 8 iterations from the all-ones vector, the factor's diagonal stored as reciprocals), with the
  * cyclic Jacobi as the fallback when the factor breaks down; both are the device's operations in its order. */
 static int refit_essential(const double* x1, const double* x2, int M, const double* E_sel, double th2,
-                           const double* E_w, double* Eout) {
+                           const uint8_t* sel, const double* E_w, double* Eout) {
     static __thread double part[64][45];
     memset(part, 0, sizeof(part));
     int n = 0;
     for (int i = 0; i < M; ++i) {
         double den;
-        if (sampson_sq(E_sel, x1 + 2 * i, x2 + 2 * i, &den) > th2) continue;
+        if (sel ? !sel[i] : sampson_sq(E_sel, x1 + 2 * i, x2 + 2 * i, &den) > th2) continue;
         double dw;
         sampson_sq(E_w, x1 + 2 * i, x2 + 2 * i, &dw);
         const double w2 = dw > 1e-300 ? 1.0 / dw : 0.0;
@@ -695,6 +695,97 @@ static int refit_essential(const double* x1, const double* x2, int M, const doub
     nrm = sqrt(nrm);
     for (int k = 0; k < 9; ++k) Eout[k] /= nrm;
     return 1;
+}
+
+/* ------------------------------------------------------------------ graph-cut labelling (GC-RANSAC LO) */
+/* GC-RANSAC's local optimisation labels the points inlier / outlier by a minimum s-t cut of
+ *   E(L) = (1 - lambda) sum_i D_i(L_i) + lambda sum_{i~j} V_ij(L_i, L_j)
+ * (Barath & Matas, CVPR 2018; OpenCV USAC LOCAL_OPTIM_GC), here with the truncated quadratic of the MSAC term as
+ * the data cost: with q_i the point's MSAC term (integer, Q = 65536 for an outlier), D_i(in) = q_i, D_i(out) = Q - q_i,
+ * and the pairwise cost V(in, in) = (q_i + q_j) / 2, V(out, out) = Q - (q_i + q_j) / 2, V(in, out) = Q (submodular:
+ * V(in,in) + V(out,out) = Q <= 2Q). Neighbours are the points sharing a cell of a 4-D grid over (x1, y1, x2, y2)
+ * (cell side `cell` in normalised units), so the graph falls apart into one clique per cell and the minimum cut of
+ * each clique is found exactly without a flow: for a fixed number m of inliers in a cell of k points the energy
+ * only depends on which points through sum_S q with a positive coefficient, so the best S is the m points of lowest
+ * q (ties: lower index), and 2 * E(m) is an integer evaluated for every m from prefix sums. The smallest m reaching
+ * the minimum is taken (the minimal source set), so the labelling is unique and the kernel reproduces it bit for bit.
+ * lambda = lam_num / lam_den. Returns the number of points labelled inlier. */
+typedef struct {
+    int64_t key;
+    uint32_t q;
+    int idx;
+} gc_item;
+
+static int gc_cmp(const void* a, const void* b) {
+    const gc_item* x = (const gc_item*)a;
+    const gc_item* y = (const gc_item*)b;
+    if (x->key != y->key) return x->key < y->key ? -1 : 1;
+    if (x->q != y->q) return x->q < y->q ? -1 : 1;
+    return x->idx - y->idx;
+}
+
+static int64_t gc_cell_key(const float* p, double inv_cell) {
+    int64_t k = 0;
+    for (int d = 0; d < 4; ++d) {
+        const int64_t c = (int64_t)floor((double)p[d] * inv_cell) & 0xFFFF;
+        k = (k << 16) | c;
+    }
+    return k;
+}
+
+/* The labelling of M points given their MSAC terms q and cell keys (exported for tests). */
+int oracle_gc_label_q(const uint32_t* q, const int64_t* key, int M, int64_t lam_num, int64_t lam_den, uint8_t* lab) {
+    const int64_t Q = 65536;
+    gc_item* it = (gc_item*)malloc(sizeof(gc_item) * (size_t)(M > 0 ? M : 1));
+    for (int i = 0; i < M; ++i) {
+        it[i].q = q[i];
+        it[i].key = key[i];
+        it[i].idx = i;
+        lab[i] = 0;
+    }
+    qsort(it, (size_t)M, sizeof(gc_item), gc_cmp);
+    int n_in = 0;
+    for (int a = 0; a < M;) {
+        int b = a;
+        int64_t sum = 0;
+        while (b < M && it[b].key == it[a].key) sum += it[b++].q;
+        const int64_t k = b - a;
+        int64_t best = INT64_MAX, pre = 0;
+        int best_m = 0;
+        for (int64_t m = 0; m <= k; ++m) {  /* 2 E(m): m lowest-q points inliers, the other t outliers */
+            if (m > 0) pre += it[a + m - 1].q;
+            const int64_t t = k - m, post = sum - pre;
+            const int64_t U = 2 * pre + 2 * (t * Q - post);
+            const int64_t P = (m > 0 ? (m - 1) * pre : 0) + t * (t - 1) * Q - (t > 0 ? (t - 1) * post : 0) +
+                              2 * m * t * Q;
+            const int64_t e = (lam_den - lam_num) * U + lam_num * P;
+            if (e < best) { best = e; best_m = (int)m; }
+        }
+        for (int m = 0; m < best_m; ++m) lab[it[a + m].idx] = 1;
+        n_in += best_m;
+        a = b;
+    }
+    free(it);
+    return n_in;
+}
+
+static int gc_label(const double* Ed, const float* pts, int M, float thr2, double cell, int64_t lam_num,
+                    int64_t lam_den, uint8_t* lab) {
+    float E[9];
+    for (int k = 0; k < 9; ++k) E[k] = (float)Ed[k];
+    const float scale = 65536.0f / thr2;
+    uint32_t* q = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(M > 0 ? M : 1));
+    int64_t* key = (int64_t*)malloc(sizeof(int64_t) * (size_t)(M > 0 ? M : 1));
+    const double inv_cell = 1.0 / cell;
+    for (int i = 0; i < M; ++i) {
+        int in;
+        q[i] = msac_cost(E, pts[4 * i], pts[4 * i + 1], pts[4 * i + 2], pts[4 * i + 3], thr2, scale, &in);
+        key[i] = gc_cell_key(pts + 4 * i, inv_cell);
+    }
+    const int n = oracle_gc_label_q(q, key, M, lam_num, lam_den, lab);
+    free(q);
+    free(key);
+    return n;
 }
 
 /* ------------------------------------------------------------------ recoverPose */
@@ -781,9 +872,9 @@ static int update_num_iters(double p, double ep, int model_points, int max_iters
  * Outputs E (9), the inlier mask (M bytes), R (9), t (3). Returns the inlier count, or -1 when no model was found.
  * *n_hyp receives the number of hypotheses evaluated.
  */
-int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, double prob, int max_iters,
-                    uint64_t seed, int pair_id, int scoring, double* E_out, uint8_t* mask_out, double* R_out,
-                    double* t_out, int* n_hyp) {
+int oracle_ransac_E_gc(const double* x1n, const double* x2n, int M, double thr, double prob, int max_iters,
+                       uint64_t seed, int pair_id, int scoring, int gc_iters, double gc_cell, int gc_lam_num,
+                       int gc_lam_den, double* E_out, uint8_t* mask_out, double* R_out, double* t_out, int* n_hyp) {
     init_tables();
     if (M < 6) return -1;
     float* pts = (float*)malloc(sizeof(float) * 4 * (size_t)M);
@@ -845,17 +936,19 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
     int cur = count_inliers(bestE, pts, M, thr2, NULL);
     uint32_t cur_score = 0;
     if (scoring) cur_score = msac_score(bestE, pts, M, thr2, &cur, NULL);
-    {
+    const int gc_only = gc_iters < 0;  /* gc_iters < 0: the graph-cut LO replaces the iterative LO (USAC_ACCURATE) */
+    if (gc_only) gc_iters = -gc_iters;
+    if (!gc_only) {
         double E[9];
         memcpy(E, bestE, sizeof(E));
         for (int k = 0; k < LO_STEPS; ++k) {
             const double th = thr * (LO_MULT - (LO_MULT - 1.0) * k / (LO_STEPS - 1));
             double Esel[9], En[9];
             memcpy(Esel, E, sizeof(Esel));
-            if (!refit_essential(x1n, x2n, M, Esel, th * th, Esel, En)) break;
+            if (!refit_essential(x1n, x2n, M, Esel, th * th, NULL, Esel, En)) break;
             for (int r = 1; r < LO_IRLS; ++r) {
                 double Et[9];
-                if (!refit_essential(x1n, x2n, M, Esel, th * th, En, Et)) break;
+                if (!refit_essential(x1n, x2n, M, Esel, th * th, NULL, En, Et)) break;
                 memcpy(En, Et, sizeof(En));
             }
             int c;
@@ -875,12 +968,41 @@ int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, dou
             }
         }
     }
+    /* graph-cut LO (GC-RANSAC, MSAC only): label by the minimum cut under the best model, refit on the labelled
+     * points (Sampson-weighted 8-point, LO_IRLS rounds), keep the refit while its MSAC score drops */
+    if (gc_iters > 0 && scoring) {
+        uint8_t* lab = (uint8_t*)malloc((size_t)M);
+        for (int g = 0; g < gc_iters; ++g) {
+            if (gc_label(bestE, pts, M, thr2, gc_cell, gc_lam_num, gc_lam_den, lab) < 8) break;
+            double En[9];
+            if (!refit_essential(x1n, x2n, M, NULL, 0.0, lab, bestE, En)) break;
+            for (int r = 1; r < LO_IRLS; ++r) {
+                double Et[9];
+                if (!refit_essential(x1n, x2n, M, NULL, 0.0, lab, En, Et)) break;
+                memcpy(En, Et, sizeof(En));
+            }
+            int c;
+            const uint32_t sc = msac_score(En, pts, M, thr2, &c, NULL);
+            if (sc >= cur_score) break;
+            cur_score = sc;
+            cur = c;
+            memcpy(bestE, En, sizeof(bestE));
+        }
+        free(lab);
+    }
     uint8_t* mask = mask_out;
     cur = count_inliers(bestE, pts, M, thr2, mask);
     memcpy(E_out, bestE, sizeof(bestE));
     oracle_recover_pose(bestE, x1n, x2n, mask, M, R_out, t_out);
     free(pts);
     return cur;
+}
+
+int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, double prob, int max_iters,
+                    uint64_t seed, int pair_id, int scoring, double* E_out, uint8_t* mask_out, double* R_out,
+                    double* t_out, int* n_hyp) {
+    return oracle_ransac_E_gc(x1n, x2n, M, thr, prob, max_iters, seed, pair_id, scoring, 0, 1.0, 0, 1, E_out,
+                              mask_out, R_out, t_out, n_hyp);
 }
 
 /* Squared Sampson distances of n correspondences under F (row-major 3x3) -- reference

@@ -216,3 +216,54 @@ def test_oracle_pinned_to_round2_oracle_on_lund_c1(oracle_mod):
         assert n == prev["n_inliers"][p]
         np.testing.assert_array_equal(mask, masks[off[p]: off[p + 1]])
         close(R, t, p)
+
+
+def _gc_energy(q, key, lab, lam):
+    """2 * E(L) * den of the graph-cut LO (oracle/ransac.c gc_label) by its definition, summed over pairs."""
+    Q = 65536
+    num, den = lam
+    U = sum(2 * qi if li else 2 * (Q - qi) for qi, li in zip(q, lab))
+    P = 0
+    for i in range(len(q)):
+        for j in range(i + 1, len(q)):
+            if key[i] != key[j]:
+                continue
+            if lab[i] and lab[j]:
+                P += q[i] + q[j]
+            elif not lab[i] and not lab[j]:
+                P += 2 * Q - q[i] - q[j]
+            else:
+                P += 2 * Q
+    return (den - num) * U + num * P
+
+
+@pytest.mark.parametrize("lam", [(39, 40), (1, 2), (7, 50), (0, 1)])
+def test_gc_label_is_the_exact_min_cut(oracle_mod, lam):
+    """The per-cell closed form of the graph-cut labelling equals the exhaustive minimum of its energy over every
+    labelling of small random cells (the minimal inlier set on ties), so any exact min-cut agrees with it."""
+    import itertools
+
+    rng = np.random.default_rng(int(lam[0]) * 7 + 1)
+    for trial in range(40):
+        k = int(rng.integers(1, 9))
+        q = rng.choice([0, 1, 500, 20000, 32768, 40000, 65535, 65536], size=k).astype(np.int64)
+        q = np.where(rng.random(k) < 0.5, rng.integers(0, 65537, size=k), q)
+        key = rng.integers(0, 3, size=k)
+        got = oracle_mod.gc_label_q(q, key, lam)
+        best = min(_gc_energy(q, key, lab, lam) for lab in itertools.product([0, 1], repeat=k))
+        assert _gc_energy(q, key, got, lam) == best, (trial, q, key, got)
+        # minimal: no optimal labelling has fewer inliers in any cell
+        for c in np.unique(key):
+            cells = [lab for lab in itertools.product([0, 1], repeat=k) if _gc_energy(q, key, lab, lam) == best]
+            assert min(sum(l for l, kk in zip(lab, key) if kk == c) for lab in cells) == got[key == c].sum()
+
+
+def test_gc_lo_stage_on_known_answers(oracle_mod):
+    """The graph-cut LO stage (GC-RANSAC's local optimisation, after or instead of the iterative LO) keeps the
+    two-plane scene's known answer: every putative verified, R and t within 2 degrees."""
+    uv1, uv2, R, t = scenes.two_planes_scene(4, 4)
+    for gc_iters in (10, -10):
+        E, mask, Re, te, n, _ = oracle_mod.ransac_E_gc(uv1, uv2, 0.5, gc_iters, 0.2)
+        assert n == len(uv1)
+        assert scenes.rotation_angle_deg(Re, R) < 2.0
+        assert scenes.direction_angle_deg(te, t) < 2.0
