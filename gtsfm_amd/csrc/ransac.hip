@@ -1860,9 +1860,13 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     // Chunks of 64 hypotheses, as the oracle; launches cover 1, 1, 2, 4, 8, 8, ... chunks. Most pairs stop within the
     // first two chunks; the pairs that run on are few, so their later chunks are solved together (speculatively: a
     // chunk the score kernel does not reach is discarded) to give the solver kernels enough waves.
+    // A small batch (e.g. one rank's share of C2 at 8 GPUs: 619 pairs) leaves most of the GPU idle in those first
+    // one-chunk launches and pays each launch's latency: launches then cover 2, 4, 8, 8, ... chunks (the extra
+    // chunks are speculative, exactly as later launches' are: n_hyp and the selected model do not change).
     const int n_batches = (max_iters + kBatch - 1) / kBatch;
+    const bool small = (size_t)n_pairs * (kBatch / (kLanes / 2)) < 2048;  // solve1 workgroups of a one-chunk launch
     for (int b = 0, g = 1, launch = 0; b < n_batches; b += g, ++launch) {
-        g = launch < 2 ? 1 : std::min(kMaxGroups, 1 << (launch - 1));
+        g = small ? std::min(kMaxGroups, 2 << launch) : launch < 2 ? 1 : std::min(kMaxGroups, 1 << (launch - 1));
         g = std::min(g, n_batches - b);
         hipLaunchKernelGGL(ransac_solve1_kernel, dim3(n_pairs, g * kBatch / (kLanes / 2)), dim3(64), kSolveLds, stream,
                            d_match_count, mcap, x1n, x2n, seed, pair_id_base, d_pair_ids, st, stage, nsol);

@@ -1321,7 +1321,8 @@ struct Layout {
     int B, H, W, n_oct, max_kpts;
     int Ho[kMaxOct], Wo[kMaxOct];
     size_t g[kMaxOct][kLevels];  // byte offsets
-    size_t seen, seen_bytes, cand, ref, kps_sh, kp_shard_counts, kps, kp_counts, counters, sel, n_sel, total;
+    size_t seen, seen_bytes, seen_off[kMaxOct], cand, ref, kps_sh, kp_shard_counts, kps, kp_counts, counters, sel,
+        n_sel, total;
 };
 
 int num_octaves(int H, int W) {
@@ -1354,15 +1355,22 @@ Layout make_layout(int B, int H, int W, int max_kpts) {
         h /= 2;
         w /= 2;
     }
-    L.seen_bytes = gtsfm_align_up(((size_t)B * kLayers * (2 * H) * (2 * W) + 31) / 32 * 4, 256);
+    // every octave's seen-bitmap and candidate counters have their own region, cleared by one memset per extraction
+    // (per-octave memsets were two fill launches of ~5 us per octave)
+    L.seen_bytes = 0;
+    for (int o = 0; o < L.n_oct; ++o) {
+        L.seen_off[o] = L.seen_bytes;
+        L.seen_bytes += gtsfm_align_up(((size_t)B * kLayers * L.Ho[o] * L.Wo[o] + 31) / 32 * 4, 256);
+    }
     L.seen = take(L.seen_bytes);
     L.cand = take((size_t)B * kCandCapPerImg * sizeof(Cand));
     L.ref = take((size_t)B * kCandCapPerImg * sizeof(Refined));
     L.kps_sh = take((size_t)B * kKpCapPerImg * sizeof(KeyRec));
-    L.kp_shard_counts = take((size_t)B * kKpShards * kKpCntStride * sizeof(int));
     L.kps = take((size_t)B * kKpCapPerImg * sizeof(KeyRec));
     L.kp_counts = take((size_t)B * sizeof(int));
-    L.counters = take((size_t)(kCandShards + 16) * sizeof(int));
+    // the two counter blocks are adjacent: one memset clears both
+    L.kp_shard_counts = take((size_t)B * kKpShards * kKpCntStride * sizeof(int));
+    L.counters = take((size_t)kMaxOct * (kCandShards + 16) * sizeof(int));
     L.sel = take((size_t)B * max_kpts * sizeof(int));
     L.n_sel = take((size_t)B * sizeof(int));
     L.total = off;
@@ -1391,7 +1399,7 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
     if (workspace_bytes < L.total) return GTSFM_ERR_CAPACITY;
     unsigned char* ws = (unsigned char*)d_workspace;
     auto F = [&](size_t off) { return (float*)(ws + off); };
-    int* counters = (int*)(ws + L.counters);
+    int* counters_all = (int*)(ws + L.counters);
     int* kp_counts = (int*)(ws + L.kp_counts);
     const int B = n_img;
 
@@ -1410,8 +1418,10 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         for (int i = 1; i < kLevels; ++i)
             if (gauss_taps(sig[i], &taps[i])) return GTSFM_ERR_ARG;
     }
-    GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.kp_shard_counts, 0, (size_t)B * kKpShards * kKpCntStride * sizeof(int),
+    GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.kp_shard_counts, 0,
+                                   L.counters + (size_t)kMaxOct * (kCandShards + 16) * sizeof(int) - L.kp_shard_counts,
                                    stream));
+    GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.seen, 0, L.seen_bytes, stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(d_counts, 0, (size_t)B * sizeof(int), stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(d_xy, 0, (size_t)B * max_kpts * 2 * sizeof(float), stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(d_attr, 0, (size_t)B * max_kpts * 3 * sizeof(float), stream));
@@ -1450,20 +1460,19 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         }
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
-        GTSFM_CHECK_HIP(hipMemsetAsync(counters, 0, (kCandShards + 16) * sizeof(int), stream));
-        GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.seen, 0,
-                                       gtsfm_align_up(((size_t)B * kLayers * h * w + 31) / 32 * 4, 4), stream));
+        int* counters = counters_all + o * (kCandShards + 16);
+        uint32_t* seen = (uint32_t*)(ws + L.seen + L.seen_off[o]);
         GaussSet G;
         for (int i = 0; i < kLevels; ++i) G.g[i] = F(L.g[o][i]);
         const int shard_cap = (int)((size_t)B * kCandCapPerImg / kCandShards);
         hipLaunchKernelGGL(extrema_kernel, dim3((w + kExWaves * kExOut - 1) / (kExWaves * kExOut),
                                                 (h + kExStrip - 1) / kExStrip, B),
                            dim3(64 * kExWaves), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap,
-                           (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref), counters + kCandShards,
+                           seen, (Refined*)(ws + L.ref), counters + kCandShards,
                            B * kCandCapPerImg);
         // fused: only list overflows reach the shards, so one block per shard
         hipLaunchKernelGGL(refine_kernel, dim3(kCandShards), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
-                           shard_cap, G, h, w, B, (uint32_t*)(ws + L.seen), (Refined*)(ws + L.ref),
+                           shard_cap, G, h, w, B, seen, (Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg);
         hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps_sh),
