@@ -1063,14 +1063,15 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // entries are summed per lane (point i in lane i mod 64), then reduced across the wave by wave_sum_f64; the oracle
 // forms the same partial sums and restates the reduction order (wave_sum_order), so the sums agree bit for bit.
 __device__ bool wave_refit(const double2* x1, const double2* x2, int M, const double* Esel, double th2,
-                           const double* Ew, double* Eout, int lane, double* jac_a, double* jac_v) {
+                           const uint8_t* sel, const double* Ew, double* Eout, int lane, double* jac_a,
+                           double* jac_v) {
     double acc[45];
 #pragma unroll
     for (int k = 0; k < 45; ++k) acc[k] = 0.0;
     int n = 0;
     for (int i = lane; i < M; i += 64) {
         double den;
-        if (sampson_sq(Esel, x1[i], x2[i], &den) > th2) continue;
+        if (sel ? !sel[i] : sampson_sq(Esel, x1[i], x2[i], &den) > th2) continue;  // a label, or the threshold
         double dw;
         sampson_sq(Ew, x1[i], x2[i], &dw);
         const double w2 = dw > 1e-300 ? 1.0 / dw : 0.0;
@@ -1608,7 +1609,90 @@ __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* 
     }
 }
 
-// Per pair: status, iterative LO from the best hypothesis, final mask, recoverPose.
+// ------------------------------------------------------------------ graph-cut LO (GC-RANSAC, oracle/ransac.c gc_label)
+// The MSAC path's local optimisation: label every putative inlier / outlier by the minimum s-t cut of the truncated
+// quadratic energy with spatial coherence over a 4-D grid of (x1, y1, x2, y2), refit on the labelled points, keep the
+// refit while its MSAC score drops. Same-cell neighbours make the graph a union of cliques whose minimum cut has a
+// closed form (the oracle's header proves it): sort by (cell, MSAC term, index), then per run of one cell the m lowest
+// terms are the inliers for the m minimising the integer energy 2 E(m). Pairs above kGcMaxM keep the iterative LO.
+constexpr int kGcIters = 10;
+constexpr double kGcCellThr = 12.5;  // grid cell side in inlier thresholds (50 px at 4 px)
+constexpr long long kGcLamNum = 39, kGcLamDen = 40;
+constexpr int kGcMaxM = 32768;       // the sort key's 15-bit index
+
+__device__ __forceinline__ uint32_t gc_cell_key(float4 p, double inv_cell) {
+    const float c[4] = {p.x, p.y, p.z, p.w};
+    uint32_t k = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) k = (k << 8) | ((uint32_t)((int)floor((double)c[d] * inv_cell) + 128) & 0xFFu);
+    return k;
+}
+
+// Labels (lab[i] = 1: inlier) of the M putatives under E; returns their number (uniform). keys: 2^ceil(log2 M) u64
+// of scratch. Sort key = cell << 32 | MSAC term << 15 | index, bitonic-sorted by the wave in place.
+__device__ int wave_gc_label(const float* Ef, const float4* pts, int M, float thr2, float scale, double inv_cell,
+                             unsigned long long* keys, uint8_t* lab, int lane) {
+    int n2 = 1;
+    while (n2 < M) n2 <<= 1;
+    for (int i = lane; i < n2; i += 64) {
+        unsigned long long k = ~0ull;
+        if (i < M) {
+            bool in;
+            const uint32_t q = msac_cost(Ef, pts[i], thr2, scale, in);
+            k = ((unsigned long long)gc_cell_key(pts[i], inv_cell) << 32) | ((unsigned long long)q << 15) |
+                (unsigned long long)i;
+            lab[i] = 0;
+        }
+        keys[i] = k;
+    }
+    __syncthreads();
+    for (int kk = 2; kk <= n2; kk <<= 1)
+        for (int j = kk >> 1; j > 0; j >>= 1) {
+            for (int i = lane; i < n2; i += 64) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const unsigned long long a = keys[i], b = keys[l];
+                    if ((a > b) == ((i & kk) == 0)) {
+                        keys[i] = b;
+                        keys[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // every run head (first element of a cell) scans its run: prefix sums of the MSAC terms and 2 E(m) for all m
+    int n_in = 0;
+    const long long Q = 65536;
+    for (int i = lane; i < M; i += 64) {
+        const unsigned long long ki = keys[i];
+        if (i > 0 && (keys[i - 1] >> 32) == (ki >> 32)) continue;
+        long long sum = 0;
+        int b = i;
+        while (b < M && (keys[b] >> 32) == (ki >> 32)) sum += (long long)((keys[b++] >> 15) & 0x1FFFFu);
+        const long long k = b - i;
+        long long best = LLONG_MAX, pre = 0;
+        int best_m = 0;
+        for (long long m = 0; m <= k; ++m) {
+            if (m > 0) pre += (long long)((keys[i + m - 1] >> 15) & 0x1FFFFu);
+            const long long t = k - m, post = sum - pre;
+            const long long U = 2 * pre + 2 * (t * Q - post);
+            const long long P = (m > 0 ? (m - 1) * pre : 0) + t * (t - 1) * Q - (t > 0 ? (t - 1) * post : 0) +
+                                2 * m * t * Q;
+            const long long e = (kGcLamDen - kGcLamNum) * U + kGcLamNum * P;
+            if (e < best) {
+                best = e;
+                best_m = (int)m;
+            }
+        }
+        for (int m = 0; m < best_m; ++m) lab[keys[i + m] & 0x7FFFu] = 1;
+        n_in += best_m;
+    }
+    __syncthreads();
+    for (int m = 32; m >= 1; m >>= 1) n_in += __shfl_xor(n_in, m);
+    return n_in;
+}
+
+// Per pair: status, LO from the best hypothesis (graph-cut for MSAC, iterative for RANSAC), final mask, recoverPose.
 // two waves per SIMD (256 VGPRs, 22 spilled): 0.92 -> 0.73 ms per C2 step against one
 __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restrict__ pairs,
                                                            const double* __restrict__ intr,
@@ -1617,7 +1701,9 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
                                                            const double2* __restrict__ x2n_all,
                                                            const float4* __restrict__ pts_all, double thr_px,
                                                            int msac, RansacOutputs out,
-                                                           const PairState* __restrict__ st) {
+                                                           const PairState* __restrict__ st,
+                                                           unsigned char* __restrict__ gc_scratch,
+                                                           size_t gc_stride) {
     __shared__ double jac_a[81], jac_v[81];
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
@@ -1674,18 +1760,45 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
         cur_sc = msac_d(bestE, cur);
     else
         cur = count_d(bestE);
-    {
+    const bool gc = msac && M <= kGcMaxM;
+    if (gc) {  // graph-cut LO (oracle_ransac_E: the MSAC path)
+        unsigned long long* keys = (unsigned long long*)(gc_scratch + (size_t)p * gc_stride);
+        int n2 = 1;
+        while (n2 < M) n2 <<= 1;
+        uint8_t* lab = (uint8_t*)(keys + n2);
+        const double inv_cell = 1.0 / (kGcCellThr * thr);
+        for (int g = 0; g < kGcIters; ++g) {
+            float Ef[9];
+            for (int e = 0; e < 9; ++e) Ef[e] = (float)bestE[e];
+            if (wave_gc_label(Ef, pts, M, thr2, scale, inv_cell, keys, lab, lane) < 8) break;
+            double En[9];
+            if (!wave_refit(x1, x2, M, nullptr, 0.0, lab, bestE, En, lane, jac_a, jac_v)) break;
+            bool ok = true;
+            for (int r = 1; r < kLoIrls && ok; ++r) {
+                double Et[9];
+                ok = wave_refit(x1, x2, M, nullptr, 0.0, lab, En, Et, lane, jac_a, jac_v);
+                if (ok)
+                    for (int e = 0; e < 9; ++e) En[e] = Et[e];
+            }
+            int c;
+            const uint32_t sc = msac_d(En, c);
+            if (sc >= cur_sc) break;
+            cur_sc = sc;
+            cur = c;
+            for (int e = 0; e < 9; ++e) bestE[e] = En[e];
+        }
+    } else {
         double E[9];
         for (int e = 0; e < 9; ++e) E[e] = bestE[e];
         for (int k = 0; k < kLoSteps; ++k) {
             const double th = thr * (kLoMult - (kLoMult - 1.0) * k / (kLoSteps - 1));
             double Esel[9], En[9];
             for (int e = 0; e < 9; ++e) Esel[e] = E[e];
-            if (!wave_refit(x1, x2, M, Esel, th * th, Esel, En, lane, jac_a, jac_v)) break;
+            if (!wave_refit(x1, x2, M, Esel, th * th, nullptr, Esel, En, lane, jac_a, jac_v)) break;
             bool ok = true;
             for (int r = 1; r < kLoIrls && ok; ++r) {
                 double Et[9];
-                ok = wave_refit(x1, x2, M, Esel, th * th, En, Et, lane, jac_a, jac_v);
+                ok = wave_refit(x1, x2, M, Esel, th * th, nullptr, En, Et, lane, jac_a, jac_v);
                 if (ok)
                     for (int e = 0; e < 9; ++e) En[e] = Et[e];
             }
@@ -1877,8 +1990,11 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     }
     GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask, d_n_models};
+    // the graph-cut LO sorts in the stage buffer (free once the solver loop is done): 2^ceil(log2 M) keys + M labels
+    static_assert((size_t)kStageVals * kMaxHyp * sizeof(double) >= (size_t)kGcMaxM * 9, "GC scratch fits the stage");
     hipLaunchKernelGGL(ransac_refine_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics, d_match_count,
-                       mcap, x1n, x2n, pts, thr_px, msac ? 1 : 0, o, st);
+                       mcap, x1n, x2n, pts, thr_px, msac ? 1 : 0, o, st, (unsigned char*)stage,
+                       (size_t)kStageVals * kMaxHyp * sizeof(double));
     GTSFM_CHECK_HIP(hipGetLastError());
     return GTSFM_OK;
 }

@@ -46,6 +46,15 @@
 #define LO_STEPS 4
 #define LO_IRLS 3
 #define LO_MULT 6.0
+/* graph-cut LO (the MSAC path's LO, GC-RANSAC as USAC_ACCURATE configures it): at most GC_ITERS labelling + refit
+ * rounds, grid cells of GC_CELL_THR inlier thresholds (50 px at sift_front_end.yaml's 4 px), spatial coherence
+ * lambda = GC_LAM_NUM / GC_LAM_DEN; pairs with more than GC_MAX_M putatives keep the iterative LO (the device's sort
+ * key holds a 15-bit index) */
+#define GC_ITERS 10
+#define GC_CELL_THR 12.5
+#define GC_LAM_NUM 39
+#define GC_LAM_DEN 40
+#define GC_MAX_M 32768
 
 /* ------------------------------------------------------------------ sampling */
 static uint64_t sm_mix(uint64_t z) {
@@ -724,13 +733,15 @@ static int gc_cmp(const void* a, const void* b) {
     return x->idx - y->idx;
 }
 
+/* 4-D grid cell of a correspondence: (x1, y1, x2, y2) / cell, floored, offset by 128 and kept to 8 bits each (exact
+ * for |coordinate| < 127 cells: 6350 px at 50-px cells) */
 static int64_t gc_cell_key(const float* p, double inv_cell) {
-    int64_t k = 0;
+    uint32_t k = 0;
     for (int d = 0; d < 4; ++d) {
-        const int64_t c = (int64_t)floor((double)p[d] * inv_cell) & 0xFFFF;
-        k = (k << 16) | c;
+        const uint32_t c = (uint32_t)((int)floor((double)p[d] * inv_cell) + 128) & 0xFFu;
+        k = (k << 8) | c;
     }
-    return k;
+    return (int64_t)k;
 }
 
 /* The labelling of M points given their MSAC terms q and cell keys (exported for tests). */
@@ -998,11 +1009,14 @@ int oracle_ransac_E_gc(const double* x1n, const double* x2n, int M, double thr, 
     return cur;
 }
 
+/* The verifier as the product runs it: MSAC with the graph-cut LO (GC-RANSAC) in place of the iterative LO;
+ * inlier-count selection (RANSAC) with the iterative LO. */
 int oracle_ransac_E(const double* x1n, const double* x2n, int M, double thr, double prob, int max_iters,
                     uint64_t seed, int pair_id, int scoring, double* E_out, uint8_t* mask_out, double* R_out,
                     double* t_out, int* n_hyp) {
-    return oracle_ransac_E_gc(x1n, x2n, M, thr, prob, max_iters, seed, pair_id, scoring, 0, 1.0, 0, 1, E_out,
-                              mask_out, R_out, t_out, n_hyp);
+    const int gc = scoring && M <= GC_MAX_M;
+    return oracle_ransac_E_gc(x1n, x2n, M, thr, prob, max_iters, seed, pair_id, scoring, gc ? -GC_ITERS : 0,
+                              GC_CELL_THR * thr, GC_LAM_NUM, GC_LAM_DEN, E_out, mask_out, R_out, t_out, n_hyp);
 }
 
 /* Squared Sampson distances of n correspondences under F (row-major 3x3) -- reference
