@@ -1619,6 +1619,7 @@ constexpr int kGcIters = 10;
 constexpr double kGcCellThr = 12.5;  // grid cell side in inlier thresholds (50 px at 4 px)
 constexpr long long kGcLamNum = 39, kGcLamDen = 40;
 constexpr int kGcMaxM = 32768;       // the sort key's 15-bit index
+constexpr int kGcLdsKeys = 2048;     // pairs with up to this many putatives sort in LDS (18 KB), larger ones in HBM
 
 __device__ __forceinline__ uint32_t gc_cell_key(float4 p, double inv_cell) {
     const float c[4] = {p.x, p.y, p.z, p.w};
@@ -1630,8 +1631,8 @@ __device__ __forceinline__ uint32_t gc_cell_key(float4 p, double inv_cell) {
 
 // Labels (lab[i] = 1: inlier) of the M putatives under E; returns their number (uniform). keys: 2^ceil(log2 M) u64
 // of scratch. Sort key = cell << 32 | MSAC term << 15 | index, bitonic-sorted by the wave in place.
-__device__ int wave_gc_label(const float* Ef, const float4* pts, int M, float thr2, float scale, double inv_cell,
-                             unsigned long long* keys, uint8_t* lab, int lane) {
+__device__ __forceinline__ int wave_gc_label(const float* Ef, const float4* pts, int M, float thr2, float scale,
+                                             double inv_cell, unsigned long long* keys, uint8_t* lab, int lane) {
     int n2 = 1;
     while (n2 < M) n2 <<= 1;
     for (int i = lane; i < n2; i += 64) {
@@ -1705,6 +1706,8 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
                                                            unsigned char* __restrict__ gc_scratch,
                                                            size_t gc_stride) {
     __shared__ double jac_a[81], jac_v[81];
+    __shared__ unsigned long long gc_keys_lds[kGcLdsKeys];
+    __shared__ uint8_t gc_lab_lds[kGcLdsKeys];
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     const int M = match_count[p];
@@ -1762,15 +1765,18 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
         cur = count_d(bestE);
     const bool gc = msac && M <= kGcMaxM;
     if (gc) {  // graph-cut LO (oracle_ransac_E: the MSAC path)
-        unsigned long long* keys = (unsigned long long*)(gc_scratch + (size_t)p * gc_stride);
         int n2 = 1;
         while (n2 < M) n2 <<= 1;
-        uint8_t* lab = (uint8_t*)(keys + n2);
+        const bool in_lds = n2 <= kGcLdsKeys;
+        unsigned long long* keys = in_lds ? gc_keys_lds : (unsigned long long*)(gc_scratch + (size_t)p * gc_stride);
+        uint8_t* lab = in_lds ? gc_lab_lds : (uint8_t*)(keys + n2);
         const double inv_cell = 1.0 / (kGcCellThr * thr);
         for (int g = 0; g < kGcIters; ++g) {
             float Ef[9];
             for (int e = 0; e < 9; ++e) Ef[e] = (float)bestE[e];
-            if (wave_gc_label(Ef, pts, M, thr2, scale, inv_cell, keys, lab, lane) < 8) break;
+            const int n_lab = in_lds ? wave_gc_label(Ef, pts, M, thr2, scale, inv_cell, gc_keys_lds, gc_lab_lds, lane)
+                                     : wave_gc_label(Ef, pts, M, thr2, scale, inv_cell, keys, lab, lane);
+            if (n_lab < 8) break;
             double En[9];
             if (!wave_refit(x1, x2, M, nullptr, 0.0, lab, bestE, En, lane, jac_a, jac_v)) break;
             bool ok = true;

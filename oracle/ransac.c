@@ -23,10 +23,10 @@
  *     (truncated quadratic sum_i min(e_i, thr^2), lowest wins), with each term quantised to an integer so the
  *     sum is exact in any order: q_i = floor(e_i * 2^16 / thr^2) clamped to 65535 for an inlier, 65536 for an
  *     outlier, e_i = num^2 / den in float32. The first candidate wins ties in both modes.
- *   - local optimisation (stand-in for USAC_ACCURATE's LO + final polish; iterative LO in the style of
- *     Lebeda et al. BMVC 2012): 4 steps with the selection threshold shrinking from 6*thr to thr, each 3 rounds
- *     of Sampson-weighted (IRLS) linear 8-point on the selected points, projected onto the essential manifold;
- *     a refined model is kept when it has at least as many inliers at thr.
+ *   - local optimisation: for MSAC, GC-RANSAC's graph-cut LO (USAC_ACCURATE's LOCAL_OPTIM_GC; gc_label below);
+ *     for RANSAC, the iterative LO of Lebeda et al. (BMVC 2012): 4 steps with the selection threshold shrinking
+ *     from 6*thr to thr. Both refit with 3 rounds of Sampson-weighted (IRLS) linear 8-point on the selected points,
+ *     projected onto the essential manifold; a refined model is kept when its score improves.
  *   - recoverPose: SVD decomposition into 4 (R,t), cheirality count (depth in (0, 50) in both cameras).
  * Deterministic sampling: splitmix64 counter hash of (seed, pair id, hypothesis, draw) — the HIP kernel draws the
  * same samples.
