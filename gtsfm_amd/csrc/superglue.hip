@@ -754,84 +754,70 @@ __device__ __forceinline__ void lse_merge(float& mx, float& s, float mo, float s
 
 __device__ __forceinline__ float sk_norm(int m, int n) { return -logf((float)m + (float)n); }
 
-// One pass over Z per Sinkhorn iteration (round 5; the two-kernel pass read Z once for u and once for v): a
-// workgroup takes kSkRows rows of one pair into LDS, computes their u (row log-sum-exp of Z + v; one wave per row)
-// and then, from the same LDS rows, each column's partial log-sum-exp of Z + u over those rows: (max, sum) to `part`
-// [pair][row block][column]; sk_colmerge_kernel folds the row blocks into v. Z is read once per iteration instead of
-// twice; the partials add ld / kSkRows of its size each way.
-constexpr int kSkRows = 8;
-__global__ __launch_bounds__(256) void sk_fused_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
-                                                       int kmax, float* __restrict__ u, const float* __restrict__ v,
-                                                       float2* __restrict__ part) {
-    extern __shared__ float zr[];  // [kSkRows][ld]
-    __shared__ float ub[kSkRows];
-    const int p = blockIdx.y, rb = blockIdx.x;
+// u[i] for rows 0..m: one wave per row
+__global__ __launch_bounds__(256) void sk_rows_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                      int kmax, float* __restrict__ u, const float* __restrict__ v) {
+    const int p = blockIdx.y;
     const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
-    const int i0 = rb * kSkRows;
-    if (i0 > m) return;
-    const int nr = min(kSkRows, m + 1 - i0);
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (i > m) return;
     const long ld = kmax + 1;
-    const float* Zp = Z + (long)p * ld * ld;
+    const float* row = Z + (long)p * ld * ld + (long)i * ld;
     const float* vp = v + (long)p * ld;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int r = 0; r < nr; ++r)
-        for (int j = tid; j <= n; j += 256) zr[r * ld + j] = Zp[(long)(i0 + r) * ld + j];
-    __syncthreads();
-    const float norm = sk_norm(m, n);
-    for (int r = wave; r < nr; r += 4) {  // one wave per row: u
-        const float* row = zr + r * ld;
-        float mx = -INFINITY, s = 0.0f;
-        for (int j0 = lane; j0 <= n; j0 += 256) {
-            float x[4];
+    float mx = -INFINITY, s = 0.0f;
+    for (int j0 = lane; j0 <= n; j0 += 256) {
+        float x[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int j = j0 + 64 * k;
-                x[k] = j <= n ? row[j] + vp[j] : -INFINITY;
-            }
-            lse_push4(x, mx, s);
+        for (int k = 0; k < 4; ++k) {
+            const int j = j0 + 64 * k;
+            x[k] = j <= n ? row[j] + vp[j] : -INFINITY;
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const float mo = __shfl_xor(mx, o), so = __shfl_xor(s, o);
-            lse_merge(mx, s, mo, so);
-        }
-        if (lane == 0) {
-            const int i = i0 + r;
-            const float log_mu = i < m ? norm : logf((float)n) + norm;
-            const float ui = log_mu - (logf(s) + mx);
-            u[(long)p * ld + i] = ui;
-            ub[r] = ui;
-        }
+        lse_push4(x, mx, s);
     }
-    __syncthreads();
-    const int nrb = (int)((ld + kSkRows - 1) / kSkRows);
-    for (int j = tid; j <= n; j += 256) {  // column partials over the block's rows
-        float x[kSkRows];
 #pragma unroll
-        for (int r = 0; r < kSkRows; ++r) x[r] = r < nr ? zr[r * ld + j] + ub[r] : -INFINITY;
-        float mx = -INFINITY, s = 0.0f;
-#pragma unroll
-        for (int r = 0; r < kSkRows; r += 4) lse_push4(*(const float(*)[4])(x + r), mx, s);
-        part[((long)p * nrb + rb) * ld + j] = make_float2(mx, s);
+    for (int o = 32; o >= 1; o >>= 1) {
+        const float mo = __shfl_xor(mx, o), so = __shfl_xor(s, o);
+        lse_merge(mx, s, mo, so);
+    }
+    if (lane == 0) {
+        const float norm = sk_norm(m, n);
+        const float log_mu = i < m ? norm : logf((float)n) + norm;
+        u[(long)p * ld + i] = log_mu - (logf(s) + mx);
     }
 }
 
-// v[j] for columns 0..n from the row blocks' partial log-sum-exps
-__global__ __launch_bounds__(256) void sk_colmerge_kernel(const int* __restrict__ side_counts, int kmax,
-                                                          const float2* __restrict__ part, float* __restrict__ v) {
-    const int p = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+// v[j] for columns 0..n: 64 columns x 4 row groups per workgroup
+__global__ __launch_bounds__(256) void sk_cols_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                      int kmax, const float* __restrict__ u, float* __restrict__ v) {
+    __shared__ float pm[4][64], ps[4][64];
+    const int p = blockIdx.y;
     const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
-    if (j > n) return;
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int j = blockIdx.x * 64 + c;
+    if (blockIdx.x * 64 > n) return;
     const long ld = kmax + 1;
-    const int nrb = (int)((ld + kSkRows - 1) / kSkRows), used = m / kSkRows + 1;
+    const float* Zp = Z + (long)p * ld * ld;
+    const float* up = u + (long)p * ld;
     float mx = -INFINITY, s = 0.0f;
-    for (int rb = 0; rb < used; ++rb) {
-        const float2 q = part[((long)p * nrb + rb) * ld + j];
-        lse_merge(mx, s, q.x, q.y);
+    if (j <= n)
+        for (int i0 = g; i0 <= m; i0 += 16) {
+            float x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = i0 + 4 * k;
+                x[k] = i <= m ? Zp[(long)i * ld + j] + up[i] : -INFINITY;
+            }
+            lse_push4(x, mx, s);
+        }
+    pm[g][c] = mx;
+    ps[g][c] = s;
+    __syncthreads();
+    if (g == 0 && j <= n) {
+        for (int o = 1; o < 4; ++o) lse_merge(mx, s, pm[o][c], ps[o][c]);
+        const float norm = sk_norm(m, n);
+        const float log_nu = j < n ? norm : logf((float)m) + norm;
+        v[(long)p * ld + j] = log_nu - (logf(s) + mx);
     }
-    const float norm = sk_norm(m, n);
-    const float log_nu = j < n ? norm : logf((float)m) + norm;
-    v[(long)p * ld + j] = log_nu - (logf(s) + mx);
 }
 
 // row-wise max / argmax of the final scores ((Z + u) + v) - norm over the first n columns (first index on ties)
@@ -1176,20 +1162,15 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
     }
     hipLaunchKernelGGL(sk_init_kernel, dim3((kmax + 256) / 256, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
                        bin, u, v);
-    {
-        // partial column sums of the fused pass live in the MLP hidden buffer (free once the GNN layers are done)
-        const long ld = kmax + 1, nrb = (ld + kSkRows - 1) / kSkRows;
-        static_assert(kSkRows % 4 == 0, "partials are pushed four rows at a time");
-        if ((size_t)n_pairs * nrb * ld * sizeof(float2) > (size_t)2 * n_pairs * kmax * 512 * 4) return GTSFM_ERR_ARG;
-        float2* part = (float2*)hid;
-        const size_t zr_lds = (size_t)kSkRows * ld * sizeof(float);
-        GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)sk_fused_kernel, (int)zr_lds));
-        for (int it = 0; it < sinkhorn_iters; ++it) {
-            hipLaunchKernelGGL(sk_fused_kernel, dim3((unsigned)nrb, n_pairs), dim3(256), zr_lds, stream, Z,
-                               side_counts, kmax, u, (const float*)v, part);
-            hipLaunchKernelGGL(sk_colmerge_kernel, dim3((unsigned)((ld + 255) / 256), n_pairs), dim3(256), 0, stream,
-                               side_counts, kmax, (const float2*)part, v);
-        }
+    // Sinkhorn in two passes over Z per iteration. Measured in round 5 and not kept: one pass (a workgroup's 8 rows of
+    // Z in LDS, their row log-sum-exps, then the columns' partial log-sum-exps from LDS, merged by a second small
+    // kernel): 7.35 ms per iteration against 2.09 + 2.01 ms here (profiles/r05l_*): 65 KB of LDS per workgroup and the
+    // load / rows / columns phases in series leave it latency-bound, while these two passes stream Z at ~4 TB/s.
+    for (int it = 0; it < sinkhorn_iters; ++it) {
+        hipLaunchKernelGGL(sk_rows_kernel, dim3((kmax + 4) / 4, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
+                           u, (const float*)v);
+        hipLaunchKernelGGL(sk_cols_kernel, dim3((kmax + 64) / 64, n_pairs), dim3(256), 0, stream, Z, side_counts,
+                           kmax, (const float*)u, v);
     }
     hipLaunchKernelGGL(sk_rowmax_kernel, dim3(kmax / 4, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax, u, v,
                        max0, idx0);

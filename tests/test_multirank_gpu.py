@@ -1,0 +1,51 @@
+"""The multi-rank engine with the real HIP kernels on a one-GPU box: two ranks (both on cuda:0, process group gloo,
+the packed feature blocks gathered through the host -- RCCL refuses two ranks on one device) extract their images,
+exchange, and match / verify their pair blocks; the union of their results equals one rank's run of the whole job
+bit for bit (keypoints, putatives, verified rows, R, t). What RCCL would carry is the same packed block."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from gtsfm_amd import launch
+from tests.conftest import REPO
+
+pytestmark = pytest.mark.gpu
+RANK_SCRIPT = os.path.join(REPO, "tests", "frontend_rank.py")
+
+
+def _load(path):
+    with np.load(path) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("world,n_img", [(2, 5)])
+def test_two_ranks_on_one_gpu_equal_one_rank(tmp_path, world, n_img):
+    from gtsfm_amd import native
+    from gtsfm_amd.frontend import sharding
+
+    native.require_gpu()
+    rc = launch.spawn_ranks(world, RANK_SCRIPT, ["gpushared", str(tmp_path), str(n_img)])
+    assert rc == 0
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import frontend_rank  # noqa: E402
+
+    _, ref = frontend_rank.run_frontend_gpu(n_img, 0, 1)
+    parts = [_load(tmp_path / f"gpu_{world}_{r}.npz") for r in range(world)]
+    assert np.array_equal(np.concatenate([p["pairs"] for p in parts]), ref.pairs)
+    for key in ("status", "n_inliers", "n_matches", "isp_ok"):
+        assert np.array_equal(np.concatenate([p[key] for p in parts]), getattr(ref, key)), key
+    np.testing.assert_array_equal(np.concatenate([p["R"] for p in parts]), ref.R)
+    np.testing.assert_array_equal(np.concatenate([p["t"] for p in parts]), ref.t)
+    q = 0
+    for part in parts:
+        for p in range(len(part["pairs"])):
+            assert np.array_equal(part["v_corr"][part["offsets"][p]: part["offsets"][p + 1]], ref.verified(q)), q
+            q += 1
+    for r, part in enumerate(parts):
+        for j, i in enumerate(sharding.local_images(n_img, world, r)):
+            n = part["kp_count"][j]
+            assert n == ref.kp_count[i] and np.array_equal(part["kp_xy"][j, :n], ref.kp_xy[i, :n])
+    assert (ref.status == 0).sum() >= 3
