@@ -526,16 +526,6 @@ def main_frontend(args, info, config: str):
 
     for _ in range(args.warmup):
         res = fe.step()
-    # the device-resident step replays as one HIP graph (single-process jobs; the multi-rank step keeps eager launches
-    # around its RCCL all-gather)
-    graph = None
-    if not args.no_graph and (world == 1 or emulate):
-        try:
-            fe.capture_resident()
-            graph = True
-        except Exception as e:  # noqa: BLE001 -- reported in the JSON line, eager steps still measured
-            fe.graph, graph = None, f"capture failed: {type(e).__name__}: {e}"[:200]
-            torch.cuda.synchronize()
     tworld = 1 if emulate else world  # the emulated job has one process
     elapsed = timed_steps(fe, args.steps, False, tworld, dev)
     elapsed_res = timed_steps(fe, args.steps, True, tworld, dev)
@@ -711,7 +701,6 @@ def main_frontend(args, info, config: str):
         "mean_putatives": round(float(M_p.mean()), 1) if len(M_p) else 0.0,
         "stage_ms": st_res,
         "stage_ms_host_to_host": st_host,
-        "hip_graph": graph,
         "roofline": roof,
     }
     if emulate:
@@ -756,8 +745,6 @@ def main():
     ap.add_argument("--ba", action="store_true",
                     help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
     ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2-weak", "c4", "c3-match", "c3", "c5"])
-    ap.add_argument("--no-graph", action="store_true",
-                    help="launch the device-resident steps kernel by kernel instead of replaying one HIP graph")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="run ONE rank's share of an N-rank job on this GPU (per-rank step time; not a scaling run)")
     ap.add_argument("--emulate-rank", type=int, default=0)

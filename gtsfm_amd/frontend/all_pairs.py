@@ -302,7 +302,6 @@ class AllPairsFrontEnd:
             self.match_stream = torch.cuda.Stream(device=self.dev)
             self.match_done = [torch.cuda.Event() for _ in self.pchunks]
         self.instrument = False
-        self.graph = None  # capture_resident(): the device-resident step as one HIP graph
         self.marks: List[Tuple[str, object]] = []
         self.copy_marks: List[Tuple[str, object]] = []
 
@@ -352,27 +351,6 @@ class AllPairsFrontEnd:
         return sharding.pack_features([getattr(self.feats, n) for n, _ in fields], self.n_per,
                                       wire=[w for _, w in fields])[0]
 
-    def capture_resident(self) -> None:
-        """Captures the device-resident step (extraction, exchange, matching, verification, compaction: a few hundred
-        kernel launches, every workspace preallocated, no host synchronisation) into one HIP graph; later
-        step(resident=True) calls replay it. The step's kernels, inputs and outputs are unchanged; only the per-launch
-        host and queue overhead goes (most visible on a small rank share: C2 at 8 GPUs runs ~165 kernels in ~6 ms).
-        A multi-rank exchange over torch.distributed is not captured (single-rank or emulated exchanges only)."""
-        if not self.cuda:
-            return
-        if self.world > 1 and self.exchange is None:
-            raise RuntimeError("capture_resident: the torch.distributed all-gather is not captured")
-        side = torch.cuda.Stream(device=self.dev)
-        side.wait_stream(torch.cuda.current_stream(self.dev))
-        with torch.cuda.stream(side):
-            self.step(resident=True)  # allocations of the step's transient tensors, outside the capture
-        torch.cuda.current_stream(self.dev).wait_stream(side)
-        torch.cuda.synchronize(self.dev)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, capture_error_mode="relaxed"):
-            self.step(resident=True)
-        self.graph = g
-
     def step(self, resident: bool = False) -> Optional[HostResults]:
         """One pass of the front-end over this rank's share.
 
@@ -380,10 +358,6 @@ class AllPairsFrontEnd:
         returns HostResults. resident=True: the images already sit in HBM from an earlier step and the results stay
         there (returns None) -- the device-resident figure, reported beside the contracted one.
         """
-        if resident and self.graph is not None and not self.instrument and \
-                not torch.cuda.is_current_stream_capturing():
-            self.graph.replay()
-            return None
         cfg, k = self.cfg, self.cfg.kpts
         self.marks, self.copy_marks = [], []
         self._mark("start")

@@ -151,29 +151,3 @@ def test_engine_with_two_view_bundle_adjustment(dev):
         assert scenes.rotation_angle_deg(gpu.R[p], ref.R[p]) < 0.1
         ran += int(n > 0)
     assert ran >= 4
-
-
-@pytest.mark.parametrize("pair_chunk", [1 << 17, 8])  # one chunk; several chunks (matcher one chunk ahead on a stream)
-def test_resident_step_replayed_as_hip_graph(dev, pair_chunk):
-    """capture_resident(): the device-resident step replayed as one HIP graph leaves exactly the eager step's device
-    results (records, verified rows, offsets, support verdicts), also with the matcher's second stream."""
-    from gtsfm_amd import synthetic
-    from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig
-
-    n_img = 7
-    scene = synthetic.render_scene(24, 360, 480, device="cuda", indices=range(n_img))
-    cfg = FrontEndConfig(kpts=600, pair_chunk=pair_chunk)
-    fe = AllPairsFrontEnd(scene.images.cpu(), scene.intrinsics[:n_img], n_img, 0, 1, dev, cfg)
-    fe.step()
-    fe.step(resident=True)
-    torch.cuda.synchronize()
-    eager = [t.clone() for t in (fe.d_fixed, fe.d_ints, fe.d_offsets, fe.d_v_corr, fe.d_isp_ok)]
-    fe.capture_resident()
-    for t in (fe.d_fixed, fe.d_ints, fe.d_offsets, fe.d_v_corr, fe.d_isp_ok):
-        t.zero_()
-    for _ in range(2):
-        fe.step(resident=True)
-    torch.cuda.synchronize()
-    for a, b in zip(eager, (fe.d_fixed, fe.d_ints, fe.d_offsets, fe.d_v_corr, fe.d_isp_ok)):
-        assert torch.equal(a, b)
-    assert int((fe.d_ints[:, 0] == 0).sum()) >= 10
