@@ -406,6 +406,185 @@ __global__ __launch_bounds__(kBlurTX* blur_tyt(R, kFromU8)) void blur2d_kernel(c
     }
 }
 
+// Streaming variant of the float-input blur: one wave per (image, 64-column strip, row segment), no tile barriers.
+// Input rows arrive 8 at a time (a chunk) by global_load_lds into a per-wave LDS ring of kStreamPD + 1 chunks, issued
+// kStreamPD chunks ahead; each chunk is row-blurred in place (the row pass of blur2d_kernel) and every lane then takes
+// its own column of the 8 row-blurred values into a register window of M = 1 + ceil(2R / 8) chunks, so the vertical
+// halo is kept across chunks instead of being re-read and re-blurred per tile. From the M-th chunk on, each chunk
+// completes 8 output rows, and the column pass emits them from the window. Same fmaf chains as blur2d_kernel (row
+// pass identical; column pass acc = k0 c_y, acc = fma(kj, c_{y-j} + c_{y+j}, acc)), so the output is bit-identical.
+__host__ __device__ constexpr int blur_stream_m(int r) { return 1 + (2 * r + 7) / 8; }
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<N, I + 1>(f);
+    }
+}
+constexpr int kStreamWaves = 4, kStreamPD = 2, kStreamBufs = kStreamPD + 1;
+// Octave 0 of C2, per level (us, tiled / streaming): r 5: 1289 / 1455, r 6: 1332 / 1442, r 8: 1635 / 1507,
+// r 10: 1902 / 1467, r 13: 1996 / 1697 (profiles/r05x_*): the tiles stay at their HBM bound for narrow kernels, and
+// the streaming form wins once the row-pass halo and tile-phase serialisation dominate.
+constexpr int kBlurStreamMinR = 8;
+__host__ __device__ constexpr size_t blur_stream_lds_bytes(int r) {
+    return (size_t)kStreamWaves * kStreamBufs * 8 * blur_iwp(r) * sizeof(float);
+}
+
+template <int R>
+__global__ __launch_bounds__(64 * kStreamWaves) void blur_stream_kernel(const float* __restrict__ src,
+                                                                        float* __restrict__ dst,
+                                                                        float* __restrict__ dec, int H, int W,
+                                                                        int n_strips, int n_parts, int n_img,
+                                                                        Taps t) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    constexpr int M = blur_stream_m(R);
+    constexpr int IW = kBlurTX + 2 * R, IWP = blur_iwp(R), CH = 8 * IWP;
+    constexpr int NV = (kBlurRowOut + 2 * R) / 2;
+    static_assert(8 * (M - 1) >= 2 * R, "the window must cover the halo");
+    static_assert((kBlurRowThr - 1) * kBlurRowOut + 2 * NV <= IWP, "row-pass window past the LDS row");
+    static_assert(IW <= 2 * kBlurTX, "two load columns per row");
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // A strip's 8-row groups of every image, taken in (image, row) order, are cut into n_parts equal runs, one per wave
+    // (a run that crosses an image boundary restarts the window there). XCD-contiguous unit order, strip fastest:
+    // neighbouring strips (shared halo columns) run on one XCD at about the same rows. The unit is wave-uniform, so
+    // everything derived from it stays in scalar registers.
+    const int n_blocks = gridDim.x, per_xcd = n_blocks >> 3;
+    const int u = __builtin_amdgcn_readfirstlane((((blockIdx.x & 7) * per_xcd) + (blockIdx.x >> 3)) * kStreamWaves +
+                                                 wave);
+    if (u >= n_strips * n_parts) return;
+    const int strip = u % n_strips, part = u / n_strips;
+    const int x0 = strip * kBlurTX;
+    const int G = (H + 7) / 8, BG = n_img * G;
+    const int g_beg = (int)((long long)part * BG / n_parts), g_end = (int)((long long)(part + 1) * BG / n_parts);
+    float* ring = lds + __builtin_amdgcn_readfirstlane(wave) * (kStreamBufs * CH);
+    float k[R + 1];
+#pragma unroll
+    for (int j = 0; j <= R; ++j) k[j] = t.k[j];
+    const uint32_t oa = 4u * (uint32_t)reflect101(x0 - R + lane, W);
+    const uint32_t ob = 4u * (uint32_t)reflect101(x0 - R + kBlurTX + lane, W);
+    for (int g = g_beg; g < g_end;) {
+        const int b = g / G, gy0 = g - b * G, gy1 = min(G, gy0 + (g_end - g));
+        g += gy1 - gy0;
+        const int ys = 8 * gy0, ye = min(H, 8 * gy1);
+        // chunk c = input rows base + 8c .. + 7 (reflect-101 outside the image); chunk c >= M - 1 completes output rows
+        // ys + 8 (c - M + 1) .. + 7
+        const int base = ys + R - 8 * (M - 1);
+        const int n_chunks = (ye - ys + 7) / 8 + M - 1;
+        const float* img = src + (size_t)b * H * W;
+        // global_load_lds_dword (saddr form: scalar row base, the lane's byte offset), issued by inline asm: the compiler's
+        // own LDS-DMA tracking would wait for every chunk in flight before each chunk's LDS accesses; the waits here are
+        // explicit. 16 load instructions per chunk, always issued (chunks past the segment reload valid rows).
+        auto issue = [&](int c) {
+            const uint32_t d = __builtin_amdgcn_readfirstlane(
+                (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(ring + (c % kStreamBufs) * CH));
+            const int r0 = base + 8 * c;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const float* row = img + (size_t)reflect101(r0 + r, H) * W;
+                const uint32_t la = d + 4u * r * IWP;
+                asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(oa), "s"(row), "s"(la)
+                             : "memory", "m0");
+                if (lane < IW - kBlurTX)
+                    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(ob), "s"(row),
+                                 "s"(la + 4u * kBlurTX)
+                                 : "memory", "m0");
+            }
+        };
+        float win[8 * M];  // chunk c's column values at win[8 (c mod M) ..]
+        const int x = x0 + lane;
+        const bool dec_lane = dec != nullptr && (x & 1) == 0 && (x >> 1) < (W >> 1);
+        float* decb = dec_lane ? dec + (size_t)b * (H >> 1) * (W >> 1) + (x >> 1) : nullptr;
+        // chunk c with c mod M = K (static): wait for its rows (the kStreamPD younger chunks' loads stay in flight; stores
+        // issued in between only make the wait stricter), row-blur in place, take column `lane` into the window, then (c >=
+        // M - 1) the column pass for output rows y = ys + 8 (c - M + 1) + o: input row y + d sits (o + d - R) rows from
+        // chunk c's first row, i.e. in chunk K + floor((o + d - R) / 8) (mod M), row (o + d - R) mod 8
+        auto chunk = [&](int c, auto kc) {
+            constexpr int K = decltype(kc)::value;
+            issue(c + kStreamPD);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(16 * kStreamPD) : "memory");
+            float* in = ring + (c % kStreamBufs) * CH;
+            {
+                const int g8 = (lane % kBlurRowThr) * kBlurRowOut;
+                float* rowp = in + (lane / kBlurRowThr) * IWP;
+                typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;
+                lds_u64* wp = (lds_u64*)(rowp + g8);
+                float v[2 * NV];
+#pragma unroll
+                for (int q = 0; q < NV; ++q) {
+                    const unsigned long long w2 = wp[q];
+                    v[2 * q] = __uint_as_float((uint32_t)w2); v[2 * q + 1] = __uint_as_float((uint32_t)(w2 >> 32));
+                }
+                asm volatile("" ::: "memory");
+                pf2 o[kBlurRowOut / 2];
+#pragma unroll
+                for (int h = 0; h < kBlurRowOut / 2; ++h) o[h] = pf2{k[0], k[0]} * pf2{v[R + 2 * h], v[R + 2 * h + 1]};
+#pragma unroll
+                for (int j = 1; j <= R; ++j) {
+                    pf2 sm[kBlurRowOut / 2];
+#pragma unroll
+                    for (int h = 0; h < kBlurRowOut / 2; ++h)
+                        sm[h] = pf2{v[R + 2 * h - j], v[R + 2 * h + 1 - j]} + pf2{v[R + 2 * h + j], v[R + 2 * h + 1 + j]};
+#pragma unroll
+                    for (int h = 0; h < kBlurRowOut / 2; ++h) o[h] = __builtin_elementwise_fma(pf2{k[j], k[j]}, sm[h], o[h]);
+                }
+#pragma unroll
+                for (int h = 0; h < kBlurRowOut / 2; ++h) *(float2*)(rowp + g8 + 2 * h) = make_float2(o[h].x, o[h].y);
+            }
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int r = 0; r < 8; ++r) win[8 * K + r] = in[r * IWP + lane];
+            if (c < M - 1) return;
+            auto slot = [](int off) {  // off = o + d - R in [-2R, 7]
+                const int q = (off + 8 * M) / 8 - M;  // floor(off / 8)
+                return 8 * ((K + q + M) % M) + (off - 8 * q);
+            };
+            const int y_base = ys + 8 * (c - M + 1);
+            float* dp = dst + (size_t)b * H * W + (size_t)y_base * W + x;
+#pragma unroll
+            for (int o = 0; o < 8; o += 2) {
+                pf2 acc = pf2{k[0], k[0]} * pf2{win[slot(o - R)], win[slot(o + 1 - R)]};
+#pragma unroll
+                for (int j = 1; j <= R; ++j) {
+                    const pf2 sm = pf2{win[slot(o - R - j)], win[slot(o + 1 - R - j)]} +
+                                   pf2{win[slot(o - R + j)], win[slot(o + 1 - R + j)]};
+                    acc = __builtin_elementwise_fma(pf2{k[j], k[j]}, sm, acc);
+                }
+                const int y = y_base + o;
+                if (x < W) {
+                    if (y < ye) dp[(size_t)o * W] = acc.x;
+                    if (y + 1 < ye) dp[(size_t)(o + 1) * W] = acc.y;
+                }
+                if (decb != nullptr && y < ye && (y >> 1) < (H >> 1)) decb[(size_t)(y >> 1) * (W >> 1)] = acc.x;
+            }
+        };
+#pragma unroll
+        for (int c = 0; c < kStreamPD; ++c) issue(c);
+        // M chunks per iteration: the window slots stay static
+        for (int c = 0; c < n_chunks; c += M)
+            static_for<M>([&](auto kc) {
+                if (c + decltype(kc)::value < n_chunks) chunk(c + decltype(kc)::value, kc);
+            });
+        // the prefetched chunks land before the next run reuses the ring (and before the wave retires)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+using BlurStreamFn = void (*)(const float*, float*, float*, int, int, int, int, int, Taps);
+BlurStreamFn blur_stream_get(int r) {
+    switch (r) {
+#define GTSFM_BLURS_CASE(RR) \
+    case RR:                 \
+        return blur_stream_kernel<RR>;
+        GTSFM_BLURS_CASE(1) GTSFM_BLURS_CASE(2) GTSFM_BLURS_CASE(3) GTSFM_BLURS_CASE(4) GTSFM_BLURS_CASE(5)
+        GTSFM_BLURS_CASE(6) GTSFM_BLURS_CASE(7) GTSFM_BLURS_CASE(8) GTSFM_BLURS_CASE(9) GTSFM_BLURS_CASE(10)
+        GTSFM_BLURS_CASE(11) GTSFM_BLURS_CASE(12) GTSFM_BLURS_CASE(13) GTSFM_BLURS_CASE(14) GTSFM_BLURS_CASE(15)
+        GTSFM_BLURS_CASE(16)
+#undef GTSFM_BLURS_CASE
+        default:
+            return nullptr;
+    }
+}
+
 template <bool kFromU8>
 struct BlurTable {
     using Fn = void (*)(const float*, const uint8_t*, int, int, int, float*, float*, int, int, int, int, int, Taps);
@@ -539,7 +718,7 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 // levels' 24. Measured in round 5 and not kept: windows of 64 outputs aligned to 128-B lines, the halo columns
 // loaded separately (lanes 0 / 63 take them through the DPP's old operand): bit-exact, but 366 vs 367 us per launch
 // with the same FETCH_SIZE (the straddled lines are L2 hits) and 103 instead of 79 VGPRs (profiles/r05d_*).
-constexpr int kExWaves = 4, kExOut = 62, kExStrip = 64;
+constexpr int kExWaves = 4, kExOut = 62, kExStrip = 72;
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
@@ -689,32 +868,33 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     }
     float g1[kInLv], g2[kInLv], g3[kInLv], g4[kInLv], g5[kInLv], g6[kInLv];
     fetch(y0 + 1, g1);
+    __builtin_amdgcn_sched_barrier(0);
     fetch(y0 + 2, g2);
+    __builtin_amdgcn_sched_barrier(0);
     fetch(y0 + 3, g3);
+    __builtin_amdgcn_sched_barrier(0);
     fetch(y0 + 4, g4);
+    __builtin_amdgcn_sched_barrier(0);
     fetch(y0 + 5, g5);
+    __builtin_amdgcn_sched_barrier(0);
     fetch(y0 + 6, g6);
+    __builtin_amdgcn_sched_barrier(0);
     for (int y = y0; y < y_end; y += 6) {
         finish(g1, S2{});
         fetch(min(y + 7, y_end), g1);
         test_row(y, S1{});
-        if (y + 1 >= y_end) break;
         finish(g2, S0{});
         fetch(min(y + 8, y_end), g2);
         test_row(y + 1, S2{});
-        if (y + 2 >= y_end) break;
         finish(g3, S1{});
         fetch(min(y + 9, y_end), g3);
         test_row(y + 2, S0{});
-        if (y + 3 >= y_end) break;
         finish(g4, S2{});
         fetch(min(y + 10, y_end), g4);
         test_row(y + 3, S1{});
-        if (y + 4 >= y_end) break;
         finish(g5, S0{});
         fetch(min(y + 11, y_end), g5);
         test_row(y + 4, S2{});
-        if (y + 5 >= y_end) break;
         finish(g6, S1{});
         fetch(min(y + 12, y_end), g6);
         test_row(y + 5, S0{});
@@ -1429,6 +1609,15 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
 
     for (int i = 0; i < kLevels; ++i)
         if (taps[i].r < 1 || taps[i].r > kBlurMaxR) return GTSFM_ERR_ARG;
+
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            return GTSFM_ERR_HIP;
+        n_cu = v;
+    }
     auto blur = [&](const float* src, float* dst, float* dec, int h, int w, const Taps& t) -> int {
         const bool u8 = src == nullptr;
         const int ty = blur_ty(t.r, u8), tyt = blur_tyt(t.r, u8);
@@ -1444,7 +1633,19 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         if (u8)
             hipLaunchKernelGGL(BlurTable<true>::get(t.r), grid, dim3(kBlurTX, tyt), lds, stream, nullptr,
                                d_images, channels, H, W, dst, dec, h, w, n_tx, n_ty, B, t);
-        else
+        else if (t.r >= kBlurStreamMinR) {  // wide kernels: the streaming variant (narrow ones are HBM-bound as tiles)
+            const BlurStreamFn sf = blur_stream_get(t.r);
+            const int n_strips = (w + kBlurTX - 1) / kBlurTX;
+            const size_t lds_s = blur_stream_lds_bytes(t.r);
+            // runs of about h / n_seg rows per (image, strip), all launched at once: at least 3 per image column and
+            // 64 waves per CU in all (measured on octave 0: 1 / 3 / 8 runs per column 1.73 / 1.70 / 1.77 ms at r = 13;
+            // small octaves need the extra runs), each at least 32 rows long
+            const int n_seg = max(1, min(max(3, (64 * n_cu + B * n_strips - 1) / (B * n_strips)), (h + 31) / 32));
+            const int n_parts = B * n_seg;
+            const int n_blk = ((n_strips * n_parts + kStreamWaves - 1) / kStreamWaves + 7) / 8 * 8;
+            hipLaunchKernelGGL(sf, dim3(n_blk), dim3(64 * kStreamWaves), lds_s, stream, src, dst, dec, h, w, n_strips,
+                               n_parts, B, t);
+        } else
             hipLaunchKernelGGL(BlurTable<false>::get(t.r), grid, dim3(kBlurTX, tyt), lds, stream, src, nullptr, 0,
                                0, 0, dst, dec, h, w, n_tx, n_ty, B, t);
         return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
