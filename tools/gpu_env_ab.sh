@@ -13,5 +13,5 @@ for spec in "$@"; do
   rc=$?; echo "== $v ($assign) rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/eab_$TAG/$v.err; exit $rc; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['stage_ms'])" gpurun_out/eab_$TAG/$v.json
   f=$(find gpurun_out/eab_$TAG/p_$v -name "*kernel_stats.csv" | head -1); python tools/kstats.py $f | grep -E "$KRE" > gpurun_out/eab_$TAG/$v.k; cat gpurun_out/eab_$TAG/$v.k
-  cp $(find gpurun_out/eab_$TAG/p_$v -name "*kernel_trace.csv" | head -1) gpurun_out/eab_$TAG/$v.trace.csv; rm -rf gpurun_out/eab_$TAG/p_$v
+  rm -rf gpurun_out/eab_$TAG/p_$v
 done
