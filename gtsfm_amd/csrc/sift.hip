@@ -26,6 +26,7 @@ constexpr int kLayers = 3;
 constexpr int kLevels = kLayers + 3;
 constexpr int kDogs = kLayers + 2;
 constexpr int kMaxOct = 16;
+constexpr int kMaxDevices = 16;
 constexpr int kMaxR = 31;
 constexpr float kSigma = 1.6f;
 constexpr float kInitSigma = 0.5f;
@@ -473,7 +474,9 @@ __global__ __launch_bounds__(64 * kStreamWaves) void blur_stream_kernel(const fl
         const float* img = src + (size_t)b * H * W;
         // global_load_lds_dword (saddr form: scalar row base, the lane's byte offset), issued by inline asm: the compiler's
         // own LDS-DMA tracking would wait for every chunk in flight before each chunk's LDS accesses; the waits here are
-        // explicit. 16 load instructions per chunk, always issued (chunks past the segment reload valid rows).
+        // explicit. 16 load instructions per chunk, always issued (chunks past the segment reload valid rows). The asm
+        // sets M0 itself; the compiler keeps nothing else in M0 in this kernel (every m0 in its ISA is one of these
+        // statements), which is what the clobber warning asks to check.
         auto issue = [&](int c) {
             const uint32_t d = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(ring + (c % kStreamBufs) * CH));
@@ -1650,6 +1653,26 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
                                0, 0, dst, dec, h, w, n_tx, n_ty, B, t);
         return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
     };
+    // Detection (extrema + refinement, orientation) of octave o reads only octave o's levels, so it runs on a side
+    // stream while the main stream goes on with octave o + 1's blurs: the latency-bound refinement and orientation
+    // overlap the bandwidth-bound blurs. Octaves stay in order on the side stream (they share the candidate and
+    // refinement buffers); the main stream joins it before the keypoints are gathered.
+    hipStream_t side = nullptr;
+    hipEvent_t* ev = nullptr;
+    {
+        static hipStream_t sides[kMaxDevices] = {};
+        static hipEvent_t evs[kMaxDevices][kMaxOct + 1] = {};
+        int dev = 0;
+        GTSFM_CHECK_HIP(hipGetDevice(&dev));
+        if (dev < 0 || dev >= kMaxDevices) return GTSFM_ERR_ARG;
+        if (!sides[dev]) {
+            GTSFM_CHECK_HIP(hipStreamCreateWithFlags(&sides[dev], hipStreamNonBlocking));
+            for (int i = 0; i <= kMaxOct; ++i)
+                GTSFM_CHECK_HIP(hipEventCreateWithFlags(&evs[dev][i], hipEventDisableTiming));
+        }
+        side = sides[dev];
+        ev = evs[dev];
+    }
     for (int o = 0; o < L.n_oct; ++o) {
         const int h = L.Ho[o], w = L.Wo[o];
         // octave o > 0 starts from the layer-3 level of octave o - 1, decimated by that level's blur launch
@@ -1661,6 +1684,8 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         }
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;
+        GTSFM_CHECK_HIP(hipEventRecord(ev[o], stream));
+        GTSFM_CHECK_HIP(hipStreamWaitEvent(side, ev[o], 0));
         int* counters = counters_all + o * (kCandShards + 16);
         uint32_t* seen = (uint32_t*)(ws + L.seen + L.seen_off[o]);
         GaussSet G;
@@ -1668,18 +1693,20 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
         const int shard_cap = (int)((size_t)B * kCandCapPerImg / kCandShards);
         hipLaunchKernelGGL(extrema_kernel, dim3((w + kExWaves * kExOut - 1) / (kExWaves * kExOut),
                                                 (h + kExStrip - 1) / kExStrip, B),
-                           dim3(64 * kExWaves), 0, stream, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap,
+                           dim3(64 * kExWaves), 0, side, G, h, w, (Cand*)(ws + L.cand), counters, shard_cap,
                            seen, (Refined*)(ws + L.ref), counters + kCandShards,
                            B * kCandCapPerImg);
         // fused: only list overflows reach the shards, so one block per shard
-        hipLaunchKernelGGL(refine_kernel, dim3(kCandShards), dim3(256), 0, stream, (const Cand*)(ws + L.cand), counters,
+        hipLaunchKernelGGL(refine_kernel, dim3(kCandShards), dim3(256), 0, side, (const Cand*)(ws + L.cand), counters,
                            shard_cap, G, h, w, B, seen, (Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg);
-        hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, stream, (const Refined*)(ws + L.ref),
+        hipLaunchKernelGGL(orientation_kernel, dim3(8192), dim3(64), 0, side, (const Refined*)(ws + L.ref),
                            counters + kCandShards, B * kCandCapPerImg, G, h, w, o, (KeyRec*)(ws + L.kps_sh),
                            (int*)(ws + L.kp_shard_counts), kKpCapPerImg);
         GTSFM_CHECK_HIP(hipGetLastError());
     }
+    GTSFM_CHECK_HIP(hipEventRecord(ev[kMaxOct], side));
+    GTSFM_CHECK_HIP(hipStreamWaitEvent(stream, ev[kMaxOct], 0));
     static_assert(kKpCapPerImg % kKpShards == 0, "shards split the per-image capacity evenly");
     hipLaunchKernelGGL(kp_gather_kernel, dim3(B), dim3(256), 0, stream, (const KeyRec*)(ws + L.kps_sh),
                        (const int*)(ws + L.kp_shard_counts), kKpCapPerImg, (KeyRec*)(ws + L.kps), kp_counts);
