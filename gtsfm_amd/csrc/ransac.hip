@@ -824,7 +824,24 @@ __device__ __forceinline__ void score2(const float (&E)[9], f2 x1, f2 y1, f2 x2,
     const bool in0 = nn.x <= rhs.x, in1 = nn.y <= rhs.y;
     cnt += (in0 ? 1 : 0) + (in1 ? 1 : 0);
     if constexpr (kMsac) {
-        const f2 r = {den.x > 0.0f ? __fdiv_rn(nn.x, den.x) : 0.0f, den.y > 0.0f ? __fdiv_rn(nn.y, den.y) : 0.0f};
+        f2 r;
+        if (__all(fminf(den.x, den.y) >= 0x1p-60f)) {
+            // nn / den correctly rounded: the compiler's division sequence (reciprocal, one Newton step on it, two
+            // residual corrections) without its operand scaling and special-case fixup, which only act when an
+            // operand or an intermediate leaves the normal range. Here den is in [2^-60, 16] and nn in [0, 16], so
+            // for every quotient >= 2^-100 the result is the IEEE quotient bit for bit; a smaller one (nn near
+            // underflow) may differ in its last bits, but both quantise to the same cost 0 (q scale < 2^-44).
+            const f2 rc = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+            const f2 e = pfma(-den, rc, (f2)1.0f);
+            const f2 rr = pfma(e, rc, rc);
+            f2 q = nn * rr;
+            const f2 e2 = pfma(-den, q, nn);
+            q = pfma(e2, rr, q);
+            const f2 e3 = pfma(-den, q, nn);
+            r = pfma(e3, rr, q);
+        } else {
+            r = {den.x > 0.0f ? __fdiv_rn(nn.x, den.x) : 0.0f, den.y > 0.0f ? __fdiv_rn(nn.y, den.y) : 0.0f};
+        }
         const f2 qq = r * (f2)scale;
         const uint32_t c0 = qq.x < 65535.0f ? (uint32_t)qq.x : 65535u;
         const uint32_t c1 = qq.y < 65535.0f ? (uint32_t)qq.y : 65535u;
