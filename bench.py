@@ -27,7 +27,7 @@ Workloads:
       images, then all pairs through the same matcher.
   --config c5: a per-GPU slice of configs[4] -- SuperPoint (2048 kpts) + SuperGlue + 5-point RANSAC over all pairs
       of 32 rendered images (configs[4]'s 2000 images x 8 GPUs is ~2M SuperGlue pairs; --images sets the slice).
-Pairs are cut into one contiguous block per rank, images dealt round-robin for extraction.
+Pairs and images are dealt round-robin over the ranks (pair p to rank p mod N, image i to rank i mod N).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2-weak|c4|c3-match|c3|c5] [--images n]
                     [--no-cpu-baseline]
@@ -716,7 +716,7 @@ def main_frontend(args, info, config: str):
             "pair_limit": args.pair_limit or None,
             "note": "rank `rank` of a `world`-rank job run alone on one GPU: its images extracted, the exchange's "
                     "packing + the gathered buffer's write (the other ranks' blocks extracted untimed beforehand; "
-                    "the xGMI transfer of the all-gather is NOT included), its contiguous pair block matched, "
+                    "the xGMI transfer of the all-gather is NOT included), its pair share (every N-th pair) matched, "
                     "verified and compacted"}
     if want_baseline:
         if deep:
@@ -749,7 +749,7 @@ def main():
                     help="run ONE rank's share of an N-rank job on this GPU (per-rank step time; not a scaling run)")
     ap.add_argument("--emulate-rank", type=int, default=0)
     ap.add_argument("--pair-limit", type=int, default=0,
-                    help="with --emulate-world: only the first K pairs of the rank's block (a bounded partial run)")
+                    help="with --emulate-world: only the first K pairs of the rank's share (a bounded partial run)")
     ap.add_argument("--launch-probe", action="store_true",
                     help="each rank joins a gloo group, prints what it sees and exits (tests the launch path on CPU)")
     args = ap.parse_args()

@@ -86,8 +86,8 @@ class HipKernels:
         return self._dev.match_pairs(f.desc, f.count, pairs, ratio, self._native.GTSFM_MATCH_INT_F16, groups=groups,
                                      out=out)
 
-    def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_id_base):
-        return self._dev.ransac_essential(xy, intr, pairs, idx, cnt, thresh_px, pair_id_base=pair_id_base)
+    def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_ids):
+        return self._dev.ransac_essential(xy, intr, pairs, idx, cnt, thresh_px, pair_ids=pair_ids)
 
     def bundle_adjust(self, xy, intr, pairs, idx, cnt, res, min_inliers, max_iters, reproj_thresh, tri_thresh):
         return self._dev.bundle_adjust_2view(xy, intr, pairs, idx, cnt, res, min_inliers, max_iters, reproj_thresh,
@@ -191,7 +191,7 @@ class HostResults:
 
 
 class AllPairsFrontEnd:
-    """One rank's share of the all-pairs front-end (images i with i % world == rank, one contiguous pair block)."""
+    """One rank's share of the all-pairs front-end (images i with i % world == rank, pairs p with p % world == rank)."""
 
     def __init__(self, host_images: torch.Tensor, intrinsics: np.ndarray, n_img: int, rank: int, world: int,
                  device: torch.device, cfg: Optional[FrontEndConfig] = None, kernels=None,
@@ -200,7 +200,7 @@ class AllPairsFrontEnd:
         (gtsfm_amd.retriever; image_pairs_generator.py:29-47); None = every pair (ExhaustiveRetriever).
         exchange: None (the collective over torch.distributed), or a sharding.EmulatedAllGather when one process runs
         rank `rank`'s share of a `world`-rank job (bench.py --emulate-world).
-        pair_limit: keep only the first pair_limit pairs of this rank's block (a bounded partial run of a job whose
+        pair_limit: keep only the first pair_limit pairs of this rank's share (a bounded partial run of a job whose
         full block would take minutes per step; bench.py --pair-limit)."""
         self.cfg = cfg or FrontEndConfig()
         self.exchange = exchange
@@ -251,7 +251,8 @@ class AllPairsFrontEnd:
         block = sharding.rank_pairs(pairs, world, rank)
         if pair_limit is not None:
             block = block[: max(0, int(pair_limit))]
-        self.pair_id_base = int(block[0]) if len(block) else 0  # global pair index keys the RANSAC sampler
+        # the global pair index keys the RANSAC sampler (a pair's result does not depend on the world size)
+        self.pair_ids = torch.from_numpy(block.astype(np.int32)).to(self.dev)
         self.my_pairs = pairs[block]
         P = len(block)
         self.P = P
@@ -408,7 +409,7 @@ class AllPairsFrontEnd:
                 issue_match(c)
                 idx, mcnt = matched.pop(c)
             self._mark("match")
-            res = self.kern.verify(xy_all, self.intr, pairs, idx, mcnt, cfg.thresh_px, self.pair_id_base + a)
+            res = self.kern.verify(xy_all, self.intr, pairs, idx, mcnt, cfg.thresh_px, self.pair_ids[a:b])
             self._mark("verify")
             out, ratio_inl = res, None
             if cfg.bundle_adjust:

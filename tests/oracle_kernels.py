@@ -56,7 +56,7 @@ class OracleKernels:
             cnt[p] = len(m)
         return idx, cnt
 
-    def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_id_base):
+    def verify(self, xy, intr, pairs, idx, cnt, thresh_px, pair_ids):
         P, mcap = idx.shape[0], idx.shape[1]
         res = OracleRansacResult(P, mcap)
         for p in range(P):
@@ -70,7 +70,7 @@ class OracleKernels:
             f2, u2, v2 = intr[i2].tolist()
             x1 = (xy[i1, m[:, 0]].numpy().astype(np.float64) - [u1, v1]) / f1
             x2 = (xy[i2, m[:, 1]].numpy().astype(np.float64) - [u2, v2]) / f2
-            r = oracle.ransac_E(x1, x2, thresh_px / max(f1, f2), pair_id=pair_id_base + p)
+            r = oracle.ransac_E(x1, x2, thresh_px / max(f1, f2), pair_id=int(pair_ids[p]))
             if r is None:
                 res.status[p] = 2
                 continue

@@ -81,7 +81,7 @@ def test_c4_one_gpu_all_pairs_consistent_and_sampled_vs_oracle(oracle_mod):
             f1, f2 = K[i1], K[i2]
             x1 = (xy[i1, m[:, 0]].astype(np.float64) - f1[1:3]) / f1[0]
             x2 = (xy[i2, m[:, 1]].astype(np.float64) - f2[1:3]) / f2[0]
-            out["ref"] = oracle_mod.ransac_E(x1, x2, cfg.thresh_px / max(f1[0], f2[0]), pair_id=fe.pair_id_base + p)
+            out["ref"] = oracle_mod.ransac_E(x1, x2, cfg.thresh_px / max(f1[0], f2[0]), pair_id=int(fe.pair_ids[p]))
             out["m"] = m
         return out
 

@@ -65,18 +65,21 @@ def test_frontend_gloo_sharded_equals_single_rank(tmp_path, world, n_img):
     torch.set_num_threads(1)
     _, ref = frontend_rank.run_frontend(n_img, launch.RankInfo(0, 1, 0, torch.device("cpu")))
     parts = [_load(tmp_path / f"results_{world}_{r}.npz") for r in range(world)]
-    got_pairs = np.concatenate([p["pairs"] for p in parts])
+    # rank r holds the pairs sharding.rank_pairs(.., r) (round-robin): back to pair order
+    owner = np.concatenate([sharding.rank_pairs(ref.pairs, world, r) for r in range(world)])
+    order = np.argsort(owner)
+    got_pairs = np.concatenate([p["pairs"] for p in parts])[order]
     assert np.array_equal(got_pairs, ref.pairs) and len(ref.pairs) == n_img * (n_img - 1) // 2
     for key in ("status", "n_inliers", "n_matches", "isp_ok"):
-        assert np.array_equal(np.concatenate([p[key] for p in parts]), getattr(ref, key)), key
-    np.testing.assert_array_equal(np.concatenate([p["R"] for p in parts]), ref.R)
-    np.testing.assert_array_equal(np.concatenate([p["t"] for p in parts]), ref.t)
-    q = 0
+        assert np.array_equal(np.concatenate([p[key] for p in parts])[order], getattr(ref, key)), key
+    np.testing.assert_array_equal(np.concatenate([p["R"] for p in parts])[order], ref.R)
+    np.testing.assert_array_equal(np.concatenate([p["t"] for p in parts])[order], ref.t)
+    k = 0
     for part in parts:
         for p in range(len(part["pairs"])):
             rows = part["v_corr"][part["offsets"][p]: part["offsets"][p + 1]]
-            assert np.array_equal(rows, ref.verified(q)), q
-            q += 1
+            assert np.array_equal(rows, ref.verified(int(owner[k]))), int(owner[k])
+            k += 1
     # keypoints: each rank holds its own images, identical to the single-rank extraction of the same image
     for r, part in enumerate(parts):
         for j, i in enumerate(sharding.local_images(n_img, world, r)):

@@ -1,6 +1,6 @@
 """The multi-rank engine with the real HIP kernels on a one-GPU box: two ranks (both on cuda:0, process group gloo,
 the packed feature blocks gathered through the host -- RCCL refuses two ranks on one device) extract their images,
-exchange, and match / verify their pair blocks; the union of their results equals one rank's run of the whole job
+exchange, and match / verify their pair shares; the union of their results equals one rank's run of the whole job
 bit for bit (keypoints, putatives, verified rows, R, t). What RCCL would carry is the same packed block."""
 import os
 import sys
@@ -34,16 +34,20 @@ def test_two_ranks_on_one_gpu_equal_one_rank(tmp_path, world, n_img):
 
     _, ref = frontend_rank.run_frontend_gpu(n_img, 0, 1)
     parts = [_load(tmp_path / f"gpu_{world}_{r}.npz") for r in range(world)]
-    assert np.array_equal(np.concatenate([p["pairs"] for p in parts]), ref.pairs)
+    # rank r holds the pairs sharding.rank_pairs(.., r) (round-robin): back to pair order
+    owner = np.concatenate([sharding.rank_pairs(ref.pairs, world, r) for r in range(world)])
+    order = np.argsort(owner)
+    assert np.array_equal(np.concatenate([p["pairs"] for p in parts])[order], ref.pairs)
     for key in ("status", "n_inliers", "n_matches", "isp_ok"):
-        assert np.array_equal(np.concatenate([p[key] for p in parts]), getattr(ref, key)), key
-    np.testing.assert_array_equal(np.concatenate([p["R"] for p in parts]), ref.R)
-    np.testing.assert_array_equal(np.concatenate([p["t"] for p in parts]), ref.t)
-    q = 0
+        assert np.array_equal(np.concatenate([p[key] for p in parts])[order], getattr(ref, key)), key
+    np.testing.assert_array_equal(np.concatenate([p["R"] for p in parts])[order], ref.R)
+    np.testing.assert_array_equal(np.concatenate([p["t"] for p in parts])[order], ref.t)
+    k = 0
     for part in parts:
         for p in range(len(part["pairs"])):
+            q = int(owner[k])
             assert np.array_equal(part["v_corr"][part["offsets"][p]: part["offsets"][p + 1]], ref.verified(q)), q
-            q += 1
+            k += 1
     for r, part in enumerate(parts):
         for j, i in enumerate(sharding.local_images(n_img, world, r)):
             n = part["kp_count"][j]

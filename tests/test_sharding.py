@@ -74,7 +74,9 @@ def test_pair_blocks_partition_all_pairs():
         pairs = sharding.all_pairs(n_img)
         for world in (1, 2, 3, 8):
             owned = np.concatenate([sharding.rank_pairs(pairs, world, r) for r in range(world)])
-            assert np.array_equal(owned, np.arange(len(pairs)))
+            assert np.array_equal(np.sort(owned), np.arange(len(pairs)))  # a partition
+            sizes = [len(sharding.rank_pairs(pairs, world, r)) for r in range(world)]
+            assert max(sizes) - min(sizes) <= 1  # round-robin: shares differ by at most one pair
 
 
 def test_global_slots_are_rank_major():
