@@ -109,15 +109,18 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 // The solver's dynamically indexed arrays live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit
 // consecutive words, so every access is bank-conflict free, and nothing spills to scratch. The solver runs in two
 // kernels so each one's workgroup holds only its own phase's arrays:
-//   stage 1 (sample, 5x9 null space in registers, 10x20 Gauss-Jordan), two lanes per hypothesis: rows 2..9 of this
-//       lane's half of A (8 x 10; rows 0, 1 in registers) = 40 KB per 64-lane workgroup (four per CU);
+//   stage 1 (sample, 5x9 null space in registers, 10x20 Gauss-Jordan), two lanes per hypothesis: rows 6..9 of this
+//       lane's half of A (4 x 10; rows 0..5 in registers) = 20 KB per 64-lane workgroup;
 //   stage 2 (det B(z), Sturm chain, isolation, bisection, E): the chain is built in registers (generic degrees;
 //       a private-memory fallback for degree drops), the isolating intervals are selected into registers, and LDS
 //       holds only the isolation stack as left ends (24 doubles + 24 count bytes) = 13.5 KB per workgroup, so
 //       with <= 256 registers two waves share a SIMD.
 constexpr int kLanes = 64;
-constexpr int kRegRows = 2;   // rows of the lane's half of A kept in registers (the rest in LDS)
-constexpr int kUnion = 10 * (10 - kRegRows);  // stage-1 doubles per lane: A rows 2..9 of the lane's half
+// rows of the lane's half of A kept in registers (the rest in LDS): C2 solve1 per launch 364 / 330 / 330 / 323 us for
+// 2 / 4 / 5 / 6 (profiles/r05an_*): each Gauss-Jordan step moves every LDS row through registers, and the register
+// file has room (1 wave per SIMD either way: 314 VGPRs at 2, 406 at 6)
+constexpr int kRegRows = 6;
+constexpr int kUnion = 10 * (10 - kRegRows);  // stage-1 doubles per lane: the LDS rows of the lane's half of A
 constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
 constexpr int kRootDbl = kStack;  // stage-2 doubles per lane: the isolation stack's left ends
 constexpr int kRootB = kStack;    // stage-2 bytes per lane: the stack's Sturm sign-variation counts
@@ -517,8 +520,8 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         E[e][2] = N[2][e];
         E[e][3] = N[3][e];
     }
-    // This lane's half of A: rows 0..kRegRows-1 in registers (G), rows kRegRows..9 in LDS (A), so the workgroup's LDS
-    // is 40 KB (four workgroups per CU instead of three). Each row is accumulated in registers, then stored once.
+    // This lane's half of A: rows 0..kRegRows-1 in registers (G), rows kRegRows..9 in LDS (A). Each row is
+    // accumulated in registers, then stored once.
     LaneArr<double> A = m.u.at(-10 * kRegRows);  // A[10 * r + j] for r >= kRegRows
     double G[kRegRows][10];
     auto store_row = [&](int r, const double(&row)[20]) {
@@ -652,7 +655,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int j = 0; j < 10; ++j) Rt[r][j] = A[10 * (4 + r) + j];
+        for (int j = 0; j < 10; ++j) Rt[r][j] = ld(4 + r, j);
     RPROF(3);
     return true;
 }

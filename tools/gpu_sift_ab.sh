@@ -10,7 +10,7 @@ for v in "$@"; do
   (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/sab_$TAG/p_$v -o run -- python -u $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/sab_$TAG/$v.json 2> $R/gpurun_out/sab_$TAG/$v.err)
   rc=$?; echo "== $v rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/sab_$TAG/$v.err; exit $rc; }
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print(d['value'], d['stage_ms'])" gpurun_out/sab_$TAG/$v.json
-  f=$(find gpurun_out/sab_$TAG/p_$v -name "*kernel_stats.csv" | head -1); python tools/kstats.py $f | grep -E "blur|extrema|orient|descr|topk|refine_k" > gpurun_out/sab_$TAG/$v.k; cat gpurun_out/sab_$TAG/$v.k; rm -rf gpurun_out/sab_$TAG/p_$v
+  f=$(find gpurun_out/sab_$TAG/p_$v -name "*kernel_stats.csv" | head -1); python tools/kstats.py $f | grep -E "${KRE:-blur|extrema|orient|descr|topk|refine_k}" > gpurun_out/sab_$TAG/$v.k; cat gpurun_out/sab_$TAG/$v.k; rm -rf gpurun_out/sab_$TAG/p_$v
 done
 for v in $FETCH_VARS; do
   export GTSFM_HIP_LIB=$R/${ABDIR:-abvar}/libgtsfm_hip_$v.so
