@@ -626,12 +626,16 @@ __device__ __forceinline__ bool refine_one(const Cand cd, const GaussSet& G, int
     float xi = 0, xr = 0, xc = 0;
     int i = 0;
     bool ok = true;
+    // the last iteration's derivatives: the loop only leaves with ok on a converged step, which does not move
+    // (layer, r, c), so the final contrast and edge tests reuse them instead of gathering the same values again
+    float l_dD0 = 0, l_dD1 = 0, l_dD2 = 0, l_ctr = 0, l_dxx = 0, l_dyy = 0, l_dxy = 0;
     for (; i < kMaxInterp; i++) {
         const int img = layer, prev = layer - 1, next = layer + 1;
         const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
         const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
         const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
-        const float v2 = DAT(img, r, c) * 2;
+        const float ctr = DAT(img, r, c);
+        const float v2 = ctr * 2;
         const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
         const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
         const float dss = (DAT(next, r, c) + DAT(prev, r, c) - v2) * second_deriv_scale;
@@ -641,6 +645,7 @@ __device__ __forceinline__ bool refine_one(const Cand cd, const GaussSet& G, int
                            DAT(prev, r, c - 1)) * cross_deriv_scale;
         const float dys = (DAT(next, r + 1, c) - DAT(next, r - 1, c) - DAT(prev, r + 1, c) +
                            DAT(prev, r - 1, c)) * cross_deriv_scale;
+        l_dD0 = dD0; l_dD1 = dD1; l_dD2 = dD2; l_ctr = ctr; l_dxx = dxx; l_dyy = dyy; l_dxy = dxy;
         const float a00 = dxx, a01 = dxy, a02 = dxs, a10 = dxy, a11 = dyy, a12 = dys, a20 = dxs, a21 = dys,
                     a22 = dss;
         float det = a00 * (a11 * a22 - a21 * a12) - a01 * (a10 * a22 - a20 * a12) + a02 * (a10 * a21 - a20 * a11);
@@ -669,18 +674,10 @@ __device__ __forceinline__ bool refine_one(const Cand cd, const GaussSet& G, int
         }
     }
     if (!ok || i >= kMaxInterp) return false;
-    const int img = layer, prev = layer - 1, next = layer + 1;
-    const float dD0 = (DAT(img, r, c + 1) - DAT(img, r, c - 1)) * deriv_scale;
-    const float dD1 = (DAT(img, r + 1, c) - DAT(img, r - 1, c)) * deriv_scale;
-    const float dD2 = (DAT(next, r, c) - DAT(prev, r, c)) * deriv_scale;
-    const float tt = dD0 * xc + dD1 * xr + dD2 * xi;
-    const float contr = DAT(img, r, c) * img_scale + tt * 0.5f;
+    const float tt = l_dD0 * xc + l_dD1 * xr + l_dD2 * xi;
+    const float contr = l_ctr * img_scale + tt * 0.5f;
     if (fabsf(contr) * kLayers < kContrast) return false;
-    const float v2 = DAT(img, r, c) * 2.f;
-    const float dxx = (DAT(img, r, c + 1) + DAT(img, r, c - 1) - v2) * second_deriv_scale;
-    const float dyy = (DAT(img, r + 1, c) + DAT(img, r - 1, c) - v2) * second_deriv_scale;
-    const float dxy = (DAT(img, r + 1, c + 1) - DAT(img, r + 1, c - 1) - DAT(img, r - 1, c + 1) +
-                       DAT(img, r - 1, c - 1)) * cross_deriv_scale;
+    const float dxx = l_dxx, dyy = l_dyy, dxy = l_dxy;
     const float tr = dxx + dyy;
     const float det = dxx * dyy - dxy * dxy;
     if (det <= 0 || tr * tr * kEdge >= (kEdge + 1) * (kEdge + 1) * det) return false;
