@@ -101,12 +101,12 @@ __device__ __forceinline__ float from_fix(unsigned long long v) { return (float)
 // Fixed-point histogram value (long long)(v 2^24) as in oracle/sift.c, for v >= 0 (every contribution is a magnitude
 // times non-negative weights), without the signed 64-bit conversion sequence: x = v 2^24 splits exactly into hi = floor(x / 2^32) and lo = x - hi 2^32 (a multiple of ulp(x)
 // below 2^32), both truncated by v_cvt_u32_f32 -- the same integer as (long long)x.
-__device__ __forceinline__ unsigned long long to_fix_nn(float v) {
-    const float x = v * kFixScale;
+__device__ __forceinline__ unsigned long long to_fix_scaled(float x) {  // x = v 2^24 already
     const uint32_t hi = (uint32_t)(x * 2.3283064365386963e-10f);
     const uint32_t lo = (uint32_t)__builtin_fmaf(-(float)hi, 4294967296.0f, x);
     return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ unsigned long long to_fix_nn(float v) { return to_fix_scaled(v * kFixScale); }
 
 __device__ __forceinline__ int reflect101(int i, int n) {
     if (n == 1) return 0;
@@ -1382,6 +1382,9 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             const float w = exp_det(wexp);
             float obin = (o - ori) * bins_per_rad;
             const float mag = mag0 * w;
+            // the trilinear weights in fixed-point units (x 2^24, exact): every product and difference below scales
+            // with it in the normal range, and a value that left it unscaled is below 2^-102 here, i.e. 0 either way
+            const float mags = mag * kFixScale;
             const int r0 = (int)floorf(rbin), c0 = (int)floorf(cbin);
             int o0 = (int)floorf(obin);
             rbin -= r0;
@@ -1389,7 +1392,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             obin -= o0;
             if (o0 < 0) o0 += n;
             if (o0 >= n) o0 -= n;
-            const float v_r1 = mag * rbin, v_r0 = mag - v_r1;
+            const float v_r1 = mags * rbin, v_r0 = mags - v_r1;
             const float v_rc11 = v_r1 * cbin, v_rc10 = v_r1 - v_rc11;
             const float v_rc01 = v_r0 * cbin, v_rc00 = v_r0 - v_rc01;
             const float v_rco111 = v_rc11 * obin, v_rco110 = v_rc11 - v_rco111;
@@ -1401,7 +1404,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             // stay below 255 every fixed-point value is below 2^32 and is the single truncating conversion
             // (uint32_t)(v 2^24) -- the same integer as to_fix_nn, at a third of its instructions
             auto put = [&](int at, float v, bool small) {
-                atomicAdd(&hc[at], small ? (unsigned long long)(uint32_t)(v * kFixScale) : to_fix_nn(v));
+                atomicAdd(&hc[at], small ? (unsigned long long)(uint32_t)v : to_fix_scaled(v));
             };
             auto put8 = [&](bool small) {
                 put(idx, v_rco000, small);
