@@ -719,6 +719,10 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 // loaded separately (lanes 0 / 63 take them through the DPP's old operand): bit-exact, but 366 vs 367 us per launch
 // with the same FETCH_SIZE (the straddled lines are L2 hits) and 103 instead of 79 VGPRs (profiles/r05d_*).
 constexpr int kExWaves = 4, kExOut = 62, kExStrip = 72;
+// rows of loads in flight per wave (a multiple of 3 dividing kExStrip): 6 / 9 / 12 measured 4.98 / 5.08 / 5.10 ms for
+// octave 0 beside the next octave's blurs (profiles/r05at_*): the sweep is not waiting on its prefetch depth
+constexpr int kExAhead = 6;
+static_assert(kExAhead % 3 == 0 && kExStrip % kExAhead == 0, "row slots rotate by 3 within a strip");
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
 constexpr int kExList = 1024;  // per-block LDS list; overflow goes straight to the global list
@@ -856,8 +860,8 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     using S2 = std::integral_constant<int, 2>;
     // rows y0-1 (slot 0) and y0 (slot 1) first; then row y0+1+3k+j goes to slot (2+j)%3 and completes the window of
     // row y0+3k+j, whose centre sits in slot (1+j)%3.
-    // Six rows' loads (24 per lane) stay in flight: a row's buffer is refilled with the row six below as soon as it
-    // has been consumed (rows past the strip's last needed row y_end re-read row y_end, an L2 hit).
+    // kExAhead rows' loads stay in flight: a row's buffer is refilled with the row kExAhead below as soon as it has
+    // been consumed (rows past the strip's last needed row y_end re-read row y_end, an L2 hit).
     const int y_end = min(y0 + kExStrip, H);
     {
         float ga[kInLv], gb[kInLv];
@@ -866,39 +870,18 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
         finish(ga, S0{});
         finish(gb, S1{});
     }
-    float g1[kInLv], g2[kInLv], g3[kInLv], g4[kInLv], g5[kInLv], g6[kInLv];
-    fetch(y0 + 1, g1);
-    __builtin_amdgcn_sched_barrier(0);
-    fetch(y0 + 2, g2);
-    __builtin_amdgcn_sched_barrier(0);
-    fetch(y0 + 3, g3);
-    __builtin_amdgcn_sched_barrier(0);
-    fetch(y0 + 4, g4);
-    __builtin_amdgcn_sched_barrier(0);
-    fetch(y0 + 5, g5);
-    __builtin_amdgcn_sched_barrier(0);
-    fetch(y0 + 6, g6);
-    __builtin_amdgcn_sched_barrier(0);
-    for (int y = y0; y < y_end; y += 6) {
-        finish(g1, S2{});
-        fetch(min(y + 7, y_end), g1);
-        test_row(y, S1{});
-        finish(g2, S0{});
-        fetch(min(y + 8, y_end), g2);
-        test_row(y + 1, S2{});
-        finish(g3, S1{});
-        fetch(min(y + 9, y_end), g3);
-        test_row(y + 2, S0{});
-        finish(g4, S2{});
-        fetch(min(y + 10, y_end), g4);
-        test_row(y + 3, S1{});
-        finish(g5, S0{});
-        fetch(min(y + 11, y_end), g5);
-        test_row(y + 4, S2{});
-        finish(g6, S1{});
-        fetch(min(y + 12, y_end), g6);
-        test_row(y + 5, S0{});
-    }
+    float gq[kExAhead][kInLv];
+    static_for<kExAhead>([&](auto jc) {
+        fetch(y0 + 1 + decltype(jc)::value, gq[decltype(jc)::value]);
+        __builtin_amdgcn_sched_barrier(0);  // in row order, so the loop's waits count the younger rows exactly
+    });
+    for (int y = y0; y < y_end; y += kExAhead)
+        static_for<kExAhead>([&](auto jc) {
+            constexpr int jj = decltype(jc)::value;
+            finish(gq[jj], std::integral_constant<int, (2 + jj) % 3>{});
+            fetch(min(y + kExAhead + 1 + jj, y_end), gq[jj]);
+            test_row(y + jj, std::integral_constant<int, (1 + jj) % 3>{});
+        });
     __syncthreads();
     // the queued layer-1 / layer-3 pixels: outer DoG level's 3x3 block, every lane gathering at once
     for (int i = threadIdx.x; i < min(n_pend, kExPend); i += 64 * kExWaves) {
