@@ -505,31 +505,39 @@ __device__ __forceinline__ double pair_lo(double v) {
 // Gauss-Jordan-reduced 10 x 20 constraint matrix (all that stage 2 reads; valid in the odd lane of the pair). The
 // arithmetic per element is the single-lane elimination's, so the result is bit-identical to it. False for a
 // degenerate sample (uniform over the pair).
+//
+// Each lane builds only its own ten columns, with the same code: read homogeneously in (x, y, z, w = 1), columns 0..9
+// are the cubic monomials with at least two factors from {x, y} and 10..19 those with at least two from {z, w}, so
+// the renaming (x, y, z, w) -> (z, w, x, y) maps the second set onto the first. The odd lane builds columns 0..9 of
+// the constraint rows of the renamed E (each linear entry's coefficients [z w x y]) and so holds the original columns
+// 10..19 in the order kHiCol below (oracle/ransac.c build_rows / oracle_five_point follow the same construction).
 constexpr int kStageVals = 6 * 10 + 4 * 9;  // doubles handed from stage 1 to stage 2 per hypothesis
+// original column (minus 10) of the odd lane's column k: xxx->zzz, yyy->1, xxy->zz, xyy->z, xxz->xzz, xx->yzz,
+// yyz->x, yy->y, xyz->xz, xy->yz
+constexpr int kHiCol[10] = {6, 9, 7, 8, 0, 3, 2, 5, 1, 4};
 
 __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem m, int part, double N[4][9],
                                   double Rt[6][10]) {
     RPROF_DECL
     if (!nullspace_5x9(x1, x2, N)) return false;
     RPROF(1);
-    double E[9][4];
+    double E[9][4];  // the odd lane's entries renamed: coefficients [z w x y]
 #pragma unroll
     for (int e = 0; e < 9; ++e) {
-        E[e][0] = N[0][e];
-        E[e][1] = N[1][e];
-        E[e][2] = N[2][e];
-        E[e][3] = N[3][e];
+        E[e][0] = part ? N[2][e] : N[0][e];
+        E[e][1] = part ? N[3][e] : N[1][e];
+        E[e][2] = part ? N[0][e] : N[2][e];
+        E[e][3] = part ? N[1][e] : N[3][e];
     }
     // This lane's half of A: rows 0..kRegRows-1 in registers (G), rows kRegRows..9 in LDS (A). Each row is
-    // accumulated in registers, then stored once.
+    // accumulated in registers (only columns 0..9 are live), then stored once.
     LaneArr<double> A = m.u.at(-10 * kRegRows);  // A[10 * r + j] for r >= kRegRows
     double G[kRegRows][10];
     auto store_row = [&](int r, const double(&row)[20]) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) {
-            const double v = part ? row[10 + k] : row[k];
-            if (r < kRegRows) G[r < kRegRows ? r : 0][k] = v;
-            else A[10 * r + k] = v;
+            if (r < kRegRows) G[r < kRegRows ? r : 0][k] = row[k];
+            else A[10 * r + k] = row[k];
         }
     };
     double EEt[3][3][10], tr[10], tmp[10];
@@ -593,13 +601,14 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         best = pair_lo(best);
         if (best < 1e-14) return false;
         double prow[10];
+        // pr >= c: only register rows c..kRegRows-1 can be the pivot (static bounds, fewer selects)
         if (c < kRegRows) {  // pr may be a register row
             const bool in_lds = pr >= kRegRows;
 #pragma unroll
             for (int j = 0; j < 10; ++j) {
-                double v = in_lds ? A[10 * (in_lds ? pr : kRegRows) + j] : G[0][j];
+                double v = in_lds ? A[10 * (in_lds ? pr : kRegRows) + j] : G[c < kRegRows ? c : 0][j];
 #pragma unroll
-                for (int q = 1; q < kRegRows; ++q) v = pr == q ? G[q][j] : v;
+                for (int q = c + 1; q < kRegRows; ++q) v = pr == q ? G[q][j] : v;
                 prow[j] = v;
             }
         } else {
@@ -615,7 +624,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
                 for (int j = 0; j < 10; ++j) A[10 * pr + j] = crow[j];
             } else {
 #pragma unroll
-                for (int q = 0; q < kRegRows; ++q)
+                for (int q = c + 1; q < kRegRows; ++q)
 #pragma unroll
                     for (int j = 0; j < 10; ++j) G[q][j] = pr == q ? crow[j] : G[q][j];
             }
@@ -655,7 +664,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int j = 0; j < 10; ++j) Rt[r][j] = ld(4 + r, j);
+        for (int j = 0; j < 10; ++j) Rt[r][kHiCol[j]] = ld(4 + r, j);  // the odd lane's columns in original order
     RPROF(3);
     return true;
 }
