@@ -109,17 +109,19 @@ __device__ __forceinline__ void addmul_ql(const double* q, const double* l, doub
 // The solver's dynamically indexed arrays live in LDS, element i of lane l at base[i * 64 + l]: consecutive lanes hit
 // consecutive words, so every access is bank-conflict free, and nothing spills to scratch. The solver runs in two
 // kernels so each one's workgroup holds only its own phase's arrays:
-//   stage 1 (sample, 5x9 null space in registers, 10x20 Gauss-Jordan), two lanes per hypothesis: rows 6..9 of this
-//       lane's half of A (4 x 10; rows 0..5 in registers) = 20 KB per 64-lane workgroup;
+//   stage 1 (sample, 5x9 null space in registers, 10x20 elimination), two lanes per hypothesis: rows 8..9 of this
+//       lane's half of A (2 x 10; rows 0..7 in registers) = 10 KB per 64-lane workgroup;
 //   stage 2 (det B(z), Sturm chain, isolation, bisection, E): the chain is built in registers (generic degrees;
 //       a private-memory fallback for degree drops), the isolating intervals are selected into registers, and LDS
 //       holds only the isolation stack as left ends (24 doubles + 24 count bytes) = 13.5 KB per workgroup, so
 //       with <= 256 registers two waves share a SIMD.
 constexpr int kLanes = 64;
 // rows of the lane's half of A kept in registers (the rest in LDS): C2 solve1 per launch 364 / 330 / 330 / 323 us for
-// 2 / 4 / 5 / 6 (profiles/r05an_*): each Gauss-Jordan step moves every LDS row through registers, and the register
-// file has room (1 wave per SIMD either way: 314 VGPRs at 2, 406 at 6)
-constexpr int kRegRows = 6;
+// 2 / 4 / 5 / 6 (profiles/r05an_*): each elimination step moves every LDS row through registers, and the register
+// file has room (1 wave per SIMD either way: 314 VGPRs at 2, 406 at 6). With half-row construction and forward
+// elimination + back-substitution: 298 / 285 / 266 / 263 / 256 us for 4 / 5 / 6 / 7 / 8 (profiles/r05aw_*); 9 and 10
+// add more pivot-row selects (7292 / 7837 instructions against 6593 at 8)
+constexpr int kRegRows = 8;
 constexpr int kUnion = 10 * (10 - kRegRows);  // stage-1 doubles per lane: the LDS rows of the lane's half of A
 constexpr int kStack = 24;    // == oracle/ransac.c ISO_STACK
 constexpr int kRootDbl = kStack;  // stage-2 doubles per lane: the isolation stack's left ends
@@ -584,8 +586,9 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         store_row(0, row);
     }
     RPROF(2);
-    // Gauss-Jordan with partial pivoting on the lane's half rows; every row is moved through registers whole. Row
-    // indices are static except the pivot row pr, which is read / written through LDS or a register select.
+    // Gaussian elimination with partial pivoting (Gauss-Jordan's pivots) on the lane's half rows, then back-substitution
+    // of rows 4..9 (oracle/ransac.c oracle_five_point); every row is moved through registers whole. Row indices are
+    // static except the pivot row pr, which is read / written through LDS or a register select.
     auto ld = [&](int r, int j) -> double { return r < kRegRows ? G[r < kRegRows ? r : 0][j] : A[10 * r + j]; };
     // one column step per call with a compile-time column (no dynamically indexed register rows)
     auto gj_step = [&](auto cc) -> bool {
@@ -638,8 +641,7 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
             else A[10 * c + j] = prow[j];
         }
 #pragma unroll
-        for (int r = 0; r < 10; ++r) {
-            if (r == c) continue;
+        for (int r = c + 1; r < 10; ++r) {  // forward elimination only: rows 4..9 are back-substituted below
             double row[10];
 #pragma unroll
             for (int j = 0; j < 10; ++j) row[j] = ld(r, j);
@@ -661,6 +663,28 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         !gj_step(integral_constant<int, 6>{}) || !gj_step(integral_constant<int, 7>{}) ||
         !gj_step(integral_constant<int, 8>{}) || !gj_step(integral_constant<int, 9>{}))
         return false;
+    // back-substitution of rows 4..9 (all that stage 2 reads): 15 row updates instead of Gauss-Jordan's 45 above
+    // the pivots; rows 0..3 are dead after their forward step
+#pragma unroll
+    for (int c = 9; c >= 5; --c) {
+        double prow[10];
+#pragma unroll
+        for (int j = 0; j < 10; ++j) prow[j] = ld(c, j);
+#pragma unroll
+        for (int r = 4; r < c; ++r) {
+            double row[10];
+#pragma unroll
+            for (int j = 0; j < 10; ++j) row[j] = ld(r, j);
+            const double f = pair_lo(row[c]);
+#pragma unroll
+            for (int j = 0; j < 10; ++j) row[j] = __builtin_fma(-f, prow[j], row[j]);
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+                if (r < kRegRows) G[r < kRegRows ? r : 0][j] = row[j];
+                else A[10 * r + j] = row[j];
+            }
+        }
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll

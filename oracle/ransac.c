@@ -377,7 +377,9 @@ int oracle_five_point(const double* x1, const double* x2, double* Es) {
             for (int k = 0; k < 10; ++k) A[r][HI_COL[k]] = Ar[r][k];
     }
 
-    /* Gauss-Jordan with partial pivoting on columns 0..9 -> [I | C] */
+    /* Gaussian elimination with partial pivoting on columns 0..9 (each pivot row scaled to a unit pivot), then
+     * back-substitution of rows 4..9 only -> rows 4..9 of [I | C], all that B(z) reads. The pivots are Gauss-Jordan's;
+     * rows 0..3 are not reduced above their pivots (the device's order: ransac.hip five_point_stage1). */
     for (int c = 0; c < 10; ++c) {
         int pr = c;
         double best = fabs(A[c][c]);
@@ -388,12 +390,16 @@ int oracle_five_point(const double* x1, const double* x2, double* Es) {
             for (int j = 0; j < NMONO; ++j) { double t = A[c][j]; A[c][j] = A[pr][j]; A[pr][j] = t; }
         const double inv = 1.0 / A[c][c];
         for (int j = 0; j < NMONO; ++j) A[c][j] *= inv;
-        for (int r = 0; r < 10; ++r) {
-            if (r == c) continue;
+        for (int r = c + 1; r < 10; ++r) {
             const double f = A[r][c];
             for (int j = 0; j < NMONO; ++j) A[r][j] = fma(-f, A[c][j], A[r][j]);
         }
     }
+    for (int c = 9; c >= 5; --c)
+        for (int r = 4; r < c; ++r) {
+            const double f = A[r][c];
+            for (int j = 0; j < NMONO; ++j) A[r][j] = fma(-f, A[c][j], A[r][j]);
+        }
     /* B(z): rows k = e - z f, l = g - z h, m = i - z j (rows 4..9); columns [x-coef(deg3), y-coef(deg3), 1(deg4)] */
     /* trailing columns: 10 xzz, 11 xz, 12 x, 13 yzz, 14 yz, 15 y, 16 zzz, 17 zz, 18 z, 19 one */
     double B[3][3][5];
