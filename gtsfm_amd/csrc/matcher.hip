@@ -1098,11 +1098,15 @@ __global__ __launch_bounds__(256, 2) void fl_shortlist_kernel(const _Float16* __
     }
 }
 
-// grid (kpad / 32, P, 2 sides), 256 threads: thread (r, c) = (tid / 8, tid % 8) sums keypoint i0 + r's distance to
-// its c-th shortlisted candidate straight from HBM/L2 (float4 row walks, many loads in flight), sequentially and
-// unfused: exact_top2_kernel's arithmetic. Then one thread per keypoint scans its 8 candidates in index order (the
-// exact scan's b1 / j1 / b2 updates) and checks the certificate; uncertified keypoints go to `redo`.
-constexpr int kFlRerankRows = 256 / kFlCand;
+// grid ceil(2P / 8) * 8 units x ceil(kmax / 128) row blocks (1-D, XCD-ordered below), 256 threads, keypoints
+// i0 .. i0 + 127 of one (pair, side): the exact squared distance of each keypoint to its shortlisted candidates, each
+// summed by one thread straight from HBM/L2 (float4 row walks), sequentially and unfused: exact_top2_kernel's
+// arithmetic. Two rounds, every lane busy in both: first the two best keys' candidates (two threads per keypoint);
+// then the other six, minus those whose key bound already exceeds the larger of the first two exact distances
+// (d^2 >= (|a|^2 + key) - eps > that: neither of the exact top two, nor tied with them), compacted into a work list
+// the 256 threads share. Then one thread per keypoint scans its 8 candidates in index order (the exact scan's b1 / j1
+// / b2 updates) and checks the certificate; uncertified keypoints go to `redo`.
+constexpr int kFlRerankRows = 128;
 __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict__ desc, const int* __restrict__ counts,
                                                         int kmax, int dim, const int* __restrict__ pairs, int n_pairs,
                                                         int kpad, const float* __restrict__ norm2,
@@ -1113,16 +1117,26 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
                                                         int* __restrict__ redo_count, int4* __restrict__ redo,
                                                         int* __restrict__ unc) {
 #pragma clang fp contract(off)
-    __shared__ float sacc[kFlRerankRows][kFlCand];
-    __shared__ int sj[kFlRerankRows][kFlCand];
-    const int p = blockIdx.y, side = blockIdx.z, tid = threadIdx.x;
+    constexpr int R = kFlRerankRows, C = kFlCand;
+    static_assert(2 * R == 256, "round 1: two threads per keypoint");
+    __shared__ float sacc[R][C];
+    __shared__ int sj[R][C];
+    __shared__ uint16_t work[R * (C - 2)];
+    __shared__ int n_work;
+    // XCD-aware order: workgroups go round-robin over the 8 XCDs in dispatch order, so XCD x runs every row block of
+    // units x, x + 8, ... (unit = one (pair, side)); a unit's train rows, read at random by all of its blocks, are
+    // fetched into one XCD's L2. Side-1 units come first, in pair order (consecutive ones share their train image).
+    const int nb = (kmax + R - 1) / R;
+    const int xcd = blockIdx.x & 7, kx = blockIdx.x >> 3;
+    const int u = (kx / nb) * 8 + xcd;
+    if (u >= 2 * n_pairs) return;
+    const int side = u < n_pairs ? 1 : 0, p = u < n_pairs ? u : u - n_pairs, tid = threadIdx.x;
     const int iq = pairs[2 * p + side], it = pairs[2 * p + 1 - side];
     const int nq = counts[iq], nt = counts[it];
-    const int i0 = blockIdx.x * kFlRerankRows;
+    const int i0 = (kx % nb) * R;
     if (i0 >= nq) return;
-    const int r = tid / kFlCand, c = tid % kFlCand, i = i0 + r;
-    // the exact squared distance of this thread's candidate, sequential and unfused (exact_top2_kernel's arithmetic)
-    auto exact_d2 = [&](int jj) {
+    // the exact squared distance of keypoint i to train keypoint jj, sequential and unfused
+    auto exact_d2 = [&](int i, int jj) {
         const float* q = desc + ((size_t)iq * kmax + i) * dim;
         const float* t = desc + ((size_t)it * kmax + jj) * dim;
         float a = 0.f;
@@ -1155,34 +1169,47 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
                             D * eta * eta;
         return 1.5f * (2.f * e_dot + (D + 4.f) * 2.f / 16777216.f * (na + bn * bn));
     };
-    const size_t o = ((size_t)side * n_pairs + p) * kmax + i;
-    int j = -1;
-    float acc = __builtin_inff();
-    if (i < nq) {
-        j = cand[o * kFlCand + c];
-        if (j >= nt) j = -1;
+    const size_t obase = ((size_t)side * n_pairs + p) * kmax;  // + i: this (pair, side)'s shortlist row of keypoint i
+    // candidate ids (-1: none)
+    for (int s = tid; s < R * C; s += 256) {
+        const int r = s / C, c = s % C, i = i0 + r;
+        int j = -1;
+        if (i < nq) {
+            j = cand[(obase + i) * C + c];
+            if (j >= nt) j = -1;
+        }
+        sj[r][c] = j;
+        sacc[r][c] = __builtin_inff();
     }
-    // Two rounds. The two best keys' candidates first; then a candidate whose key bound already exceeds the larger of
-    // those two exact distances (d^2 >= (|a|^2 + key) - eps > that) can be neither of the exact top two, nor tie
-    // them, and is dropped instead of summed (its slot reads as empty in the scan below).
-    if (c < 2 && j >= 0) acc = exact_d2(j);
-    sacc[r][c] = acc;
+    if (tid == 0) n_work = 0;
     __syncthreads();
-    if (c >= 2 && j >= 0) {
+    {  // round 1: the two best keys' candidates
+        const int r = tid >> 1, c = tid & 1, j = sj[r][c];
+        if (j >= 0) sacc[r][c] = exact_d2(i0 + r, j);
+    }
+    __syncthreads();
+    // round 2's work list: candidates 2..7 that the bound cannot drop
+    for (int s = tid; s < R * (C - 2); s += 256) {
+        const int r = s / (C - 2), c = 2 + s % (C - 2), i = i0 + r;
+        const int j = sj[r][c];
+        if (j < 0) continue;
         const float a2 = fmaxf(sacc[r][0], sacc[r][1]);
         bool skip = false;
         if (safe && a2 < __builtin_inff()) {
             const float na = norm2[(size_t)iq * kpad + i];
-            skip = (na + tkey[o * kFlCand + c]) - key_eps(na) > a2 * (1.f + 1e-4f) + key_eps(na);
+            skip = (na + tkey[(obase + i) * C + c]) - key_eps(na) > a2 * (1.f + 1e-4f) + key_eps(na);
         }
-        if (skip) j = -1;
-        else acc = exact_d2(j);
+        if (skip) sj[r][c] = -1;
+        else work[atomicAdd(&n_work, 1)] = (uint16_t)(r * C + c);
     }
     __syncthreads();
-    sacc[r][c] = acc;
-    sj[r][c] = j;
+    const int nw = n_work;
+    for (int w = tid; w < nw; w += 256) {
+        const int rc = work[w], r = rc / C, c = rc % C;
+        sacc[r][c] = exact_d2(i0 + r, sj[r][c]);
+    }
     __syncthreads();
-    if (tid >= kFlRerankRows) return;
+    if (tid >= R) return;
     const int ii = i0 + tid;
     if (ii >= nq) return;
     // the shortlist in index order (insertion sort of 8 (j, acc) records; -1 = empty goes last)
@@ -1213,8 +1240,7 @@ __global__ __launch_bounds__(256) void fl_rerank_kernel(const float* __restrict_
     if (!certified && safe) {
         const float na = norm2[(size_t)iq * kpad + ii];
         const float eps = key_eps(na);
-        certified = (na + tkey[(((size_t)side * n_pairs + p) * kmax + ii) * kFlCand + kFlCand - 1]) - eps >
-                    a2 * (1.f + 1e-4f) + eps;
+        certified = (na + tkey[(obase + ii) * kFlCand + kFlCand - 1]) - eps > a2 * (1.f + 1e-4f) + eps;
     }
     if (!certified) {
         redo[atomicAdd(redo_count, 1)] = make_int4(side, p, ii, 0);
@@ -1487,7 +1513,8 @@ int run_fl_match(const float* d_desc, const int* d_counts, int n_img, int kmax, 
     }
     if (rc != GTSFM_OK) return rc;
     if (g_mnn_events[1]) GTSFM_CHECK_HIP(hipEventRecord(g_mnn_events[1], stream));
-    hipLaunchKernelGGL(fl_rerank_kernel, dim3((kmax + kFlRerankRows - 1) / kFlRerankRows, n_pairs, 2), dim3(256), 0,
+    hipLaunchKernelGGL(fl_rerank_kernel, dim3((unsigned)(((2 * (size_t)n_pairs + 7) / 8) * 8 *
+                                                ((kmax + kFlRerankRows - 1) / kFlRerankRows))), dim3(256), 0,
                        stream, d_desc, d_counts, kmax, dim, d_pairs, n_pairs, kpad, norm2, maxnorm, unsafe, cand, tkey,
                        rowres, colres, redo_count, redo, unc);
     GTSFM_CHECK_HIP(hipGetLastError());
