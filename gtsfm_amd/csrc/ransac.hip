@@ -663,8 +663,8 @@ __device__ bool five_point_stage1(const double* x1, const double* x2, SolverMem 
         !gj_step(integral_constant<int, 6>{}) || !gj_step(integral_constant<int, 7>{}) ||
         !gj_step(integral_constant<int, 8>{}) || !gj_step(integral_constant<int, 9>{}))
         return false;
-    // back-substitution of rows 4..9 (all that stage 2 reads): 15 row updates instead of Gauss-Jordan's 45 above
-    // the pivots; rows 0..3 are dead after their forward step
+    // back-substitution of rows 4..9 (all that stage 2 reads; rows 0..3 are dead after their forward step), each
+    // pivot row fully reduced before it is used
 #pragma unroll
     for (int c = 9; c >= 5; --c) {
         double prow[10];

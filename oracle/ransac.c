@@ -13,7 +13,8 @@
  * internals — graph-cut LO, SPRT, its RNG — are not reproducible without its source, so parity with OpenCV is
  * tolerance-based and pinned by the reference's known-answer verifier tests):
  *   - minimal solver: Nister's 5-point algorithm (TPAMI 2004): 4-dim null space of the 5x9 epipolar system,
- *     10 cubic constraints (det E = 0, 2EE^TE - tr(EE^T)E = 0) in 20 monomials, Gauss-Jordan, the 3x3
+ *     10 cubic constraints (det E = 0, 2EE^TE - tr(EE^T)E = 0) in 20 monomials, elimination to [I | C] (the rows
+ *     B(z) reads), the 3x3
  *     polynomial matrix B(z), degree-10 det B(z); real roots by Sturm-sequence isolation + bisection.
  *   - inlier test: squared Sampson distance <= threshold^2 (OpenCV EMEstimatorCallback::computeError), written
  *     division-free: (x2'Ex1)^2 <= thr^2 * (|Ex1|_xy^2 + |E'x2|_xy^2), float32 with explicit fmaf.
