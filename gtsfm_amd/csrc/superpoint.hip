@@ -244,14 +244,20 @@ __device__ __forceinline__ void sp_split3(float x, __bf16& h, __bf16& m, __bf16&
 
 __device__ __forceinline__ int swz16(int row, int half) { return 8 * (half ^ ((row >> 3) & 1)); }
 
+// A workgroup = kConv3RowPairs x 4 waves over kConv3Rows conv rows x 32 columns x 64 output channels: the staged
+// 16-channel weight slab (55 KB at 3 x 3) is shared by all of them, so its L2 traffic per MFMA falls with the rows.
+// C3 per step (profiles/r05bj_*, r05bk_*): 1 / 2 / 3 / 4 row pairs -> conv3 3x3+pool 5148 / 4074 / 4117 / 3927 us,
+// 3x3 1625 / 1288 / 1364 / 1285 us per launch (4: 16 waves, one workgroup per CU, 104 VGPRs).
+constexpr int kConv3RowPairs = 4, kConv3Rows = 2 * kConv3RowPairs, kConv3Threads = kConvThreads * kConv3RowPairs;
+
 template <int KS, bool POOL>
-__global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, const __bf16* __restrict__ w3) {
+__global__ __launch_bounds__(kConv3Threads, 1) void conv3_kernel(ConvArgs a, const __bf16* __restrict__ w3) {
     constexpr int R = KS / 2;
-    constexpr int PH = 2 + 2 * R, PW = 32 + 2 * R;
+    constexpr int PH = kConv3Rows + 2 * R, PW = 32 + 2 * R;
     constexpr int kPU = PH * PW * 2;             // patch staging units (pixel, 8-channel half)
     constexpr int kWU = KS * KS * 3 * 64 * 2;    // weight staging units (tap, plane, cout, half)
-    constexpr int kNP = (kPU + kConvThreads - 1) / kConvThreads;
-    constexpr int kNW = (kWU + kConvThreads - 1) / kConvThreads;
+    constexpr int kNP = (kPU + kConv3Threads - 1) / kConv3Threads;
+    constexpr int kNW = (kWU + kConv3Threads - 1) / kConv3Threads;
     __shared__ __attribute__((aligned(16))) __bf16 patch[3][PH * PW][16];
     __shared__ __attribute__((aligned(16))) __bf16 wt[KS * KS][3][64][16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -261,10 +267,10 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
     t /= a.tiles_x;
     const int ty = t % a.tiles_y;
     const int img = t / a.tiles_y;
-    const int y0 = 2 * ty, x0 = 32 * tx;
-    const int wx = wave & 1, wn = wave >> 1;
+    const int y0 = kConv3Rows * ty, x0 = 32 * tx;
+    const int wx = wave & 1, wn = (wave >> 1) & 1, wr = wave >> 2;  // wr: the wave's row pair
     const int i = lane & 31, kh = lane >> 5;
-    const int prow = i >> 4, pcol = 16 * wx + (i & 15);
+    const int prow = (i >> 4) + 2 * wr, pcol = 16 * wx + (i & 15);
     const int ncol = (lane & 31) + 32 * wn;
     const float* inb = a.in + (size_t)img * a.Hi * a.Wi * a.in_cstride + a.in_c0;
     f32x16 acc = {};
@@ -273,7 +279,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
     auto load = [&](int c0) {
 #pragma unroll
         for (int u = 0; u < kNP; ++u) {
-            const int e = tid + u * kConvThreads;
+            const int e = tid + u * kConv3Threads;
             const int pix = e >> 1, hf = e & 1;
             const int py = pix / PW, px = pix - py * PW;
             const int gy = y0 - R + py, gx = x0 - R + px;
@@ -287,7 +293,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
         const int chunk = c0 / kCinChunk, nchunk = a.Cin / kCinChunk;
 #pragma unroll
         for (int u = 0; u < kNW; ++u) {
-            const int e = tid + u * kConvThreads;
+            const int e = tid + u * kConv3Threads;
             if (e < kWU) {
                 const int hf = e & 1, co = (e >> 1) & 63, p = (e >> 7) % 3, kk = (e >> 7) / 3;
                 wv[u] = *(const u32x4*)(w3 + ((((size_t)kk * nchunk + chunk) * 3 + p) * a.cout_pad + 64 * ct + co) * 16 +
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
     auto stash = [&]() {
 #pragma unroll
         for (int u = 0; u < kNP; ++u) {
-            const int e = tid + u * kConvThreads;
+            const int e = tid + u * kConv3Threads;
             if (e < kPU) {
                 const int pix = e >> 1, hf = e & 1;
                 bf16x8 h, m, l;
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
         }
 #pragma unroll
         for (int u = 0; u < kNW; ++u) {
-            const int e = tid + u * kConvThreads;
+            const int e = tid + u * kConv3Threads;
             if (e < kWU) {
                 const int hf = e & 1, co = (e >> 1) & 63, p = (e >> 7) % 3, kk = (e >> 7) / 3;
                 *(u32x4*)&wt[kk][p][co][swz16(co, hf)] = wv[u];
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
     float* outb = a.out + a.out_c0 + co;
     if constexpr (POOL) {
         const int Ho = a.Hi / 2, Wo = a.Wi / 2;
-        const int py = y0 / 2;
+        const int py = y0 / 2 + wr;
         if (py >= Ho) return;
 #pragma unroll
         for (int qa = 0; qa < 2; ++qa)
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(kConvThreads, 2) void conv3_kernel(ConvArgs a, cons
 #pragma unroll
         for (int g = 0; g < 16; ++g) {
             const int ip = 4 * kh + (g & 3) + 8 * (g >> 2);
-            const int y = y0 + (ip >> 4), x = x0 + 16 * wx + (ip & 15);
+            const int y = y0 + 2 * wr + (ip >> 4), x = x0 + 16 * wx + (ip & 15);
             if (y >= a.Hi || x >= a.Wi) continue;
             float v = acc[g] + b;
             if (a.relu) v = v > 0.0f ? v : 0.0f;
@@ -750,11 +756,12 @@ hipError_t launch_conv(int n, const float* in, int Hi, int Wi, int in_cstride, i
     a.bias = a.w + (size_t)kSp[layer].k * kSp[layer].k * kSp[layer].cin * a.cout_pad;
     a.out = out; a.out_cstride = out_cstride; a.out_c0 = out_c0; a.Cout = Cout; a.relu = 1;
     a.tiles_x = (Wi + 31) / 32;
-    a.tiles_y = (Hi + 1) / 2;
-    if (POOL) a.tiles_y = (Hi / 2);  // pooled rows only (MaxPool2d floors; an odd last conv row is dropped)
+    a.tiles_y = (Hi + kConv3Rows - 1) / kConv3Rows;
+    // pooled rows only (MaxPool2d floors; an odd last conv row is dropped): kConv3RowPairs pooled rows per tile
+    if (POOL) a.tiles_y = (Hi / 2 + kConv3RowPairs - 1) / kConv3RowPairs;
     if (a.tiles_x == 0 || a.tiles_y == 0) return hipSuccess;
     const dim3 grid((unsigned)(a.tiles_x * a.tiles_y * n), (unsigned)((Cout + 63) / 64));
-    hipLaunchKernelGGL((conv3_kernel<KS, POOL>), grid, dim3(kConvThreads), 0, stream, a, w3 + sp_w3_offset(layer));
+    hipLaunchKernelGGL((conv3_kernel<KS, POOL>), grid, dim3(kConv3Threads), 0, stream, a, w3 + sp_w3_offset(layer));
     return hipGetLastError();
 }
 
@@ -827,9 +834,9 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, in
         a.bias = a.w + (size_t)256 * a.cout_pad;
         a.out = out; a.out_cstride = out_cstride; a.out_c0 = 0; a.Cout = Cout; a.relu = 0;
         a.tiles_x = (d.W8 + 31) / 32;
-        a.tiles_y = (d.H8 + 1) / 2;
+        a.tiles_y = (d.H8 + kConv3Rows - 1) / kConv3Rows;
         const dim3 grid((unsigned)(a.tiles_x * a.tiles_y * n), (unsigned)((Cout + 63) / 64));
-        hipLaunchKernelGGL((conv3_kernel<1, false>), grid, dim3(kConvThreads), 0, stream, a, w3 + sp_w3_offset(layer));
+        hipLaunchKernelGGL((conv3_kernel<1, false>), grid, dim3(kConv3Threads), 0, stream, a, w3 + sp_w3_offset(layer));
         return hipGetLastError();
     };
     GTSFM_CHECK_HIP(conv1x1(LPB, 0, logits, 128, 65));
