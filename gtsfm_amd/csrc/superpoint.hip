@@ -244,14 +244,22 @@ __device__ __forceinline__ void sp_split3(float x, __bf16& h, __bf16& m, __bf16&
 
 __device__ __forceinline__ int swz16(int row, int half) { return 8 * (half ^ ((row >> 3) & 1)); }
 
-// A workgroup = kConv3RowPairs x 4 waves over kConv3Rows conv rows x 32 columns x 64 output channels: the staged
+// A workgroup = conv3_rp row pairs x (4 / conv3_nt) waves over conv3_rows conv rows x 32 columns x 64 output
+// channels: the staged
 // 16-channel weight slab (55 KB at 3 x 3) is shared by all of them, so its L2 traffic per MFMA falls with the rows.
 // C3 per step (profiles/r05bj_*, r05bk_*): 1 / 2 / 3 / 4 row pairs -> conv3 3x3+pool 5148 / 4074 / 4117 / 3927 us,
 // 3x3 1625 / 1288 / 1364 / 1285 us per launch (4: 16 waves, one workgroup per CU, 104 VGPRs).
-constexpr int kConv3RowPairs = 4, kConv3Rows = 2 * kConv3RowPairs, kConv3Threads = kConvThreads * kConv3RowPairs;
+// conv3_nt: 32-channel output tiles per wave (2: each A fragment read from LDS feeds both). 3 x 3: 8 row pairs x 2
+// tiles -> 3709 / 1250 us (16 waves, 118 VGPRs; profiles/r05bm_*); the 1 x 1 heads on the 1/8 grid keep 4 row
+// pairs x 1 tile (285 against 335 us with 16-row tiles).
+__host__ __device__ constexpr int conv3_rp(int ks) { return ks == 3 ? 8 : 4; }
+__host__ __device__ constexpr int conv3_nt(int ks) { return ks == 3 ? 2 : 1; }
+__host__ __device__ constexpr int conv3_rows(int ks) { return 2 * conv3_rp(ks); }
+__host__ __device__ constexpr int conv3_threads(int ks) { return 64 * (4 / conv3_nt(ks)) * conv3_rp(ks); }
 
 template <int KS, bool POOL>
-__global__ __launch_bounds__(kConv3Threads, 1) void conv3_kernel(ConvArgs a, const __bf16* __restrict__ w3) {
+__global__ __launch_bounds__(conv3_threads(KS), 1) void conv3_kernel(ConvArgs a, const __bf16* __restrict__ w3) {
+    constexpr int kConv3NT = conv3_nt(KS), kConv3Rows = conv3_rows(KS), kConv3Threads = conv3_threads(KS);
     constexpr int R = KS / 2;
     constexpr int PH = kConv3Rows + 2 * R, PW = 32 + 2 * R;
     constexpr int kPU = PH * PW * 2;             // patch staging units (pixel, 8-channel half)
@@ -268,12 +276,14 @@ __global__ __launch_bounds__(kConv3Threads, 1) void conv3_kernel(ConvArgs a, con
     const int ty = t % a.tiles_y;
     const int img = t / a.tiles_y;
     const int y0 = kConv3Rows * ty, x0 = 32 * tx;
-    const int wx = wave & 1, wn = (wave >> 1) & 1, wr = wave >> 2;  // wr: the wave's row pair
+    // wr: the wave's row pair; wn: its output-channel tile (kConv3NT == 1)
+    const int wx = wave & 1, wn = kConv3NT == 1 ? (wave >> 1) & 1 : 0, wr = kConv3NT == 1 ? wave >> 2 : wave >> 1;
     const int i = lane & 31, kh = lane >> 5;
     const int prow = (i >> 4) + 2 * wr, pcol = 16 * wx + (i & 15);
-    const int ncol = (lane & 31) + 32 * wn;
     const float* inb = a.in + (size_t)img * a.Hi * a.Wi * a.in_cstride + a.in_c0;
-    f32x16 acc = {};
+    f32x16 acc[kConv3NT];
+#pragma unroll
+    for (int nt = 0; nt < kConv3NT; ++nt) acc[nt] = f32x16{};
     f32x4_t pv[kNP][2];
     u32x4 wv[kNW];
     auto load = [&](int c0) {
@@ -342,19 +352,25 @@ __global__ __launch_bounds__(kConv3Threads, 1) void conv3_kernel(ConvArgs a, con
 #pragma unroll
             for (int kx = 0; kx < KS; ++kx) {
                 const int pix = (prow + ky) * PW + pcol + kx, kk = ky * KS + kx;
-                const int po = swz16(pix, kh), wo = swz16(ncol, kh);
+                const int po = swz16(pix, kh);
                 const bf16x8 a0 = *(const bf16x8*)&patch[0][pix][po];
                 const bf16x8 a1 = *(const bf16x8*)&patch[1][pix][po];
                 const bf16x8 a2 = *(const bf16x8*)&patch[2][pix][po];
-                const bf16x8 b0 = *(const bf16x8*)&wt[kk][0][ncol][wo];
-                const bf16x8 b1 = *(const bf16x8*)&wt[kk][1][ncol][wo];
-                const bf16x8 b2 = *(const bf16x8*)&wt[kk][2][ncol][wo];
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+#pragma unroll
+                for (int nt = 0; nt < kConv3NT; ++nt) {
+                    const int ncol = (lane & 31) + 32 * (wn + nt), wo = swz16(ncol, kh);
+                    const bf16x8 b0 = *(const bf16x8*)&wt[kk][0][ncol][wo];
+                    const bf16x8 b1 = *(const bf16x8*)&wt[kk][1][ncol][wo];
+                    const bf16x8 b2 = *(const bf16x8*)&wt[kk][2][ncol][wo];
+                    f32x16 c = acc[nt];
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, c, 0, 0, 0);
+                    acc[nt] = c;
+                }
             }
         if (!more) break;
         __syncthreads();
@@ -362,20 +378,24 @@ __global__ __launch_bounds__(kConv3Threads, 1) void conv3_kernel(ConvArgs a, con
         __syncthreads();
     }
     // epilogue (conv_mfma_kernel's): acc[g] = conv output at tile pixel 4 kh + (g & 3) + 8 (g >> 2), channel ncol
+#pragma unroll
+    for (int nt = 0; nt < kConv3NT; ++nt) {
+    const f32x16& acc_nt = acc[nt];
+    const int ncol = (lane & 31) + 32 * (wn + nt);
     const int co = 64 * ct + ncol;
-    if (co >= a.Cout) return;
+    if (co >= a.Cout) continue;
     const float b = a.bias[co];
     float* outb = a.out + a.out_c0 + co;
     if constexpr (POOL) {
         const int Ho = a.Hi / 2, Wo = a.Wi / 2;
         const int py = y0 / 2 + wr;
-        if (py >= Ho) return;
+        if (py >= Ho) continue;
 #pragma unroll
         for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
             for (int rp = 0; rp < 2; ++rp) {
                 const int g0 = 4 * qa + 2 * rp, g1 = 4 * (qa + 2) + 2 * rp;
-                float v = fmaxf(fmaxf(acc[g0], acc[g0 + 1]), fmaxf(acc[g1], acc[g1 + 1]));
+                float v = fmaxf(fmaxf(acc_nt[g0], acc_nt[g0 + 1]), fmaxf(acc_nt[g1], acc_nt[g1 + 1]));
                 v = v + b;
                 if (a.relu) v = v > 0.0f ? v : 0.0f;
                 const int px = x0 / 2 + 8 * wx + 4 * qa + 2 * kh + rp;
@@ -387,10 +407,11 @@ __global__ __launch_bounds__(kConv3Threads, 1) void conv3_kernel(ConvArgs a, con
             const int ip = 4 * kh + (g & 3) + 8 * (g >> 2);
             const int y = y0 + 2 * wr + (ip >> 4), x = x0 + 16 * wx + (ip & 15);
             if (y >= a.Hi || x >= a.Wi) continue;
-            float v = acc[g] + b;
+            float v = acc_nt[g] + b;
             if (a.relu) v = v > 0.0f ? v : 0.0f;
             outb[(((size_t)img * a.Hi + y) * a.Wi + x) * a.out_cstride] = v;
         }
+    }
     }
 }
 
@@ -756,12 +777,12 @@ hipError_t launch_conv(int n, const float* in, int Hi, int Wi, int in_cstride, i
     a.bias = a.w + (size_t)kSp[layer].k * kSp[layer].k * kSp[layer].cin * a.cout_pad;
     a.out = out; a.out_cstride = out_cstride; a.out_c0 = out_c0; a.Cout = Cout; a.relu = 1;
     a.tiles_x = (Wi + 31) / 32;
-    a.tiles_y = (Hi + kConv3Rows - 1) / kConv3Rows;
-    // pooled rows only (MaxPool2d floors; an odd last conv row is dropped): kConv3RowPairs pooled rows per tile
-    if (POOL) a.tiles_y = (Hi / 2 + kConv3RowPairs - 1) / kConv3RowPairs;
+    a.tiles_y = (Hi + conv3_rows(KS) - 1) / conv3_rows(KS);
+    // pooled rows only (MaxPool2d floors; an odd last conv row is dropped): conv3_rp pooled rows per tile
+    if (POOL) a.tiles_y = (Hi / 2 + conv3_rp(KS) - 1) / conv3_rp(KS);
     if (a.tiles_x == 0 || a.tiles_y == 0) return hipSuccess;
     const dim3 grid((unsigned)(a.tiles_x * a.tiles_y * n), (unsigned)((Cout + 63) / 64));
-    hipLaunchKernelGGL((conv3_kernel<KS, POOL>), grid, dim3(kConv3Threads), 0, stream, a, w3 + sp_w3_offset(layer));
+    hipLaunchKernelGGL((conv3_kernel<KS, POOL>), grid, dim3(conv3_threads(KS)), 0, stream, a, w3 + sp_w3_offset(layer));
     return hipGetLastError();
 }
 
@@ -834,9 +855,9 @@ int gtsfm_superpoint_batched(const uint8_t* d_images, const uint8_t* d_masks, in
         a.bias = a.w + (size_t)256 * a.cout_pad;
         a.out = out; a.out_cstride = out_cstride; a.out_c0 = 0; a.Cout = Cout; a.relu = 0;
         a.tiles_x = (d.W8 + 31) / 32;
-        a.tiles_y = (d.H8 + kConv3Rows - 1) / kConv3Rows;
+        a.tiles_y = (d.H8 + conv3_rows(1) - 1) / conv3_rows(1);
         const dim3 grid((unsigned)(a.tiles_x * a.tiles_y * n), (unsigned)((Cout + 63) / 64));
-        hipLaunchKernelGGL((conv3_kernel<1, false>), grid, dim3(kConv3Threads), 0, stream, a, w3 + sp_w3_offset(layer));
+        hipLaunchKernelGGL((conv3_kernel<1, false>), grid, dim3(conv3_threads(1)), 0, stream, a, w3 + sp_w3_offset(layer));
         return hipGetLastError();
     };
     GTSFM_CHECK_HIP(conv1x1(LPB, 0, logits, 128, 65));
