@@ -520,8 +520,9 @@ __global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float
                                                              const int* __restrict__ side_counts, int kmax, int cross,
                                                              float* __restrict__ out /*(2P, kmax, 256)*/) {
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    __shared__ __attribute__((aligned(16))) __bf16 Ks[3][kAttnKeys][kAttnPad];
-    __shared__ __attribute__((aligned(16))) __bf16 Vs[3][kHd][kAttnPad];
+    // double-buffered: chunk c + 1 is stashed into the other buffer while chunk c is read (one barrier per chunk)
+    __shared__ __attribute__((aligned(16))) __bf16 Ks[2][3][kAttnKeys][kAttnPad];
+    __shared__ __attribute__((aligned(16))) __bf16 Vs[2][3][kHd][kAttnPad];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int qb, h, zs;
     xcd_tile(qb, h, zs);
@@ -567,18 +568,21 @@ __global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float
                 pv[u] = *(const u32x4*)(vb + (((long)p * kHeads + h) * kHd + row) * kmax + c0 + 8 * seg);
         }
     };
-    load(0);
-    for (int c0 = 0; c0 < nkeys; c0 += kAttnKeys) {
-        __syncthreads();  // previous chunk consumed
+    auto stash = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < kUnits; ++u) {
             const int e = tid + kAttnThreads * u;
             const int p = e / (kAttnKeys * 8), row = (e / 8) % kAttnKeys, seg = e % 8;
-            *(u32x4*)&Ks[p][row][8 * seg] = pk[u];
-            *(u32x4*)&Vs[p][row][8 * seg] = pv[u];
+            *(u32x4*)&Ks[buf][p][row][8 * seg] = pk[u];
+            *(u32x4*)&Vs[buf][p][row][8 * seg] = pv[u];
         }
-        __syncthreads();
-        if (c0 + kAttnKeys < nkeys) load(c0 + kAttnKeys);
+    };
+    load(0);
+    stash(0);
+    __syncthreads();
+    for (int c0 = 0, buf = 0; c0 < nkeys; c0 += kAttnKeys, buf ^= 1) {
+        const bool more = c0 + kAttnKeys < nkeys;
+        if (more) load(c0 + kAttnKeys);
         // S^T = K Q^T / 8 for 64 keys (4 tiles of 16) x the wave's query tiles
         f32x4_t s4[kAttnQT][4];
 #pragma unroll
@@ -587,9 +591,9 @@ __global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float
             for (int qt = 0; qt < kAttnQT; ++qt) s4[qt][t] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const bf16x8 k0 = *(const bf16x8*)&Ks[0][16 * t + lr][32 * s + 8 * lq];
-                const bf16x8 k1 = *(const bf16x8*)&Ks[1][16 * t + lr][32 * s + 8 * lq];
-                const bf16x8 k2 = *(const bf16x8*)&Ks[2][16 * t + lr][32 * s + 8 * lq];
+                const bf16x8 k0 = *(const bf16x8*)&Ks[buf][0][16 * t + lr][32 * s + 8 * lq];
+                const bf16x8 k1 = *(const bf16x8*)&Ks[buf][1][16 * t + lr][32 * s + 8 * lq];
+                const bf16x8 k2 = *(const bf16x8*)&Ks[buf][2][16 * t + lr][32 * s + 8 * lq];
 #pragma unroll
                 for (int qt = 0; qt < kAttnQT; ++qt) {
                     f32x4_t acc = s4[qt][t];
@@ -649,8 +653,8 @@ __global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float
                 bf16x8 v[3];
 #pragma unroll
                 for (int pl = 0; pl < 3; ++pl) {
-                    const bf16x4 a = *(const bf16x4*)&Vs[pl][16 * u + lr][32 * s + 4 * lq];
-                    const bf16x4 b = *(const bf16x4*)&Vs[pl][16 * u + lr][32 * s + 16 + 4 * lq];
+                    const bf16x4 a = *(const bf16x4*)&Vs[buf][pl][16 * u + lr][32 * s + 4 * lq];
+                    const bf16x4 b = *(const bf16x4*)&Vs[buf][pl][16 * u + lr][32 * s + 16 + 4 * lq];
                     v[pl] = bf16x8{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
                 }
 #pragma unroll
@@ -666,6 +670,8 @@ __global__ __launch_bounds__(kAttnThreads) void sg_attention3_kernel(const float
                 }
             }
         }
+        if (more) stash(buf ^ 1);  // the other buffer's last readers passed the previous barrier
+        __syncthreads();
     }
     float* ob = out + (long)zs * kmax * 256 + h * kHd;
 #pragma unroll
