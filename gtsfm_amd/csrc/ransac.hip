@@ -1444,6 +1444,36 @@ __global__ __launch_bounds__(64, 2) void ransac_solve2_kernel(const int* __restr
     RPROF(12);
 }
 
+// Pair order for the one-workgroup-per-pair launches (score, refine): pairs by putative count, largest first
+// (counting sort on 1024 count bins; order within a bin unspecified), so the longest workgroups start first and the
+// launch does not end on a large pair dispatched last. Outputs do not depend on the order.
+constexpr int kOrderBins = 1024;
+__global__ __launch_bounds__(kOrderBins) void pair_order_kernel(const int* __restrict__ match_count, int n_pairs,
+                                                                 int mcap, int* __restrict__ order) {
+    __shared__ int cnt[kOrderBins];
+    int shift = 0;
+    while ((mcap >> shift) >= kOrderBins) ++shift;
+    const int tid = threadIdx.x;
+    cnt[tid] = 0;
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += kOrderBins)
+        atomicAdd(&cnt[kOrderBins - 1 - (min(max(match_count[p], 0), mcap) >> shift)], 1);  // descending
+    __syncthreads();
+    // inclusive scan (Hillis-Steele), then exclusive starts
+    for (int d = 1; d < kOrderBins; d <<= 1) {
+        const int v = tid >= d ? cnt[tid - d] : 0;
+        __syncthreads();
+        cnt[tid] += v;
+        __syncthreads();
+    }
+    const int start = tid ? cnt[tid - 1] : 0;
+    __syncthreads();
+    cnt[tid] = start;
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += kOrderBins)
+        order[atomicAdd(&cnt[kOrderBins - 1 - (min(max(match_count[p], 0), mcap) >> shift)], 1)] = p;
+}
+
 // Scoring, one workgroup of kScoreThreads lanes per active pair and launch, LANE PER CANDIDATE: the candidates of the
 // launch's chunks (flattened in (hypothesis, solution) order, the oracle's scan order) are dealt to the lanes, and
 // every lane walks all putatives of its own candidate in index order, reading each putative as one broadcast LDS
@@ -1472,13 +1502,14 @@ __global__ __launch_bounds__(kScoreThreads) void ransac_score_kernel(const int* 
                                                                     const double* __restrict__ cand,
                                                                     const int* __restrict__ nsol, int n_chunks,
                                                                     const int* __restrict__ bound_tab,
-                                                                    PairState* __restrict__ st) {
+                                                                    PairState* __restrict__ st,
+                                                                    const int* __restrict__ order) {
     extern __shared__ float4 spts[];  // [M]
     __shared__ int flat_off[kMaxHyp + 1];       // candidates of the launch's hypotheses < h
     __shared__ uint16_t hyp_of[kMaxCand];       // flat candidate -> hypothesis slot of the launch
     __shared__ int chunk_tot[kMaxGroups];
     __shared__ unsigned long long chunk_min[kMaxGroups], pref[kMaxGroups];
-    const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int p = order[blockIdx.x], tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int M = match_count[p];
     if (M < 6) return;
     int best = st[p].best, best_h = st[p].best_h, best_s = st[p].best_s, done = st[p].done, niters = st[p].niters;
@@ -1757,11 +1788,11 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
                                                            int msac, RansacOutputs out,
                                                            const PairState* __restrict__ st,
                                                            unsigned char* __restrict__ gc_scratch,
-                                                           size_t gc_stride) {
+                                                           size_t gc_stride, const int* __restrict__ order) {
     __shared__ double jac_a[81], jac_v[81];
     __shared__ unsigned long long gc_keys_lds[kGcLdsKeys];
     __shared__ uint8_t gc_lab_lds[kGcLdsKeys];
-    const int p = blockIdx.x;
+    const int p = order[blockIdx.x];
     const int lane = threadIdx.x;
     const int M = match_count[p];
     uint8_t* mask = out.mask + (size_t)p * mcap;
@@ -1954,7 +1985,8 @@ static size_t ransac_layout(int n_pairs, int mcap, size_t* off_x2, size_t* off_p
     o += gtsfm_align_up((size_t)n_pairs * kMaxHyp * sizeof(int), 256);
     *off_stage = o;
     o += gtsfm_align_up((size_t)n_pairs * kStageVals * kMaxHyp * sizeof(double), 256);
-    o += gtsfm_align_up((size_t)n_pairs * (mcap + 1) * sizeof(int), 256);  // bound table (last)
+    o += gtsfm_align_up((size_t)n_pairs * (mcap + 1) * sizeof(int), 256);  // bound table
+    o += gtsfm_align_up((size_t)n_pairs * sizeof(int), 256);               // pair order (last)
     return o;
 }
 
@@ -2005,11 +2037,13 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     int* nsol = (int*)(ws + o_nsol);
     double* stage = (double*)(ws + o_stage);
     int* bound_tab = (int*)(ws + o_stage + gtsfm_align_up((size_t)n_pairs * kStageVals * kMaxHyp * sizeof(double), 256));
+    int* order = bound_tab + gtsfm_align_up((size_t)n_pairs * (mcap + 1) * sizeof(int), 256) / sizeof(int);
     hipLaunchKernelGGL(ransac_bound_table_kernel, dim3((mcap + 1 + 255) / 256, n_pairs), dim3(256), 0, stream,
                        d_match_count, mcap, prob, bound_tab);
     hipLaunchKernelGGL(normalize_putatives_kernel, dim3((mcap + 255) / 256, n_pairs), dim3(256), 0, stream, d_kp_xy,
                        d_intrinsics, kmax, d_pairs, d_match_idx, d_match_count, mcap, x1n, x2n, pts);
     hipLaunchKernelGGL(ransac_init_kernel, dim3((n_pairs + 255) / 256), dim3(256), 0, stream, st, n_pairs, max_iters);
+    hipLaunchKernelGGL(pair_order_kernel, dim3(1), dim3(kOrderBins), 0, stream, d_match_count, n_pairs, mcap, order);
     GTSFM_CHECK_HIP(hipGetLastError());
     GTSFM_CHECK_HIP(gtsfm_set_dynamic_lds((const void*)ransac_solve1_kernel, (int)kSolveLds));
     // the score kernel stages a pair's putatives in LDS when they fit (16 B each, up to 136 KiB beside its tables)
@@ -2020,7 +2054,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     // lanes idle while each walks many putatives
     const bool wide = (size_t)n_pairs * 272 < (size_t)64 * 1024 * 2 && mcap >= 256;
     using ScoreFn = void (*)(const int*, const double*, const int*, int, const float4*, double, double, const double*,
-                             const int*, int, const int*, PairState*);
+                             const int*, int, const int*, PairState*, const int*);
     ScoreFn score_fn;
     if (wide)
         score_fn = score_in_lds ? (msac ? ransac_score_kernel<true, true, 16> : ransac_score_kernel<true, false, 16>)
@@ -2045,7 +2079,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
         hipLaunchKernelGGL(ransac_solve2_kernel, dim3(n_pairs, g), dim3(64), kRootLds, stream, d_match_count, st,
                            stage, cand, nsol);
         hipLaunchKernelGGL(score_fn, dim3(n_pairs), dim3(kScoreThreads), score_lds, stream, d_pairs, d_intrinsics,
-                           d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st);
+                           d_match_count, mcap, pts, thr_px, prob, cand, nsol, g, bound_tab, st, order);
     }
     GTSFM_CHECK_HIP(hipGetLastError());
     const RansacOutputs o{d_E, d_R, d_t, d_n_inliers, d_status, d_n_hyp, d_inlier_mask, d_n_models};
@@ -2053,7 +2087,7 @@ int gtsfm_ransac_E_batched(const float* d_kp_xy, const double* d_intrinsics, int
     static_assert((size_t)kStageVals * kMaxHyp * sizeof(double) >= (size_t)kGcMaxM * 9, "GC scratch fits the stage");
     hipLaunchKernelGGL(ransac_refine_kernel, dim3(n_pairs), dim3(64), 0, stream, d_pairs, d_intrinsics, d_match_count,
                        mcap, x1n, x2n, pts, thr_px, msac ? 1 : 0, o, st, (unsigned char*)stage,
-                       (size_t)kStageVals * kMaxHyp * sizeof(double));
+                       (size_t)kStageVals * kMaxHyp * sizeof(double), order);
     GTSFM_CHECK_HIP(hipGetLastError());
     return GTSFM_OK;
 }
