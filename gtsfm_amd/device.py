@@ -165,14 +165,14 @@ def ransac_essential(kp_xy: torch.Tensor, intrinsics: torch.Tensor, pairs: torch
     mcap = match_idx.shape[1]
     dev = kp_xy.device
     L = native.lib()
-    E = torch.zeros((max(P, 1), 3, 3), dtype=torch.float64, device=dev)
-    R = torch.zeros_like(E)
-    t = torch.zeros((max(P, 1), 3), dtype=torch.float64, device=dev)
-    n_inl = torch.zeros((max(P, 1),), dtype=torch.int32, device=dev)
-    status = torch.zeros_like(n_inl)
-    n_hyp = torch.zeros_like(n_inl)
-    n_models = torch.zeros_like(n_inl)
-    mask = torch.zeros((max(P, 1), max(mcap, 1)), dtype=torch.uint8, device=dev)
+    # outputs carved from two zeroed buffers (one fill each instead of one per output; pairs the verifier rejects keep
+    # zero E / R / t, as do the mask entries past a pair's match count)
+    P1 = max(P, 1)
+    f64 = torch.zeros(21 * P1, dtype=torch.float64, device=dev)
+    E, R, t = f64[:9 * P1].view(P1, 3, 3), f64[9 * P1:18 * P1].view(P1, 3, 3), f64[18 * P1:].view(P1, 3)
+    i32 = torch.zeros(4 * P1, dtype=torch.int32, device=dev)
+    n_inl, status, n_hyp, n_models = (i32[j * P1:(j + 1) * P1] for j in range(4))
+    mask = torch.zeros((P1, max(mcap, 1)), dtype=torch.uint8, device=dev)
     if P > 0:
         ws = _workspace(L.gtsfm_ransac_workspace_bytes(P, mcap), dev)
         if stream is not None:
