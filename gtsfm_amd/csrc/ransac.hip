@@ -1488,7 +1488,9 @@ __global__ __launch_bounds__(kOrderBins) void pair_order_kernel(const int* __res
 // all lanes finish, thread 0 walks the chunks in order exactly like the oracle's batch loop
 // (oracle/ransac.c:679-706): best = min(best, chunk minimum), the iteration bound from the best count, done += 64,
 // stop once done >= niters (chunks past that point were solved speculatively and are discarded).
-constexpr int kScoreThreads = 512;  // measured 64 / 128 / 256 / 512: 11.9 / 9.1 / 7.8 / 7.4 ms C2 verify
+// measured 64 / 128 / 256 / 512: 11.9 / 9.1 / 7.8 / 7.4 ms C2 verify; with largest-first pairs 256 / 512 / 1024:
+// 360 / 284 / 318 us per C2 launch (profiles/r05_late_ablations/r05cc_*)
+constexpr int kScoreThreads = 512;
 constexpr int kMaxCand = kMaxHyp * kMaxSol;  // candidates one launch may hold per pair (13 bits of the key)
 static_assert(kMaxCand < (1 << 13), "flat candidate index must fit the key's 13 bits");
 constexpr int kKeyCountBits = 19;
