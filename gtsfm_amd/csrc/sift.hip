@@ -1278,7 +1278,13 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
     const int lane = threadIdx.x;
     for (int slot = blockIdx.x; slot < n_img * max_kpts; slot += gridDim.x) {
         const int img = slot / max_kpts, q = slot % max_kpts;
-        if (q >= n_sel[img]) continue;  // uniform per block
+        if (q >= n_sel[img]) {  // uniform per block: a padding row, zeroed here (no memset of the outputs)
+            const size_t row = (size_t)img * max_kpts + q;
+            for (int k = lane; k < 128; k += 64) out_desc[row * 128 + k] = 0.f;
+            if (lane < 2) out_xy[row * 2 + lane] = 0.f;
+            if (lane < 3) out_attr[row * 3 + lane] = 0.f;
+            continue;
+        }
         const KeyRec kp = kps[(size_t)img * kp_cap + sel[(size_t)img * max_kpts + q]];
         for (int i = lane; i < kCopies * HBP; i += 64) hist[i] = 0ull;
         __syncthreads();
@@ -1589,9 +1595,7 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
                                    stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(ws + L.seen, 0, L.seen_bytes, stream));
     GTSFM_CHECK_HIP(hipMemsetAsync(d_counts, 0, (size_t)B * sizeof(int), stream));
-    GTSFM_CHECK_HIP(hipMemsetAsync(d_xy, 0, (size_t)B * max_kpts * 2 * sizeof(float), stream));
-    GTSFM_CHECK_HIP(hipMemsetAsync(d_attr, 0, (size_t)B * max_kpts * 3 * sizeof(float), stream));
-    GTSFM_CHECK_HIP(hipMemsetAsync(d_desc, 0, (size_t)B * max_kpts * 128 * sizeof(float), stream));
+    // d_xy / d_attr / d_desc: every row is written by descriptor_kernel (padding rows as zeros)
 
     for (int i = 0; i < kLevels; ++i)
         if (taps[i].r < 1 || taps[i].r > kBlurMaxR) return GTSFM_ERR_ARG;
