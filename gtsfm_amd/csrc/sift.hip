@@ -474,9 +474,10 @@ __global__ __launch_bounds__(64 * kStreamWaves) void blur_stream_kernel(const fl
         const float* img = src + (size_t)b * H * W;
         // global_load_lds_dword (saddr form: scalar row base, the lane's byte offset), issued by inline asm: the compiler's
         // own LDS-DMA tracking would wait for every chunk in flight before each chunk's LDS accesses; the waits here are
-        // explicit. 16 load instructions per chunk, always issued (chunks past the segment reload valid rows). The asm
-        // sets M0 itself; the compiler keeps nothing else in M0 in this kernel (every m0 in its ISA is one of these
-        // statements), which is what the clobber warning asks to check.
+        // explicit. 16 load instructions per chunk, always issued (chunks past the segment reload valid rows). The LDS
+        // address goes in as an M0 operand ("{m0}" constraint): the compiler writes M0 itself and knows the asm reads
+        // it, so no register it keeps live can alias M0 (tests/test_build_isa.py checks the built code object); the
+        // s_nop covers the M0-write -> LDS-DMA hazard.
         auto issue = [&](int c) {
             const uint32_t d = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(ring + (c % kStreamBufs) * CH));
@@ -485,12 +486,10 @@ __global__ __launch_bounds__(64 * kStreamWaves) void blur_stream_kernel(const fl
             for (int r = 0; r < 8; ++r) {
                 const float* row = img + (size_t)reflect101(r0 + r, H) * W;
                 const uint32_t la = d + 4u * r * IWP;
-                asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(oa), "s"(row), "s"(la)
-                             : "memory", "m0");
+                asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(oa), "s"(row), "{m0}"(la) : "memory");
                 if (lane < IW - kBlurTX)
-                    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(ob), "s"(row),
-                                 "s"(la + 4u * kBlurTX)
-                                 : "memory", "m0");
+                    asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(ob), "s"(row), "{m0}"(la + 4u * kBlurTX)
+                                 : "memory");
             }
         };
         float win[8 * M];  // chunk c's column values at win[8 (c mod M) ..]

@@ -35,12 +35,27 @@ class DetectorDescriptorCacher(DetectorDescriptorBase):
         key = "{}_{}".format(self._detector_descriptor_obj_cache_key, cache_utils.generate_hash_for_image(image))
         return self._cache_root / "detector_descriptor" / f"{key}.pbz2"
 
+    @property
+    def wrapped(self) -> DetectorDescriptorBase:
+        """The detector-descriptor whose results are cached (the batched generator runs its misses on the device)."""
+        return self._detector_descriptor
+
+    def cache_lookup(self, image: Image) -> Optional[Tuple[Keypoints, np.ndarray]]:
+        """The cached (keypoints, descriptors) of `image`, or None on a miss (:58-63)."""
+        cached = io_utils.read_from_bz2_file(self._cache_path(image))
+        if cached is None:
+            return None
+        return cached["keypoints"], cached["descriptors"]
+
+    def cache_store(self, image: Image, keypoints: Keypoints, descriptors: np.ndarray) -> None:
+        """Writes the entry under the reference's key and payload (:65-69)."""
+        io_utils.write_to_bz2_file({"keypoints": keypoints, "descriptors": descriptors}, self._cache_path(image))
+
     def detect_and_describe(self, image: Image) -> Tuple[Keypoints, np.ndarray]:
-        """Cached `detect_and_describe` of the wrapped object (:69-95)."""
-        path = self._cache_path(image)
-        cached = io_utils.read_from_bz2_file(path)
+        """Cached `detect_and_describe` of the wrapped object (:71-95)."""
+        cached = self.cache_lookup(image)
         if cached is not None:
-            return cached["keypoints"], cached["descriptors"]
+            return cached
         keypoints, descriptors = self._detector_descriptor.detect_and_describe(image)
-        io_utils.write_to_bz2_file({"keypoints": keypoints, "descriptors": descriptors}, path)
+        self.cache_store(image, keypoints, descriptors)
         return keypoints, descriptors

@@ -48,13 +48,24 @@ class MatcherCacher(MatcherBase):
     def __repr__(self) -> str:
         return f"MatcherCacher({self._matcher!r})"
 
+    @property
+    def wrapped(self) -> MatcherBase:
+        """The matcher whose results are cached (the batched generator runs its misses on the device)."""
+        return self._matcher
+
+    def cache_path(self, keypoints_i1: Keypoints, keypoints_i2: Keypoints, descriptors_i1: np.ndarray,
+                   descriptors_i2: np.ndarray, im_shape_i1: Tuple[int, int, int],
+                   im_shape_i2: Tuple[int, int, int]) -> Path:
+        """`cache/matcher/{key}.pbz2` (:82-84). Only the first 10 descriptor rows of each image enter the key."""
+        key = matcher_cache_key(self._matcher_obj_key, keypoints_i1, keypoints_i2, descriptors_i1, descriptors_i2,
+                                im_shape_i1, im_shape_i2)
+        return self._cache_root / "matcher" / f"{key}.pbz2"
+
     def match(self, keypoints_i1: Keypoints, keypoints_i2: Keypoints, descriptors_i1: np.ndarray,
               descriptors_i2: np.ndarray, im_shape_i1: Tuple[int, int, int],
               im_shape_i2: Tuple[int, int, int]) -> np.ndarray:
         """Cached `match` of the wrapped object (:126-192)."""
-        key = matcher_cache_key(self._matcher_obj_key, keypoints_i1, keypoints_i2, descriptors_i1, descriptors_i2,
-                                im_shape_i1, im_shape_i2)
-        path = self._cache_root / "matcher" / f"{key}.pbz2"
+        path = self.cache_path(keypoints_i1, keypoints_i2, descriptors_i1, descriptors_i2, im_shape_i1, im_shape_i2)
         cached = io_utils.read_from_bz2_file(path)
         if cached is not None:
             return cached

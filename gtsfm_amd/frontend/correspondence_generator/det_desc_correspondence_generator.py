@@ -13,7 +13,12 @@ batched matcher launch per chunk of pairs:
 - SIFTDetectorDescriptor + TwoWayMatcher (configs C1, C2, C4): the exact-integer fp16 MFMA distance GEMM;
 - SuperPointDetectorDescriptor + TwoWayMatcher (config C3): the F16_RERANK matcher on the float descriptors;
 - SuperPointDetectorDescriptor + SuperGlueMatcher (config C5): batched SuperGlue (superglue.hip).
-Any other combination (e.g. cacher-wrapped plugins) runs its own per-call methods in the reference's order.
+The reference's shipped configs wrap both plugins in caches (sift_front_end.yaml:23-33: DetectorDescriptorCacher
+around SIFT, MatcherCacher around TwoWayMatcher). Those wrappers are looked through: every image and pair is first
+answered from the cache directory under the reference's keys (detector_descriptor_cacher.py:58-69,
+matcher_cacher.py:82-192), and only the misses go through the batched launches above; their results are written back
+under the same keys and payloads, exactly what the per-call cachers would have written. Any other combination runs
+its own per-call methods in the reference's order.
 """
 from __future__ import annotations
 
@@ -25,6 +30,8 @@ import torch
 from gtsfm_amd import device, native
 from gtsfm_amd.common.image import Image
 from gtsfm_amd.common.keypoints import Keypoints
+from gtsfm_amd.frontend.cacher.detector_descriptor_cacher import DetectorDescriptorCacher
+from gtsfm_amd.frontend.cacher.matcher_cacher import MatcherCacher
 from gtsfm_amd.frontend.correspondence_generator.correspondence_generator_base import CorrespondenceGeneratorBase
 from gtsfm_amd.frontend.detector_descriptor.detector_descriptor_base import DetectorDescriptorBase
 from gtsfm_amd.frontend.detector_descriptor.sift import SIFTDetectorDescriptor, extract_group, sift_groups
@@ -32,6 +39,7 @@ from gtsfm_amd.frontend.matcher.matcher_base import MatcherBase
 from gtsfm_amd.frontend.detector_descriptor.superpoint import SuperPointDetectorDescriptor
 from gtsfm_amd.frontend.matcher.superglue_matcher import MATCH_THRESHOLD, SuperGlueMatcher
 from gtsfm_amd.frontend.matcher.twoway_matcher import MatchingDistanceType, TwoWayMatcher
+import gtsfm_amd.utils.io as io_utils
 
 PAIR_CHUNK = 8192  # pairs per matcher launch: (chunk, k, 2) int32 indices = 128 MiB at k = 2048
 
@@ -165,6 +173,60 @@ def superglue_pairs_batched(matcher: SuperGlueMatcher, feats: DeviceFeatures, im
     return out
 
 
+def features_from_host(entries: Sequence[Tuple[Keypoints, np.ndarray]], kmin: int, dim: int,
+                       with_scores: bool) -> DeviceFeatures:
+    """Host (keypoints, descriptors) per image -> one padded device block (cache hits enter the batched path here)."""
+    n = len(entries)
+    k = max([kmin] + [len(kp) for kp, _ in entries])
+    xy = np.zeros((n, k, 2), np.float32)
+    desc = np.zeros((n, k, dim), np.float32)
+    sc = np.zeros((n, k), np.float32)
+    count = np.zeros((n,), np.int32)
+    for i, (kp, d) in enumerate(entries):
+        m = len(kp)
+        d = np.asarray(d).reshape(m, -1) if m else np.zeros((0, dim), np.float32)
+        if m and d.shape[1] != dim:
+            raise ValueError(f"cached descriptors have {d.shape[1]} dims, the detector gives {dim}")
+        count[i] = m
+        xy[i, :m] = kp.coordinates
+        desc[i, :m] = d
+        if with_scores and kp.responses is not None:
+            sc[i, :m] = kp.responses
+    dev = torch.device("cuda")
+    out = DeviceFeatures(torch.from_numpy(xy).to(dev), torch.from_numpy(desc).to(dev), torch.from_numpy(count).to(dev),
+                         [kp for kp, _ in entries])
+    if with_scores:
+        out.scores = torch.from_numpy(sc).to(dev)
+    return out
+
+
+def merge_features(parts: Sequence[Tuple[List[int], DeviceFeatures]], n: int) -> DeviceFeatures:
+    """Scatters per-subset device blocks (e.g. cache hits and batched misses) into one block over all n images."""
+    k = max(f.desc.shape[1] for _, f in parts)
+    dim = parts[0][1].desc.shape[2]
+    dev = parts[0][1].desc.device
+    with_scores = all(hasattr(f, "scores") for _, f in parts)
+    xy = torch.zeros((n, k, 2), dtype=torch.float32, device=dev)
+    desc = torch.zeros((n, k, dim), dtype=torch.float32, device=dev)
+    count = torch.zeros((n,), dtype=torch.int32, device=dev)
+    sc = torch.zeros((n, k), dtype=torch.float32, device=dev) if with_scores else None
+    kps: List[Optional[Keypoints]] = [None] * n
+    for idx, f in parts:
+        if not idx:
+            continue
+        sel = torch.tensor(idx, dtype=torch.long, device=dev)
+        kk = f.desc.shape[1]
+        xy[sel, :kk], desc[sel, :kk], count[sel] = f.xy, f.desc, f.count
+        if sc is not None:
+            sc[sel, :kk] = f.scores
+        for j, i in enumerate(idx):
+            kps[i] = f.keypoints[j]
+    out = DeviceFeatures(xy, desc, count, kps)  # type: ignore[arg-type]
+    if sc is not None:
+        out.scores = sc
+    return out
+
+
 class DetDescCorrespondenceGenerator(CorrespondenceGeneratorBase):
     """Traditional detect -> describe -> match, batched on the device when the plugins are the HIP ones."""
 
@@ -176,10 +238,18 @@ class DetDescCorrespondenceGenerator(CorrespondenceGeneratorBase):
     def __repr__(self) -> str:
         return f"DetDescCorrespondenceGenerator:\n   {self._detector_descriptor}\n   {self._matcher}\n"
 
+    def _plugins(self):
+        """(detector, detector cache or None, matcher, matcher cache or None): the reference configs' cachers are
+        looked through so that the plugins they wrap can run batched."""
+        d, m = self._detector_descriptor, self._matcher
+        dc = d if type(d) is DetectorDescriptorCacher else None
+        mc = m if type(m) is MatcherCacher else None
+        return (dc.wrapped if dc else d), dc, (mc.wrapped if mc else m), mc
+
     def _batched(self) -> Optional[str]:
         """Which batched device path serves this plugin pair: 'sift', 'superpoint_twoway', 'superpoint_superglue',
         or None (per-call)."""
-        d, m = self._detector_descriptor, self._matcher
+        d, _, m, _ = self._plugins()
         twoway_l2 = type(m) is TwoWayMatcher and m._distance_type is MatchingDistanceType.EUCLIDEAN
         if type(d) is SIFTDetectorDescriptor and twoway_l2:
             return "sift"
@@ -189,29 +259,104 @@ class DetDescCorrespondenceGenerator(CorrespondenceGeneratorBase):
             return "superpoint_superglue"
         return None
 
+    def _extract(self, path: str, imgs: List[Image]) -> Tuple[DeviceFeatures, List[np.ndarray]]:
+        """Batched extraction of every image that the detector cache (if any) does not hold; the first 10
+        descriptor rows of every image as the per-call path would hand them to the matcher cache's key."""
+        d, dc, _, _ = self._plugins()
+        sift = path == "sift"
+        extract = extract_sift_batched if sift else extract_superpoint_batched
+        if dc is None:
+            return extract(d, imgs), None
+        hit_idx, hit_entries, miss = [], [], []
+        for i, im in enumerate(imgs):
+            c = dc.cache_lookup(im)
+            if c is None:
+                miss.append(i)
+            else:
+                hit_idx.append(i)
+                hit_entries.append(c)
+        heads: List[np.ndarray] = [None] * len(imgs)  # type: ignore[list-item]
+        parts: List[Tuple[List[int], DeviceFeatures]] = []
+        if miss:
+            fm = extract(d, [imgs[i] for i in miss])
+            cnt = fm.count.cpu().numpy()
+            desc_h = fm.desc.cpu().numpy()
+            for j, i in enumerate(miss):
+                dj = desc_h[j, : cnt[j]].copy()  # exactly the per-call plugin's descriptors
+                dc.cache_store(imgs[i], fm.keypoints[j], dj)
+                heads[i] = dj[:10]
+            parts.append((miss, fm))
+        if hit_entries:
+            dim = 128 if sift else 256
+            parts.append((hit_idx, features_from_host(hit_entries, d.max_keypoints, dim, with_scores=not sift)))
+            for i, (_, dsc) in zip(hit_idx, hit_entries):
+                heads[i] = np.asarray(dsc)[:10]
+        if not hit_entries:
+            return parts[0][1], heads
+        feats = merge_features(parts, len(imgs))
+        feats.from_host = True
+        return feats, heads
+
+    def _match(self, path: str, feats: DeviceFeatures, imgs: List[Image], image_pairs: Sequence[Tuple[int, int]],
+               heads: Optional[List[np.ndarray]]) -> Dict[Tuple[int, int], np.ndarray]:
+        """Batched matching of every pair that the matcher cache (if any) does not hold; misses written back."""
+        _, _, m, mc = self._plugins()
+        if mc is not None and heads is None:
+            head = feats.desc[:, :10].cpu().numpy()
+            cnt = feats.count.cpu().numpy()
+            heads = [head[i, : min(10, cnt[i])] for i in range(len(imgs))]
+        pairs = [(int(a), int(b)) for a, b in image_pairs]
+        corr: Dict[Tuple[int, int], np.ndarray] = {}
+        paths = {}
+        todo = pairs
+        if mc is not None:
+            todo = []
+            for (i1, i2) in pairs:
+                p = mc.cache_path(feats.keypoints[i1], feats.keypoints[i2], heads[i1], heads[i2], imgs[i1].shape,
+                                  imgs[i2].shape)
+                c = io_utils.read_from_bz2_file(p)
+                if c is None:
+                    todo.append((i1, i2))
+                    paths[(i1, i2)] = p
+                else:
+                    corr[(i1, i2)] = c
+        if todo:
+            if path == "superpoint_superglue":
+                got = superglue_pairs_batched(m, feats, [im.value_array.shape for im in imgs], todo)
+            else:
+                got = match_pairs_batched(feats, todo, m._ratio_test_threshold, self._match_mode(path, feats))
+            for key in todo:
+                if mc is not None:
+                    io_utils.write_to_bz2_file(got[key], paths[key])
+                corr[key] = got[key]
+        return {key: corr[key] for key in pairs}
+
+    @staticmethod
+    def _match_mode(path: str, feats: DeviceFeatures) -> int:
+        if path != "sift":
+            # 256-D float descriptors: fp16 MFMA shortlist + certified exact re-rank (same matches as EXACT_F32)
+            return native.GTSFM_MATCH_F16_RERANK
+        if getattr(feats, "from_host", False):
+            # cache entries (e.g. OpenCV's descriptors written by the reference) are checked, not assumed, to be the
+            # small integers the exact fp16 path needs (TwoWayMatcher.select_match_mode's test); every mode gives
+            # the same matches, so one mode for the whole block is only a speed choice
+            d = feats.desc
+            ok = (d.shape[2] <= 139 and d.shape[1] <= 8192 and bool((d >= 0).all()) and bool((d <= 1023).all())
+                  and bool((d == torch.round(d)).all())
+                  and bool(((d.double() ** 2).sum(-1) < float(1 << 19)).all()))
+            return native.GTSFM_MATCH_INT_F16 if ok else native.GTSFM_MATCH_F16_RERANK
+        # HIP SIFT descriptors are integers in [0, 255] with |d|^2 < 2^19: the exact fp16 MFMA path applies
+        return native.GTSFM_MATCH_INT_F16
+
     def generate_correspondences(
         self, client, images: List, image_pairs: List[Tuple[int, int]]
     ) -> Tuple[List[Keypoints], Dict[Tuple[int, int], np.ndarray]]:
         imgs = [resolve(im) for im in images]
         path = self._batched()
-        if path == "sift":
-            feats = extract_sift_batched(self._detector_descriptor, imgs)
-            self.device_features = feats
-            # SIFT descriptors are integers in [0, 255] with |d|^2 < 2^19: the exact fp16 MFMA path applies
-            corr = match_pairs_batched(feats, image_pairs, self._matcher._ratio_test_threshold,
-                                       native.GTSFM_MATCH_INT_F16)
-            return feats.keypoints, corr
         if path is not None:
-            feats = extract_superpoint_batched(self._detector_descriptor, imgs)
+            feats, heads = self._extract(path, imgs)
             self.device_features = feats
-            if path == "superpoint_twoway":
-                # 256-D float descriptors: fp16 MFMA shortlist + certified exact re-rank (same matches as EXACT_F32)
-                corr = match_pairs_batched(feats, image_pairs, self._matcher._ratio_test_threshold,
-                                           native.GTSFM_MATCH_F16_RERANK)
-            else:
-                corr = superglue_pairs_batched(self._matcher, feats, [im.value_array.shape for im in imgs],
-                                               image_pairs)
-            return feats.keypoints, corr
+            return feats.keypoints, self._match(path, feats, imgs, image_pairs, heads)
         features = [self._detector_descriptor.detect_and_describe(im) for im in imgs]
         corr = {}
         for (i1, i2) in image_pairs:

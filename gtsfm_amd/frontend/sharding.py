@@ -101,17 +101,30 @@ def allgather_features(tensors: Sequence[torch.Tensor], n_per: int,
     exchange (optional): an EmulatedAllGather standing in for the collective (one process running one rank's share
     of a larger job on one GPU); the packing and unpacking around it are the real ones.
     """
-    if exchange is not None:
-        block, layout = pack_features(tensors, n_per, wire)
-        return unpack_features(exchange(block), layout)
-    world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
-    if world == 1:
-        return tuple(tensors)
+    if exchange is None:
+        world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
+        if world == 1:
+            return tuple(tensors)
+        exchange = CollectiveAllGather(group)
     block, layout = pack_features(tensors, n_per, wire)
-    off = block.numel()
-    g = torch.empty(world * off, dtype=torch.uint8, device=block.device)
-    torch.distributed.all_gather_into_tensor(g, block, group=group)
-    return unpack_features(g.view(world, off), layout)
+    return unpack_features(exchange(block), layout)
+
+
+class CollectiveAllGather:
+    """The exchange's collective: one all_gather_into_tensor of the packed per-rank blocks over the process group
+    (RCCL over xGMI under the "nccl" backend). allgather_features uses it for world > 1; passed explicitly as
+    `exchange`, it runs the collective at any world size, including 1 (tests/test_rccl_gpu.py drives the RCCL path
+    on a one-GPU box that way)."""
+
+    def __init__(self, group: Optional[torch.distributed.ProcessGroup] = None):
+        self.group = group
+
+    def __call__(self, block: torch.Tensor) -> torch.Tensor:
+        world = torch.distributed.get_world_size(self.group)
+        off = block.numel()
+        g = torch.empty(world * off, dtype=torch.uint8, device=block.device)
+        torch.distributed.all_gather_into_tensor(g, block, group=self.group)
+        return g.view(world, off)
 
 
 class EmulatedAllGather:

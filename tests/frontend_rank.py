@@ -7,6 +7,9 @@
                                                               rehearsal of the multi-rank engine); the exchange is the
                                                               engine's packing with the blocks gathered over gloo on
                                                               the host (RCCL refuses two ranks on one GPU)
+    python tests/frontend_rank.py rccl1 OUT_DIR N_IMG      -> an RCCL ("nccl") process group of world size 1 on cuda:0,
+                                                              formed before any other GPU call; the exchange forced
+                                                              through all_gather_into_tensor on device buffers
 """
 import json
 import os
@@ -53,7 +56,7 @@ class HostGlooAllGather:
         return g.view(world, block.numel()).to(block.device)
 
 
-def run_frontend_gpu(n_img: int, rank: int, world: int):
+def run_frontend_gpu(n_img: int, rank: int, world: int, exchange=None):
     from gtsfm_amd import synthetic
     from gtsfm_amd.frontend import sharding
     from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig
@@ -63,8 +66,39 @@ def run_frontend_gpu(n_img: int, rank: int, world: int):
     scene = synthetic.render_scene(ORBIT, GPU_H, GPU_W, device=str(dev), tex_size=1024, indices=mine)
     cfg = FrontEndConfig(kpts=GPU_KPTS, pair_chunk=4)
     fe = AllPairsFrontEnd(scene.images.cpu(), scene.intrinsics[:n_img], n_img, rank, world, dev, cfg,
-                          exchange=HostGlooAllGather() if world > 1 else None)
+                          exchange=exchange if exchange is not None else HostGlooAllGather() if world > 1 else None)
     return fe, fe.step()
+
+
+def run_rccl1(out_dir: str, n_img: int):
+    """World-size-1 RCCL group: the packed exchange through the collective (pack -> all_gather_into_tensor ->
+    unpack on device buffers), checked byte for byte here, then one engine step through it and one plain step."""
+    from gtsfm_amd.frontend import sharding
+
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", device_id=dev)  # before any other GPU call
+    try:
+        assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+        gen = torch.Generator().manual_seed(0)
+        xy = (torch.rand((3, 50, 2), generator=gen) * 1000).to(dev)
+        desc = torch.randint(0, 256, (3, 50, 128), generator=gen).float().to(dev)
+        cnt = torch.tensor([50, 7, 0], dtype=torch.int32, device=dev)
+        checks = {}
+        for n_per in (3, 5):  # exact and padded rank blocks
+            got = sharding.allgather_features([xy, desc, cnt], n_per, wire=[None, torch.uint8, None],
+                                              exchange=sharding.CollectiveAllGather())
+            for name, a, b in zip(("xy", "desc", "cnt"), (xy, desc, cnt), got):
+                assert b.device == dev and b.dtype == a.dtype and b.shape[0] == n_per, (name, b.shape)
+                checks[f"{name}_{n_per}"] = bool(torch.equal(b[:3], a)) and bool((b[3:] == 0).all())
+        torch.cuda.synchronize()
+        _, r_c = run_frontend_gpu(n_img, 0, 1, exchange=sharding.CollectiveAllGather())
+        save(os.path.join(out_dir, "rccl_collective.npz"), r_c)
+        _, r_p = run_frontend_gpu(n_img, 0, 1)
+        save(os.path.join(out_dir, "rccl_plain.npz"), r_p)
+        with open(os.path.join(out_dir, "rccl_checks.json"), "w") as f:
+            json.dump(checks, f)
+    finally:
+        dist.destroy_process_group()
 
 
 def save(path, r):
@@ -74,6 +108,9 @@ def save(path, r):
 
 def main():
     mode, out_dir = sys.argv[1], sys.argv[2]
+    if mode == "rccl1":
+        run_rccl1(out_dir, int(sys.argv[3]))
+        return
     if mode == "gpushared":
         rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
         dist.init_process_group("gloo")

@@ -53,3 +53,24 @@ def test_two_ranks_on_one_gpu_equal_one_rank(tmp_path, world, n_img):
             n = part["kp_count"][j]
             assert n == ref.kp_count[i] and np.array_equal(part["kp_xy"][j, :n], ref.kp_xy[i, :n])
     assert (ref.status == 0).sum() >= 3
+
+
+def test_rccl_exchange_world1_equals_plain_step(tmp_path):
+    """the `nccl` (RCCL) process group forms on cuda:0 (world size 1, before any other GPU call
+    in that process), the packed feature exchange runs through all_gather_into_tensor on device buffers and comes back
+    byte for byte, and one engine step through the collective equals the plain step (which skips the exchange at
+    world 1) in every result field."""
+    import json
+
+    from gtsfm_amd import native
+
+    native.require_gpu()
+    rc = launch.spawn_ranks(1, RANK_SCRIPT, ["rccl1", str(tmp_path), "4"])
+    assert rc == 0
+    checks = json.load(open(tmp_path / "rccl_checks.json"))
+    assert checks and all(checks.values()), checks
+    a, b = _load(tmp_path / "rccl_collective.npz"), _load(tmp_path / "rccl_plain.npz")
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert (a["status"] == 0).sum() >= 2
