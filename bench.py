@@ -27,6 +27,8 @@ Workloads:
       images, then all pairs through the same matcher.
   --config c5: a per-GPU slice of configs[4] -- SuperPoint (2048 kpts) + SuperGlue + 5-point RANSAC over all pairs
       of 32 rendered images (configs[4]'s 2000 images x 8 GPUs is ~2M SuperGlue pairs; --images sets the slice).
+  --config netvlad: SURVEY §8 f3 -- NetVLAD global descriptors of 64 rendered 1080p images + the retriever's
+      similarity / top-20 pairs (images/s; not a BASELINE config).
 Pairs and images are dealt round-robin over the ranks (pair p to rank p mod N, image i to rank i mod N).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1|c2|c2-weak|c4|c3-match|c3|c5] [--images n]
@@ -54,6 +56,7 @@ from gtsfm_amd import launch  # noqa: E402
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0  # HBM3E spec, MI355X_MICROARCH.md
 VALU_F32_PEAK_TFLOPS = 157.3  # vector fp32, MI355X_MICROARCH.md (SURVEY.md §8(d) grades RANSAC against it)
+VALU_F64_PEAK_TFLOPS = 78.6  # vector fp64, AMD's MI355X spec (half the fp32 vector rate; not in MI355X_MICROARCH.md)
 RATIO = 0.8
 THRESH_PX = 4.0
 MIN_INLIERS = 15
@@ -68,18 +71,25 @@ def images_for(n_gpus: int, base: int = 100) -> int:
     return n
 
 
-def pmc_traffic():
-    """HBM bytes per mnn_pp_kernel launch (the distance GEMM) from the committed rocprofv3 --pmc summary of this bench's command
-    (profiles/*_mnn_pmc.json, written by tools/pmc_summary.py --json): FETCH_SIZE doubled per MI355X_MICROARCH.md
-    (gfx950 tallies 128-B reads at 64 B) + WRITE_SIZE, in bytes. None when no summary is committed."""
+def pmc_traffic(config: str):
+    """HBM bytes per mnn_pp_kernel launch (the distance GEMM) of THIS config's bench command, from the latest committed
+    rocprofv3 --pmc summary for it (profiles/*_<config>_mnn_pmc.json, tools/gpu_pmc_mnn.sh TAG bench <config>;
+    for c2 also the untagged profiles/*_mnn_pmc.json of rounds 1-5, which were all taken on the c2 command):
+    FETCH_SIZE doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B) + WRITE_SIZE, in bytes.
+    None when no summary of this config is committed (never another config's figure)."""
     import glob
+    import re
 
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_mnn_pmc.json")))
+    files = glob.glob(os.path.join(REPO, "profiles", f"*_{config}_mnn_pmc.json"))
+    if config == "c2":
+        files += [f for f in glob.glob(os.path.join(REPO, "profiles", "*_mnn_pmc.json"))
+                  if re.fullmatch(r"r\d+[a-z]*_mnn_pmc\.json", os.path.basename(f))]
     if not files:
         return None
-    with open(files[-1]) as f:
+    latest = max(files, key=lambda f: os.path.basename(f).split("_")[0])
+    with open(latest) as f:
         d = json.load(f)
-    return float(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], REPO)
+    return float(d["hbm_bytes_per_launch"]), os.path.relpath(latest, REPO)
 
 
 def deep_pmc(config: str):
@@ -148,7 +158,8 @@ def cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, threads:
         what = (f"oracle (oracle/*.c, {threads} threads): SIFT of {len(sample)} of the {n_img} images, evenly spaced "
                 f"({t_sift_wall / len(sample) * 1e3:.0f} ms/img wall) + match+verify of {len(pairs)} pairs among them "
                 f"({t_pair_wall / len(pairs) * 1e3:.0f} ms/pair wall), scaled to {n_img} images / {P} pairs")
-    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port", "sample": what}
+    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads,
+            "kind": "port" if whole else "port, extrapolated", "sample": what}
 
 
 def sample_images(n_img: int, n_sift: int) -> np.ndarray:
@@ -184,7 +195,7 @@ def c3_cpu_baseline(desc: torch.Tensor, threads: int = 16, n_pairs: int = 16) ->
         t0 = time.time()
         list(pool.map(lambda p: oracle.twoway_match(h[p[0]], h[p[1]], RATIO), pairs))
         dt = time.time() - t0
-    return {"value": len(pairs) / dt, "unit": "matched image-pairs/s", "cores": threads, "kind": "port",
+    return {"value": len(pairs) / dt, "unit": "matched image-pairs/s", "cores": threads, "kind": "port, extrapolated",
             "sample": f"oracle twoway_match (oracle/twoway.c, {threads} threads), {len(pairs)} pairs of "
                       f"{h.shape[1]}x{h.shape[2]} descriptors, {dt:.1f} s wall"}
 
@@ -262,6 +273,103 @@ def main_c3(args, world, rank, dev):
 
 
 
+def vgg16_conv_flop(H: int, W: int) -> float:
+    """Multiply-add flop (2 per MAC) of VGG16 features[:-2] on an H x W image (13 conv3x3, pools floor)."""
+    layers = [(3, 64, 0), (64, 64, 1), (64, 128, 0), (128, 128, 1), (128, 256, 0), (256, 256, 0), (256, 256, 1),
+              (256, 512, 0), (512, 512, 0), (512, 512, 1), (512, 512, 0), (512, 512, 0), (512, 512, 0)]
+    h, w, total = H, W, 0.0
+    for cin, cout, pool in layers:
+        total += 2.0 * 9 * cin * cout * h * w
+        if pool:
+            h, w = h // 2, w // 2
+    return total
+
+
+def main_netvlad(args, world, rank, dev):
+    """SURVEY §8 row f3 (retrieval), the descriptor half: NetVLAD global descriptors (VGG16 + NetVLAD layer +
+    whitening, netvlad_global_descriptor.py / thirdparty/hloc/netvlad.py) of n rendered 1080p images resident in HBM,
+    then the NetVLAD retriever's similarity GEMM + top-k pairs (netvlad_retriever.py:77-228, num_matched 20, min_score
+    0.3 as sift_front_end.yaml). Seeded random weights (tests/netvlad_weights.py). Images dealt round-robin over ranks;
+    each rank describes its own images (replicas: no exchange is timed)."""
+    from gtsfm_amd import device as hip
+    from gtsfm_amd import native, synthetic
+    from gtsfm_amd.frontend.global_descriptor.netvlad_global_descriptor import WORKSPACE_BUDGET, pack_netvlad_weights
+    from gtsfm_amd.frontend import sharding
+
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from netvlad_weights import netvlad_state_dict
+
+    n_img = args.images or 64
+    H, W = args.height, args.width
+    mine = sharding.local_images(n_img, world, rank)
+    scene = synthetic.render_scene(n_img, H, W, device=str(dev), indices=mine)
+    imgs = scene.images.contiguous()
+    sd = netvlad_state_dict(0)
+    w = torch.from_numpy(pack_netvlad_weights(sd)).to(dev)
+    lib = native.lib()
+    per = int(lib.gtsfm_netvlad_workspace_bytes(1, H, W))
+    g = max(1, min(len(mine), WORKSPACE_BUDGET // per))
+    ws = torch.empty(int(lib.gtsfm_netvlad_workspace_bytes(g, H, W)), dtype=torch.uint8, device=dev)
+    out = torch.empty((len(mine), 4096), dtype=torch.float32, device=dev)
+
+    def step():
+        for s0 in range(0, len(mine), g):
+            d, _ = hip.netvlad_describe(imgs[s0: s0 + g], w, workspace=ws)
+            out[s0: s0 + g] = d
+        if world == 1:
+            sim = hip.retrieval_similarity(out, 50)
+            return hip.retrieval_pairs(sim, 20, 0.3)
+        return None
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_loop(step, args.steps, world, dev)
+    # the descriptor stage alone, timed with events on the compute stream
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for s0 in range(0, len(mine), g):
+        hip.netvlad_describe(imgs[s0: s0 + g], w, workspace=ws)
+    ev[1].record()
+    torch.cuda.synchronize()
+    desc_ms = ev[0].elapsed_time(ev[1])
+    flop = len(mine) * vgg16_conv_flop(H, W)
+    tf = flop / (desc_ms * 1e-3) / 1e12
+    split_peak = MFMA_F16_PEAK_TFLOPS / 6.0
+    value = n_img / (elapsed / args.steps)
+    out_line = {
+        "metric": "NetVLAD global descriptors + retrieval pairs, images/sec (f3)",
+        "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak" if world > 1 else "strong", "vs_baseline": None,
+        "dtype": "u8 image / fp32-accurate bf16x3-MFMA VGG16 / fp32 MFMA VLAD + whitening",
+        "data": "synthetic (rendered textured room); seeded random NetVLAD weights (tests/netvlad_weights.py)",
+        "config": {"workload": f"f3: {n_img} synthetic {W}x{H} images -> NetVLAD 4096-D descriptors -> "
+                               "similarity + top-20 pairs (min_score 0.3)", "images": n_img,
+                   "parallelism": f"images x{world}"},
+        "roofline": {"bound": "mfma", "achieved": round(tf, 1), "peak": round(split_peak, 1), "unit": "TFLOP/s",
+                     "frac": round(tf / split_peak, 4), "traffic": None, "kernel_ms": round(desc_ms, 3),
+                     "kernel": "NetVLAD descriptor launches (conv3_kernel x 12 + input conv + VLAD + whitening)",
+                     "work": "VGG16 features[:-2] conv flop %.1f GFLOP per image (2 per MAC) over %d images; convs "
+                             "as fp32-accurate bf16x3 split products (peak = dense bf16 MFMA / 6)"
+                             % (vgg16_conv_flop(H, W) / 1e9, len(mine))},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        from oracle import deep
+
+        torch.set_num_threads(16)
+        host = imgs[:2].cpu().numpy()
+        t0 = time.time()
+        for im in host:
+            deep.netvlad(im, sd)
+        dt = (time.time() - t0) / len(host)
+        out_line["cpu_baseline"] = {"value": round(1.0 / dt, 4), "unit": "images/s", "cores": 16,
+                                    "kind": "port, extrapolated",
+                                    "sample": f"oracle/deep.py netvlad (torch fp32, 16 threads) on 2 of the images: "
+                                              f"{dt:.2f} s/image"}
+    if rank == 0:
+        print(json.dumps(out_line), flush=True)
+
+
 def timed_loop(step, steps: int, world: int, dev) -> float:
     """Seconds for `steps` calls of step(): barrier + synchronize on both sides, max over ranks."""
     torch.cuda.synchronize()
@@ -304,6 +412,16 @@ def sift_bytes_per_image(H: int, W: int, kpts: int) -> float:
     """SURVEY.md §8(d) algorithmic bytes of SIFT extraction per image: 84 * sum_o P_o + H*W + K*(128*4 + 16), with
     sum_o P_o = 4HW * 4/3 (21 fp32 image passes per pyramid pixel over the 2x-upsampled octave pyramid)."""
     return 84.0 * (4.0 * H * W * 4.0 / 3.0) + H * W + kpts * (128 * 4 + 16)
+
+
+def sift_moved_bytes_per_image(H: int, W: int, kpts: int) -> float:
+    """Bytes the SIFT kernels actually move per image (beside §8(d)'s 84 B per pyramid pixel, which counts DoG
+    writes and reads that no kernel performs: DoG is formed in LDS / registers): the u8 RGB read and octave 0's base
+    level write (gray + 2x upsample + first blur fused), per octave pixel 5 level blurs read + written (40 B), the six
+    levels read by the extrema sweep (24 B) and the next octave's base written by the layer-3 blur (1 B per pixel of
+    this octave), plus the keypoint records and descriptors written."""
+    P = 4.0 * H * W * 4.0 / 3.0  # sum over octaves of the level pixel counts (octave 0 is the 2x-upsampled image)
+    return 3.0 * H * W + 4.0 * (4.0 * H * W) + 65.0 * P + kpts * (128 * 4 + 16)
 
 
 def lund_door_c1():
@@ -417,7 +535,7 @@ def deep_cpu_baseline(images, intrinsics: np.ndarray, n_img: int, kpts: int, sp_
     P = n_img * (n_img - 1) // 2
     total = n_img * t_img + P * t_pair
     what = ("SuperGlue (oracle/deep.py)" if sg_sd is not None else "TwoWayMatcher (oracle/twoway.c)")
-    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port",
+    return {"value": P / total, "unit": "verified image-pairs/sec", "cores": threads, "kind": "port, extrapolated",
             "sample": f"CPU restatement on {threads} threads: SuperPoint (oracle/deep.py, torch fp32) of "
                       f"{len(sample)} of the {n_img} images ({t_img:.2f} s/img), {what} + oracle RANSAC on the "
                       f"{len(pairs)} pairs among them ({t_pair:.2f} s/pair wall), scaled to {n_img} images / {P} pairs"}
@@ -576,13 +694,22 @@ def main_frontend(args, info, config: str):
     pl = pr[a_last:b_last]  # the kernel events end on the LAST pair chunk's launch: its pairs are that launch's work
     D = fe.desc_dim
     H_p, M_p, S_p = stats["n_hyp"], stats["n_matches"], stats["n_models"]
-    verify_flop = float((1.2e4 * H_p + 36.0 * M_p * S_p).sum().item())
+    solve_flop = float((1.2e4 * H_p).sum().item())  # 5-point solver, fp64 (ransac_solve1 / solve2)
+    score_flop = float((36.0 * M_p * S_p).sum().item())  # Sampson scoring, fp32 (ransac_score)
+    verify_flop = solve_flop + score_flop
     ex_ms, m_ms, ver_ms = (st_res.get(k, float("nan")) for k in ("extract", "match", "verify"))
     verify_tf = verify_flop / (ver_ms * 1e-3) / 1e12
-    verify_stage = {"bound": "valu", "achieved": round(verify_tf, 2), "peak": VALU_F32_PEAK_TFLOPS,
-                    "unit": "TFLOP/s", "frac": round(verify_tf / VALU_F32_PEAK_TFLOPS, 4), "ms": ver_ms,
-                    "work": "SURVEY 8(d): sum_p H_p*1.2e4 + 36*M_p*(models scored)_p; H mean %.1f, models/H %.2f"
-                            % (float(H_p.mean()), float(S_p.sum() / max(float(H_p.sum()), 1.0)))}
+    # each part against its own vector peak: the stage's time at peak is the sum of the two parts' times at peak
+    t_peak = solve_flop / (VALU_F64_PEAK_TFLOPS * 1e12) + score_flop / (VALU_F32_PEAK_TFLOPS * 1e12)
+    verify_stage = {"bound": "valu (fp64 solve + fp32 score)", "achieved": round(verify_tf, 2),
+                    "peak": round(verify_flop / t_peak / 1e12, 1) if t_peak > 0 else None,
+                    "unit": "TFLOP/s", "frac": round(t_peak / (ver_ms * 1e-3), 4) if ver_ms > 0 else None,
+                    "ms": ver_ms, "solve_gflop_fp64": round(solve_flop / 1e9, 2),
+                    "score_gflop_fp32": round(score_flop / 1e9, 2),
+                    "work": "SURVEY 8(d): sum_p H_p*1.2e4 (fp64, vs %.1f TF) + 36*M_p*(models scored)_p (fp32, vs %.1f "
+                            "TF); peak = the two parts' flop-weighted peak; H mean %.1f, models/H %.2f"
+                            % (VALU_F64_PEAK_TFLOPS, VALU_F32_PEAK_TFLOPS, float(H_p.mean()),
+                               float(S_p.sum() / max(float(H_p.sum()), 1.0)))}
     gemm_ms = float(np.median(kernel_ms))
     gemm_flop = float((2.0 * kc[pl[:, 0]] * kc[pl[:, 1]] * D).sum())
     gemm_flop_all = float((2.0 * kc[pr[:, 0]] * kc[pr[:, 1]] * D).sum())
@@ -590,11 +717,13 @@ def main_frontend(args, info, config: str):
     if not deep:
         extract_bytes = fe.n_local * sift_bytes_per_image(H, W, kpts)
         extract_gbs = extract_bytes / (ex_ms * 1e-3) / 1e9
+        moved_bytes = fe.n_local * sift_moved_bytes_per_image(H, W, kpts)
+        moved_gbs = moved_bytes / (ex_ms * 1e-3) / 1e9
         kpad = -(-kpts // 256) * 256
         # the last launch's operand images (both sides of its pairs) read once, its putatives written once
         n_launch_img = len(np.unique(pl))
         algo_bytes = 2 * n_launch_img * kpad * 144 * 2 + 2 * len(pl) * kpts * 8  # two fp16 forms, K = 144
-        traffic = pmc_traffic()
+        traffic = pmc_traffic(config)
         roof = {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(gemm_tf / MFMA_F16_PEAK_TFLOPS, 4), "traffic": traffic[0] if traffic else None,
                 "traffic_source": traffic[1] if traffic else None, "algorithmic_bytes": algo_bytes,
@@ -605,7 +734,11 @@ def main_frontend(args, info, config: str):
             "extract": {"bound": "hbm", "achieved": round(extract_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(extract_gbs / HBM_PEAK_GBS, 4), "ms": ex_ms,
                         "work": "SURVEY 8(d): 84*sum_o P_o + H*W + K*528 B/image = %.3f GB x %d images"
-                                % (sift_bytes_per_image(H, W, kpts) / 1e9, fe.n_local)},
+                                % (sift_bytes_per_image(H, W, kpts) / 1e9, fe.n_local),
+                        "moved_bytes": round(moved_bytes), "frac_moved": round(moved_gbs / HBM_PEAK_GBS, 4),
+                        "moved_note": "bytes the SIFT kernels actually move (%.3f GB/image: 3HW + 16HW + 65 B per "
+                                      "pyramid pixel + records; DoG is never written): %.1f GB/s"
+                                      % (sift_moved_bytes_per_image(H, W, kpts) / 1e9, moved_gbs)},
             "match": {"bound": "mfma", "achieved": round(gemm_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(gemm_tf / MFMA_F16_PEAK_TFLOPS, 4), "ms": round(gemm_ms, 3),
                       "work": "2*K1*K2*128 flop per pair (distance GEMM counted once)"},
@@ -744,7 +877,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ba", action="store_true",
                     help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c2-weak", "c4", "c3-match", "c3", "c5"])
+    ap.add_argument("--config", default="c2",
+                    choices=["c1", "c2", "c2-weak", "c4", "c3-match", "c3", "c5", "netvlad"])
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="run ONE rank's share of an N-rank job on this GPU (per-rank step time; not a scaling run)")
     ap.add_argument("--emulate-rank", type=int, default=0)
@@ -770,6 +904,8 @@ def main():
     try:
         if args.config == "c3-match":
             main_c3(args, info.world, info.rank, info.device)
+        elif args.config == "netvlad":
+            main_netvlad(args, info.world, info.rank, info.device)
         else:
             main_frontend(args, info, args.config)
     finally:

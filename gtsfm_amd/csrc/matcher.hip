@@ -25,6 +25,7 @@
 // LDS compaction and a bitonic sort on (distance, i1) — the reference's output order.
 #include "common.hpp"
 
+#include <atomic>
 #include <type_traits>
 
 namespace {
@@ -825,14 +826,19 @@ int pp_split(int n_groups, int kmax, int n_cu) {
     return best;
 }
 
+// CU count of the CURRENT device (cached per device id: a process may drive several GPUs)
 int device_cu_count() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
+    constexpr int kDevs = 64;
+    static std::atomic<int> cached[kDevs];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (dev >= 0 && dev < kDevs) {
+        const int c = cached[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
     }
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    if (dev >= 0 && dev < kDevs) cached[dev].store(n, std::memory_order_relaxed);
     return n;
 }
 

@@ -856,7 +856,6 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     };
     using S0 = std::integral_constant<int, 0>;
     using S1 = std::integral_constant<int, 1>;
-    using S2 = std::integral_constant<int, 2>;
     // rows y0-1 (slot 0) and y0 (slot 1) first; then row y0+1+3k+j goes to slot (2+j)%3 and completes the window of
     // row y0+3k+j, whose centre sits in slot (1+j)%3.
     // kExAhead rows' loads stay in flight: a row's buffer is refilled with the row kExAhead below as soon as it has
@@ -1599,13 +1598,12 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
     for (int i = 0; i < kLevels; ++i)
         if (taps[i].r < 1 || taps[i].r > kBlurMaxR) return GTSFM_ERR_ARG;
 
-    static int n_cu = 0;
-    if (n_cu == 0) {
-        int dev = 0, v = 0;
+    int n_cu = 0;
+    {
+        int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
             return GTSFM_ERR_HIP;
-        n_cu = v;
     }
     auto blur = [&](const float* src, float* dst, float* dec, int h, int w, const Taps& t) -> int {
         const bool u8 = src == nullptr;
@@ -1643,30 +1641,50 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
     // stream while the main stream goes on with octave o + 1's blurs: the latency-bound refinement and orientation
     // overlap the bandwidth-bound blurs. Octaves stay in order on the side stream (they share the candidate and
     // refinement buffers); the main stream joins it before the keypoints are gathered.
+    // The side stream and its events are per device and created once (under a lock). The call as a whole is not
+    // safe to run from two host threads on one device at once (they would share the side stream's events); callers
+    // serialise per device, as every caller in this package does.
     hipStream_t side = nullptr;
     hipEvent_t* ev = nullptr;
     {
+        static std::mutex mu;
         static hipStream_t sides[kMaxDevices] = {};
         static hipEvent_t evs[kMaxDevices][kMaxOct + 1] = {};
         int dev = 0;
         GTSFM_CHECK_HIP(hipGetDevice(&dev));
         if (dev < 0 || dev >= kMaxDevices) return GTSFM_ERR_ARG;
+        std::lock_guard<std::mutex> lock(mu);
         if (!sides[dev]) {
-            GTSFM_CHECK_HIP(hipStreamCreateWithFlags(&sides[dev], hipStreamNonBlocking));
+            hipStream_t st = nullptr;
+            GTSFM_CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
             for (int i = 0; i <= kMaxOct; ++i)
                 GTSFM_CHECK_HIP(hipEventCreateWithFlags(&evs[dev][i], hipEventDisableTiming));
+            sides[dev] = st;
         }
         side = sides[dev];
         ev = evs[dev];
     }
+    // an error inside the octave loop still joins the side stream's work to the caller's stream
+    auto join_side = [&]() {
+        if (hipEventRecord(ev[kMaxOct], side) == hipSuccess) (void)hipStreamWaitEvent(stream, ev[kMaxOct], 0);
+    };
     for (int o = 0; o < L.n_oct; ++o) {
         const int h = L.Ho[o], w = L.Wo[o];
         // octave o > 0 starts from the layer-3 level of octave o - 1, decimated by that level's blur launch
-        if (o == 0 && blur(nullptr, F(L.g[0][0]), nullptr, h, w, taps[0])) return GTSFM_ERR_HIP;
+        if (o == 0 && blur(nullptr, F(L.g[0][0]), nullptr, h, w, taps[0])) {
+            join_side();
+            return GTSFM_ERR_HIP;
+        }
         for (int i = 1; i < kLevels; ++i) {
             float* dec = (i == kLayers && o + 1 < L.n_oct) ? F(L.g[o + 1][0]) : nullptr;
-            if (dec && (L.Ho[o + 1] != h / 2 || L.Wo[o + 1] != w / 2)) return GTSFM_ERR_ARG;
-            if (blur(F(L.g[o][i - 1]), F(L.g[o][i]), dec, h, w, taps[i])) return GTSFM_ERR_HIP;
+            if (dec && (L.Ho[o + 1] != h / 2 || L.Wo[o + 1] != w / 2)) {
+                join_side();
+                return GTSFM_ERR_ARG;
+            }
+            if (blur(F(L.g[o][i - 1]), F(L.g[o][i]), dec, h, w, taps[i])) {
+                join_side();
+                return GTSFM_ERR_HIP;
+            }
         }
         GTSFM_CHECK_HIP(hipGetLastError());
         if (h <= 2 * kBorder || w <= 2 * kBorder) continue;

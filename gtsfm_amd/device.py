@@ -94,8 +94,9 @@ def _split_cost(n_groups: int, group_size: int, kmax: int, n_cu: int) -> float:
 def match_plan(pairs: np.ndarray, kmax: int, dim: int, n_cu: Optional[int] = None) -> Optional[np.ndarray]:
     """Pair groups for the INT_F16 distance GEMM (gtsfm_match_batched_grouped), sized to fill the GPU: the largest
     group size (most reuse of the register operand) is kept unless a smaller one, together with the library's pass
-    split, finishes in fewer estimated workgroup rounds. A rank's share of C2 at 8 GPUs (619 pairs) has ~155 groups of
-    4 for 256 CUs: groups of 1 split into 2 pass ranges (1238 workgroups) take 10 pair-passes of time instead of 16."""
+    split, finishes in fewer estimated workgroup rounds. A rank's share of C2 at 8 GPUs (~619 pairs dealt in whole
+    (i1, i2 // 4) runs, sharding.rank_pairs) has ~160 groups of 4 for 256 CUs: full groups of 2 split over pass ranges
+    take 10 pair-passes of time instead of 12."""
     gmax = match_group_size(kmax, dim)
     if gmax <= 1:
         return None
@@ -513,3 +514,32 @@ def retrieval_pairs(scores: torch.Tensor, num_select: int, min_score: Optional[f
                                                     _ptr(cnt), native.stream_handle(stream)),
                  "gtsfm_retrieval_pairs")
     return out, cnt
+
+
+def netvlad_describe(images: torch.Tensor, weights: torch.Tensor, whiten: bool = True,
+                     stream: Optional[torch.cuda.Stream] = None, workspace: Optional[torch.Tensor] = None,
+                     keep_vlad: bool = False) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """NetVLAD global descriptors of a batch of same-sized (n, H, W, 3) uint8 RGB images (gtsfm_netvlad_batched).
+
+    weights: the packed fp32 blob (gtsfm_amd.frontend.global_descriptor.netvlad_global_descriptor.pack_netvlad_weights).
+    Returns (desc (n, 4096) f32 or None when whiten is False, vlad (n, 32768) f32 or None unless keep_vlad or
+    not whiten): the whitened, L2-normalised descriptor and the NetVLADLayer output before whitening."""
+    assert images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous() and images.dim() == 4
+    assert images.shape[3] == 3, "NetVLAD takes RGB images (netvlad.py:172: image.shape[1] == 3)"
+    assert weights.is_cuda and weights.dtype == torch.float32 and weights.is_contiguous()
+    L = native.lib()
+    assert weights.numel() == L.gtsfm_netvlad_weights_floats()
+    n, H, W = images.shape[0], images.shape[1], images.shape[2]
+    dev = images.device
+    desc = torch.empty((n, 4096), dtype=torch.float32, device=dev) if whiten else None
+    vlad = torch.empty((n, 32768), dtype=torch.float32, device=dev) if (keep_vlad or not whiten) else None
+    if n == 0:
+        return desc, vlad
+    need = L.gtsfm_netvlad_workspace_bytes(n, H, W)
+    ws = workspace if workspace is not None and workspace.numel() >= need else _workspace(need, dev)
+    if stream is not None:
+        ws.record_stream(stream)
+    rc = L.gtsfm_netvlad_batched(_ptr(images), n, H, W, 3, _ptr(weights), int(bool(whiten)), _ptr(vlad), _ptr(desc),
+                                 _ptr(ws), ws.numel(), native.stream_handle(stream))
+    native.check(rc, "gtsfm_netvlad_batched")
+    return desc, vlad

@@ -8,11 +8,14 @@ every pair task. Here each rank owns a fixed share instead:
 - exchange: ONE all-gather of the fixed-size per-rank feature block (descriptors, keypoint xy, counts packed into one
   byte buffer), padded to `n_per = ceil(n / world)` images per rank, so the gathered tensors are rank-major: image i
   sits in global slot `(i mod world) * n_per + i // world`;
-- matching + verification: the lexicographic (i1, i2) pair list dealt round-robin (rank r owns pairs r, r + world,
-  r + 2 world, ...). Contiguous blocks left the ranks unequal: the pair list's tail holds the close (many-match)
-  pairs of the last images, so at C4 on 8 ranks rank 7's RANSAC took 74 ms against rank 0's 44 (`profiles/r05aj_*`).
-  Consecutive pairs of a rank still mostly share i1 (the matcher's pair groups keep A in registers), and every pair
-  keeps its global index, which keys the RANSAC sampler: a pair's result does not depend on the world size.
+- matching + verification: the (i1, i2) pair list cut into runs of consecutive pairs that share i1 and the block
+  i2 // PAIR_BLOCK (the distance GEMM's pair groups, device.pair_groups: up to 4 pairs that share the register
+  operand), the runs dealt round-robin (run r to rank r mod world). Contiguous blocks of the list left the ranks
+  unequal: its tail holds the close (many-match) pairs of the last images, so at C4 on 8 ranks rank 7's RANSAC took
+  74 ms against rank 0's 44 (`profiles/r05aj_*`). Dealing single pairs round-robin (round 5) balanced them but split
+  every pair group across ranks (at 2 / 4 ranks a rank's groups were half / a quarter full, so the matcher re-read
+  its register operand per pair); whole runs keep the groups and the balance. Every pair keeps its global index,
+  which keys the RANSAC sampler: a pair's result does not depend on the world size.
 
 Nothing here is GPU specific: the same functions run on CPU tensors under the gloo backend (tests/test_sharding.py).
 """
@@ -46,9 +49,41 @@ def all_pairs(n_img: int) -> np.ndarray:
     return np.stack([i1, i2], axis=1).astype(np.int64)
 
 
-def rank_pairs(pairs: np.ndarray, world: int, rank: int) -> np.ndarray:
-    """Positions (into `pairs`) of the pairs rank `rank` matches and verifies: every world-th pair from `rank`."""
-    return np.arange(rank, len(pairs), max(world, 1), dtype=np.int64)
+PAIR_BLOCK = 4  # i2 block of the distance GEMM's pair groups (device.pair_groups at the default max group of 4)
+
+
+def pair_runs(pairs: np.ndarray, block: int = PAIR_BLOCK) -> np.ndarray:
+    """Run id of every pair: consecutive pairs with the same (i1, i2 // block) share a run."""
+    pairs = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    if len(pairs) == 0:
+        return np.zeros(0, dtype=np.int64)
+    key = pairs[:, 0] * (int(pairs[:, 1].max()) // block + 1) + pairs[:, 1] // block
+    return np.r_[0, np.cumsum(key[1:] != key[:-1])].astype(np.int64)
+
+
+def rank_pairs(pairs: np.ndarray, world: int, rank: int, block: int = PAIR_BLOCK) -> np.ndarray:
+    """Positions (into `pairs`) of the pairs rank `rank` matches and verifies, in list order: the runs of pair_runs
+    dealt in list order, each to the rank holding the fewest pairs so far (lowest rank on ties) -- round-robin while
+    the runs are equal, and never more than one run (<= block pairs) apart when they are not."""
+    world = max(world, 1)
+    if world == 1:
+        return np.arange(len(pairs), dtype=np.int64)
+    return np.flatnonzero(run_owners(pairs, world, block) == rank).astype(np.int64)
+
+
+def run_owners(pairs: np.ndarray, world: int, block: int = PAIR_BLOCK) -> np.ndarray:
+    """Owning rank of every pair under rank_pairs' dealing."""
+    run = pair_runs(pairs, block)
+    if len(run) == 0:
+        return run
+    sizes = np.bincount(run)
+    owner_of_run = np.empty(len(sizes), dtype=np.int64)
+    load = [0] * world
+    for r, sz in enumerate(sizes.tolist()):
+        k = min(range(world), key=load.__getitem__)
+        owner_of_run[r] = k
+        load[k] += sz
+    return owner_of_run[run]
 
 
 def pack_features(tensors: Sequence[torch.Tensor], n_per: int,
@@ -145,9 +180,10 @@ class EmulatedAllGather:
         return g
 
 
-def gather_pair_results(local: torch.Tensor, n_pairs: int,
+def gather_pair_results(local: torch.Tensor, pairs: np.ndarray,
                         group: Optional[torch.distributed.ProcessGroup] = None) -> torch.Tensor:
-    """Reassembles a per-pair result tensor (rank r holds the pairs rank_pairs(.., r)) into pair order everywhere.
+    """Reassembles a per-pair result tensor (rank r holds the pairs rank_pairs(pairs, .., r), in that order) into
+    pair order everywhere.
 
     Used only where a caller wants every rank to hold every pair's compact result (R, t, counts); the bench and the
     batched drop-ins copy each rank's results to the host instead.
@@ -155,10 +191,14 @@ def gather_pair_results(local: torch.Tensor, n_pairs: int,
     world = torch.distributed.get_world_size(group) if torch.distributed.is_initialized() else 1
     if world == 1:
         return local
-    per = int(math.ceil(n_pairs / world))
+    owned = [rank_pairs(pairs, world, r) for r in range(world)]
+    per = max(len(o) for o in owned)
     pad = per - local.shape[0]
     buf = torch.cat([local, local.new_zeros((pad,) + tuple(local.shape[1:]))]) if pad else local.contiguous()
     g = torch.empty((world * per,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     torch.distributed.all_gather_into_tensor(g, buf, group=group)
-    # rank-major (rank, k) -> pair k * world + rank
-    return g.view((world, per) + tuple(local.shape[1:])).transpose(0, 1).reshape((world * per,) + tuple(local.shape[1:]))[:n_pairs]
+    g = g.view((world, per) + tuple(local.shape[1:]))
+    out = local.new_empty((len(pairs),) + tuple(local.shape[1:]))
+    for r, o in enumerate(owned):
+        out[torch.from_numpy(o).to(out.device)] = g[r, : len(o)]
+    return out

@@ -28,7 +28,7 @@ c_size_t = ctypes.c_size_t
 c_uint64 = ctypes.c_uint64
 
 # Mirrors include/gtsfm_hip.h
-ABI_VERSION = 400  # GTSFM_HIP_ABI_VERSION: lib() refuses a library built for another ABI
+ABI_VERSION = 401  # GTSFM_HIP_ABI_VERSION: lib() refuses a library built for another ABI
 GTSFM_OK = 0
 GTSFM_ERR_ARG = -1
 GTSFM_ERR_HIP = -2
@@ -98,6 +98,10 @@ SIGNATURES = {
     "gtsfm_retrieval_similarity": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "gtsfm_retrieval_pairs": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, ctypes.c_float, c_int, c_void_p, c_void_p,
                                       c_void_p]),
+    "gtsfm_netvlad_weights_floats": (c_size_t, []),
+    "gtsfm_netvlad_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "gtsfm_netvlad_batched": (
+        c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "gtsfm_compact_verified": (
         c_int,
         [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_double, c_void_p, c_void_p,

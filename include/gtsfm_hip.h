@@ -18,6 +18,8 @@
  *   gtsfm_sift_*            <- gtsfm/frontend/detector_descriptor/sift.py:27-56 detect_and_describe
  *                              (cv.cvtColor RGB2GRAY + cv.SIFT_create().detectAndCompute + Keypoints.get_top_k)
  *   gtsfm_retrieval_*       <- gtsfm/retriever/netvlad_retriever.py:77-228 (similarity blocks + pairs_from_score_matrix)
+ *   gtsfm_netvlad_*         <- gtsfm/frontend/global_descriptor/netvlad_global_descriptor.py:27-46 describe +
+ *                              thirdparty/hloc/netvlad.py:28-71 (NetVLADLayer), :160-191 (NetVLAD.forward)
  */
 #ifndef GTSFM_HIP_H_
 #define GTSFM_HIP_H_
@@ -39,7 +41,7 @@ extern "C" {
  * ---------------------------------------------------------------------------------------------- */
 /* ABI version (major*100 + minor); a binding built against this header checks that the library
  * returns GTSFM_HIP_ABI_VERSION before binding anything else. */
-#define GTSFM_HIP_ABI_VERSION 400
+#define GTSFM_HIP_ABI_VERSION 401
 int gtsfm_hip_abi_version(void);
 /* Name of the offload target the kernels were compiled for (e.g. "gfx950"). */
 const char* gtsfm_hip_target(void);
@@ -304,6 +306,28 @@ int gtsfm_retrieval_similarity(const float* d_desc, int n_img, int dim, int bloc
  * reference masks its argument in place). */
 int gtsfm_retrieval_pairs(const float* d_scores, int n_rows, int n_cols, const unsigned char* d_invalid, int num_select,
                           float min_score, int use_min_score, int* d_out_pairs, int* d_row_count, void* stream);
+
+/* ---- Global descriptor (f3): NetVLAD ---------------------------------------------------------------------------- */
+
+/* Replaces NetVLADGlobalDescriptor.describe (gtsfm/frontend/global_descriptor/netvlad_global_descriptor.py:27-46)
+ * and the network it runs (thirdparty/hloc/netvlad.py:160-191), batched over n same-sized RGB images
+ * d_images[n][H][W][3] u8 (describe()'s image.value_array). Per image: x = clamp(u / 255 * 255, 0, 255) - mean,
+ * VGG16 features[:-2] (13 conv3x3 + ReLU except the last, 2x2 max-pools after convs 2, 4, 7, 10, floor), per-location
+ * L2 pre-normalisation, NetVLADLayer (K = 64 clusters, D = 512: softmax(score_proj x), residual sums, intra-norm,
+ * d-major flatten, L2), then (whiten != 0) the 32768 -> 4096 whitening Linear and L2.
+ * d_weights: gtsfm_netvlad_weights_floats() floats:
+ *   mean[4] (averageImage RGB, 1 pad); per conv l = 0..12: W[9][cin][cout] (W[ky*3+kx][ci][co] = torch
+ *   backbone weight[co][ci][ky][kx]) then bias[cout], (cin, cout) = (3,64) (64,64) (64,128) (128,128) (128,256)
+ *   (256,256) (256,256) (256,512) (512,512) x 5; score_proj[64][512]; centers[512][64]; whiten W[4096][32768]
+ *   (nn.Linear's weight, row = output); whiten b[4096].
+ * Outputs: d_vlad[n][32768] (may be NULL when whiten != 0) and d_desc[n][4096] (whiten != 0). fp32-accurate
+ * arithmetic (convolutions as split-bf16 MFMA products, the rest fp32): parity with the reference is a tolerance. */
+size_t gtsfm_netvlad_weights_floats(void);
+
+size_t gtsfm_netvlad_workspace_bytes(int n, int H, int W);
+
+int gtsfm_netvlad_batched(const uint8_t* d_images, int n, int H, int W, int C, const float* d_weights, int whiten,
+                          float* d_vlad, float* d_desc, void* d_workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -12,8 +12,12 @@ Follows the vendored modules the reference runs (/root/reference/thirdparty/Supe
   (:70-82), 18 AttentionalPropagation layers self/cross (:85-138; 4 heads, head-interleaved channels d*4 + h),
   final_proj, scores / sqrt(256), log_optimal_transport with 20 Sinkhorn iterations (:141-170;
   superglue_matcher.py:25), mutual argmax + exp(score) > 0.2 (:266-276).
+- netvlad(): NetVLAD.forward (thirdparty/hloc/netvlad.py:160-191) as NetVLADGlobalDescriptor.describe drives it
+  (netvlad_global_descriptor.py:36-46): x / 255 * 255, clamp, - averageImage, VGG16 features[:-2] (torchvision's
+  configuration "D": 13 conv3x3 + ReLU except the last, max-pools after conv 2, 4, 7, 10), per-location L2
+  pre-normalisation, NetVLADLayer (:56-71; the residual sums written as sum_n s x - c sum_n s), whitening, L2.
 Pinned against the reference modules' own outputs on seeded random weights (tests/golden/superpoint_random_w0.npz,
-superglue_random_w0.npz, written in this container by tests/golden/make_*_golden.py): tests/test_oracle_deep.py.
+superglue_random_w0.npz, netvlad_random_w0.npz, written in this container by tests/golden/make_*_golden.py): tests/test_oracle_deep.py.
 """
 from __future__ import annotations
 
@@ -168,3 +172,30 @@ def log_optimal_transport(scores: torch.Tensor, alpha: torch.Tensor, iters: int)
         u = log_mu - torch.logsumexp(couplings + v.unsqueeze(1), dim=2)
         v = log_nu - torch.logsumexp(couplings + u.unsqueeze(2), dim=1)
     return couplings + u.unsqueeze(2) + v.unsqueeze(1) - norm
+
+
+NETVLAD_CONVS = [(0, False), (2, True), (5, False), (7, True), (10, False), (12, False), (14, True), (17, False),
+                 (19, False), (21, True), (24, False), (26, False), (28, False)]  # (backbone index, pool after)
+
+
+def netvlad(image: np.ndarray, sd: Dict[str, np.ndarray], whiten: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+    """(desc (4096,), vlad (32768,)) float32 of one (H, W, 3) uint8 RGB image; desc is vlad when whiten is False."""
+    with torch.no_grad():
+        x = torch.from_numpy(np.ascontiguousarray(image)).permute(2, 0, 1)[None].float() / 255
+        x = torch.clamp(x * 255, 0.0, 255.0) - _t(sd, "preprocess_mean").view(1, 3, 1, 1)
+        for i, (idx, pool) in enumerate(NETVLAD_CONVS):
+            x = F.conv2d(x, _t(sd, f"backbone.{idx}.weight"), _t(sd, f"backbone.{idx}.bias"), padding=1)
+            if i + 1 < len(NETVLAD_CONVS):
+                x = F.relu(x)
+            if pool:
+                x = F.max_pool2d(x, 2, 2)
+        x = F.normalize(x.reshape(1, x.shape[1], -1), dim=1)[0]  # (512, N)
+        s = F.softmax(_t(sd, "netvlad.score_proj.weight")[:, :, 0] @ x, dim=0)  # (64, N)
+        c = _t(sd, "netvlad.centers")  # (512, 64)
+        v = x @ s.T - c * s.sum(1)[None]  # sum_n s[k, n] (x[:, n] - c[:, k])
+        v = F.normalize(v, dim=0).reshape(-1)
+        vlad = v / torch.clamp(v.norm(), min=1e-12)
+        if not whiten:
+            return vlad.numpy(), vlad.numpy()
+        y = _t(sd, "whiten.weight") @ vlad + _t(sd, "whiten.bias")
+        return (y / torch.clamp(y.norm(), min=1e-12)).numpy(), vlad.numpy()

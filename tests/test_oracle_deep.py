@@ -63,3 +63,20 @@ def test_superglue_restatement_matches_reference(case):
     assert (m0 != ref).sum() <= max(1, 0.005 * len(ref)), ((m0 != ref).sum(), len(ref))
     both = (m0 >= 0) & (ref >= 0)
     np.testing.assert_allclose(ms0[both], k("mscores0")[both], atol=1e-4)
+
+
+def test_oracle_netvlad_vs_reference_golden():
+    """oracle.deep.netvlad against the reference's NetVLAD.forward / NetVLADLayer (tests/golden/make_netvlad_golden.py,
+    seeded random weights; the VGG16 layer list itself is parity-unpinned: torchvision is absent). Only summation
+    order differs (the residual sums are formed as sum s x - c sum s instead of the reference's explicit residuals)."""
+    from netvlad_weights import netvlad_cases as cases, netvlad_state_dict
+    from oracle import deep
+
+    sd = netvlad_state_dict(0)
+    with np.load(os.path.join(GOLDEN, "netvlad_random_w0.npz")) as z:
+        gold = {k: z[k] for k in z.files}
+    for name, imgs in cases().items():
+        for i, im in enumerate(imgs):
+            desc, vlad = deep.netvlad(im, sd)
+            np.testing.assert_allclose(vlad, gold[f"{name}/vlad"][i], atol=2e-6)
+            np.testing.assert_allclose(desc, gold[f"{name}/desc"][i], atol=2e-6)

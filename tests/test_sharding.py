@@ -63,7 +63,7 @@ def _worker(rank: int, world: int, port: int, n_img: int, out_dir: str):
             m = oracle.twoway_match(desc_all[s1, : cnt_all[s1]].numpy(), desc_all[s2, : cnt_all[s2]].numpy(), 0.8)
             counts.append(len(m))
         local = torch.tensor(counts, dtype=torch.int64)
-        full = sharding.gather_pair_results(local, len(pairs))
+        full = sharding.gather_pair_results(local, pairs)
         np.save(os.path.join(out_dir, f"counts_{world}_{rank}.npy"), full.numpy())
     finally:
         dist.destroy_process_group()
@@ -76,7 +76,12 @@ def test_pair_blocks_partition_all_pairs():
             owned = np.concatenate([sharding.rank_pairs(pairs, world, r) for r in range(world)])
             assert np.array_equal(np.sort(owned), np.arange(len(pairs)))  # a partition
             sizes = [len(sharding.rank_pairs(pairs, world, r)) for r in range(world)]
-            assert max(sizes) - min(sizes) <= 1  # round-robin: shares differ by at most one pair
+            assert max(sizes) - min(sizes) <= sharding.PAIR_BLOCK  # runs of <= 4 pairs, each to the least-loaded rank
+            for r in range(world):  # a rank's pairs stay in list order and keep whole (i1, i2 // 4) runs
+                own = sharding.rank_pairs(pairs, world, r)
+                assert np.all(np.diff(own) > 0)
+                run = sharding.pair_runs(pairs)
+                assert set(np.flatnonzero(np.isin(run, run[own])).tolist()) == set(own.tolist())
 
 
 def test_global_slots_are_rank_major():
@@ -108,8 +113,10 @@ def test_gloo_sharded_front_end_matches_single_process(world, tmp_path, oracle_m
 
 
 def test_match_plan_fills_the_gpu():
-    """match_plan keeps groups of 4 at C2 (4950 pairs: 1238 groups, 5 full rounds) and, for one rank's share of C2 at
-    8 GPUs (619 pairs), picks smaller groups whose pass-split workgroups take 10 instead of 16 pair-passes."""
+    """C2 (4950 pairs) keeps full groups of 4. The rank shares keep them too (whole runs are dealt): at 2 and 4 ranks
+    (nearly) every group of 4 is full and the plan keeps full groups of 2 or 4 (single-pair round-robin dealing left
+    them half / a quarter full, so the plan fell back to groups of 1); at 8 ranks (~620 pairs, ~160 groups for 256 CUs)
+    the plan trades group size for pass-split workgroups: 10 instead of 12 pair-passes."""
     from gtsfm_amd import device, native
     from gtsfm_amd.frontend import sharding
 
@@ -117,9 +124,14 @@ def test_match_plan_fills_the_gpu():
     pairs = sharding.all_pairs(100)
     g = device.match_plan(pairs, 2048, 128, n_cu=256)
     assert g.shape[1] == 4
+    for world in (2, 4):
+        share = pairs[sharding.rank_pairs(pairs, world, 0)]
+        gw = device.match_plan(share, 2048, 128, n_cu=256)
+        assert (device.pair_groups(share, 4) >= 0).mean() > 0.95
+        assert gw.shape[1] >= 2 and (gw >= 0).mean() > 0.95, (world, gw.shape, (gw >= 0).mean())
     share = pairs[sharding.rank_pairs(pairs, 8, 0)]
     g8 = device.match_plan(share, 2048, 128, n_cu=256)
-    assert g8.shape[1] < 4
+    assert (device.pair_groups(share, 4) >= 0).mean() > 0.95
     assert device._split_cost(len(g8), g8.shape[1], 2048, 256) <= 10
     assert sorted(g8[g8 >= 0].tolist()) == list(range(len(share)))
 
