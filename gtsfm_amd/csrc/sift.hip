@@ -17,6 +17,9 @@
 #pragma clang fp contract(off)
 #include <float.h>
 #include <math.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "common.hpp"
 
@@ -585,6 +588,298 @@ BlurStreamFn blur_stream_get(int r) {
         default:
             return nullptr;
     }
+}
+
+// Row pass of one 8-row chunk held in LDS (row stride IWP, input column x + R for output column x), in place: 8
+// threads per row, 8 outputs each, the same packed fmaf chains and window reads as blur_stream_kernel's row pass.
+template <int R, int IWP>
+__device__ __forceinline__ void row_blur_chunk(float* chunk, const float (&k)[R + 1], int lane) {
+    constexpr int NV = (kBlurRowOut + 2 * R) / 2;
+    static_assert((kBlurRowThr - 1) * kBlurRowOut + 2 * NV <= IWP, "row-pass window past the LDS row");
+    const int g8 = (lane % kBlurRowThr) * kBlurRowOut;
+    float* rowp = chunk + (lane / kBlurRowThr) * IWP;
+    typedef __attribute__((address_space(3))) const volatile unsigned long long lds_u64;
+    lds_u64* wp = (lds_u64*)(rowp + g8);
+    float v[2 * NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+        const unsigned long long w2 = wp[q];
+        v[2 * q] = __uint_as_float((uint32_t)w2); v[2 * q + 1] = __uint_as_float((uint32_t)(w2 >> 32));
+    }
+    asm volatile("" ::: "memory");
+    pf2 o[kBlurRowOut / 2];
+#pragma unroll
+    for (int h = 0; h < kBlurRowOut / 2; ++h) o[h] = pf2{k[0], k[0]} * pf2{v[R + 2 * h], v[R + 2 * h + 1]};
+#pragma unroll
+    for (int j = 1; j <= R; ++j) {
+        pf2 sm[kBlurRowOut / 2];
+#pragma unroll
+        for (int h = 0; h < kBlurRowOut / 2; ++h)
+            sm[h] = pf2{v[R + 2 * h - j], v[R + 2 * h + 1 - j]} + pf2{v[R + 2 * h + j], v[R + 2 * h + 1 + j]};
+#pragma unroll
+        for (int h = 0; h < kBlurRowOut / 2; ++h) o[h] = __builtin_elementwise_fma(pf2{k[j], k[j]}, sm[h], o[h]);
+    }
+#pragma unroll
+    for (int h = 0; h < kBlurRowOut / 2; ++h) *(float2*)(rowp + g8 + 2 * h) = make_float2(o[h].x, o[h].y);
+    asm volatile("" ::: "memory");
+}
+
+// Column pass over a three-chunk register window (8 rows per chunk, chunk slots rotating mod 3, the newest chunk in
+// slot J): the 8 outputs of the middle chunk, acc = k0 c_y, acc = fma(kj, c_{y-j} + c_{y+j}, acc) (R <= 8).
+template <int R, int J>
+__device__ __forceinline__ void col_blur_window(const float (&win)[24], const float (&k)[R + 1], float (&out)[8]) {
+    static_assert(R <= 8, "the halo fits the neighbouring chunks");
+    auto slot = [](int off) {  // off = output row offset + tap in [-R, 7 + R], relative to the middle chunk's first row
+        const int q = (off + 16) / 8 - 2;  // floor(off / 8) in {-1, 0, 1}
+        return 8 * ((J - 1 + q + 6) % 3) + (off - 8 * q);
+    };
+#pragma unroll
+    for (int o = 0; o < 8; o += 2) {
+        pf2 acc = pf2{k[0], k[0]} * pf2{win[slot(o)], win[slot(o + 1)]};
+#pragma unroll
+        for (int j = 1; j <= R; ++j) {
+            const pf2 sm = pf2{win[slot(o - j)], win[slot(o + 1 - j)]} + pf2{win[slot(o + j)], win[slot(o + 1 + j)]};
+            acc = __builtin_elementwise_fma(pf2{k[j], k[j]}, sm, acc);
+        }
+        out[o] = acc.x;
+        out[o + 1] = acc.y;
+    }
+}
+
+// Octave 0's base level as a streaming pass from the gray bytes (no upsampled image in memory, no tile barriers):
+//   G0 = GaussianBlur_{sig_diff}(resize_2x(gray(image)))
+// (sift.py:44-66 -> cv::SIFT createInitialImage). gray_pad_kernel first writes the gray image (cv::cvtColor's fixed
+// point for RGB) with a padded row pitch; then one wave per (image, row segment, 64-column strip), lane = G0 column.
+// Per 8-row chunk of upsampled rows: the chunk's gray source rows (at most 6, 48 aligned bytes each) arrive in a
+// per-wave LDS slot by LDS-DMA issued two chunks ahead; the upsampled rows (INTER_LINEAR 2x: gray integers times
+// quarter weights, so every product and sum is exact in fp32 in any order) are written to an LDS chunk, row-blurred in
+// place, and each lane takes its column into a three-chunk window whose column pass gives the lane's 8 G0 values one
+// chunk later. Every fmaf chain is the one blur2d_kernel<5, true> evaluates (reflect-101 rows and columns past the
+// image edge compute the mirrored pixel's value bit for bit), so the pyramid is unchanged.
+// Octave 0 of C2 (100 x 3840 x 2160 from RGB): 0.99 ms + 0.20 ms gray staging, against 1.82 ms for the upsampling tile
+// kernel (profiles/r06j_*; with the source bytes prefetched one chunk ahead into registers instead, the compiler's
+// vmcnt(0) at every chunk left it at 1.13 ms). Measured and not kept: the same wave also running G1's row and column
+// passes on its G0 chunks (strips of 54 G1 columns, no G0 re-read): 179 VGPRs, 2 waves per SIMD, 3.5 ms for both
+// levels (4.2 ms with spills at 128 VGPRs) against about 2.3 ms as two launches -- the serial LDS round trips of two
+// blur stages per chunk need more waves in flight than that register budget leaves.
+// The kernel is OpenCV's for its default sigma (1.6, 3 layers, input sigma 0.5): sig_diff = 1.249, 11 taps, compiled
+// in (literal operands); the host takes this path only when the taps it computed for the call are these bits.
+constexpr int kBaseR = 5;
+constexpr float kBaseTaps[kBaseR + 1] = {0x1.4713ccp-2f, 0x1.dac53p-3f,   0x1.6b0372p-4f,
+                                         0x1.2469fap-6f, 0x1.f04b72p-10f, 0x1.bbb2a4p-14f};
+// Gray source rows are staged with a padded pitch (kBasePitchPad bytes past the row, rounded to 64) so that every
+// chunk's source window -- 12 aligned dwords from the strip's first source column rounded down to 4 -- is one
+// in-bounds, aligned read per dword.
+constexpr int kBaseRowDw = 12;                 // dwords per staged source row: >= ((64 + 2 R) / 2 + 3 + 3) / 4
+constexpr int kBaseRowB = 4 * kBaseRowDw;      // LDS ring row stride (bytes)
+constexpr int kBaseRingRows = 6;               // source rows of one chunk
+constexpr int kBasePD = 2;                     // chunks prefetched ahead
+constexpr int kBasePitchPad = kBaseRowB;
+constexpr int kBaseWaveFloats = (kBasePD + 1) * kBaseRingRows * kBaseRowDw + 8 * blur_iwp(kBaseR);
+__host__ __device__ constexpr int base_pitch(int w0) { return (w0 + kBasePitchPad + 63) / 64 * 64; }
+
+// cv::cvtColor RGB -> gray fixed point, (R 4899 + G 9617 + B 1868 + 2^13) >> 14 (C = 3), or a copy (C = 1), into rows of
+// base_pitch(W0) bytes (zero padded): one thread per 4 output bytes of a row, one dword store; the source as C aligned
+// dwords when the source rows are dword aligned (`aligned`: base address and W0 C both multiples of 4) and the 4
+// pixels lie inside the row, else byte by byte.
+__device__ __forceinline__ uint32_t cv_gray(uint32_t r, uint32_t g, uint32_t b) {
+    return (r * 4899u + g * 9617u + b * 1868u + (1u << 13)) >> 14;
+}
+template <int C>
+__global__ __launch_bounds__(256) void gray_pad_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ gray,
+                                                       int n_rows, int W0, int pitch, int aligned) {
+    const int dw_per_row = pitch / 4;
+    const long long n = (long long)n_rows * dw_per_row;
+    for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+        const int row = (int)(i / dw_per_row), x0 = 4 * (int)(i - (long long)row * dw_per_row);
+        const uint8_t* s = src + ((size_t)row * W0 + x0) * C;
+        uint32_t out = 0;
+        if (aligned && x0 + 4 <= W0) {
+            const uint32_t* w = (const uint32_t*)s;
+            if constexpr (C == 1) {
+                out = w[0];
+            } else {
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+                out = cv_gray(w0 & 255, (w0 >> 8) & 255, (w0 >> 16) & 255) |
+                      cv_gray(w0 >> 24, w1 & 255, (w1 >> 8) & 255) << 8 |
+                      cv_gray((w1 >> 16) & 255, w1 >> 24, w2 & 255) << 16 |
+                      cv_gray((w2 >> 8) & 255, (w2 >> 16) & 255, w2 >> 24) << 24;
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (x0 + q < W0) out |= (C == 1 ? s[q] : cv_gray(s[C * q], s[C * q + 1 % C], s[C * q + 2 % C])) << (8 * q);
+        }
+        ((uint32_t*)gray)[i] = out;
+    }
+}
+
+__global__ __launch_bounds__(64 * kStreamWaves) __attribute__((amdgpu_waves_per_eu(4))) void base_stream_kernel(
+    const uint8_t* __restrict__ gray8, int H0, int W0, int pitch, float* __restrict__ g0, float* __restrict__ sink,
+    int H, int W, int n_strips, int n_seg, int n_img) {
+    constexpr int R1 = kBaseR, IW1 = 64 + 2 * R1, IWP1 = blur_iwp(R1), WF = kBaseWaveFloats;
+    // chunk j holds upsampled rows ys - kLead + 8 j ..; its G0 chunk (the middle one of the window) starts 8 rows earlier
+    constexpr int kLead = 8;
+    constexpr int kItems = kBaseRingRows * kBaseRowDw;
+    static_assert(IW1 <= 128 && (IW1 / 2 + 3) + 3 <= kBaseRowB, "one extra column per lane; the source span fits");
+    static_assert(kItems <= 2 * 64, "two dword loads per lane cover a chunk's source rows");
+    __shared__ __attribute__((aligned(16))) float lds[kStreamWaves * WF];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n_blocks = gridDim.x, per_xcd = n_blocks >> 3;
+    const int u = __builtin_amdgcn_readfirstlane((((blockIdx.x & 7) * per_xcd) + (blockIdx.x >> 3)) * kStreamWaves +
+                                                 wave);
+    if (u >= n_strips * n_seg * n_img) return;
+    const int strip = u % n_strips, part = u / n_strips;
+    const int b = part / n_seg, seg = part - b * n_seg;
+    const int G8 = (H + 7) / 8;
+    const int ys = 8 * (int)((long long)seg * G8 / n_seg);
+    const int ye = min(H, 8 * (int)((long long)(seg + 1) * G8 / n_seg));
+    if (ys >= ye) return;
+    const int s0 = strip * 64;
+    float* wl = lds + __builtin_amdgcn_readfirstlane(wave) * WF;
+    float* ring = wl;  // kBasePD + 1 slots of a chunk's source rows (kBaseRowB bytes each), filled by LDS-DMA
+    float* ch1 = wl + (kBasePD + 1) * kBaseRingRows * kBaseRowDw;  // upsampled chunk, then its row blur
+    float k1[R1 + 1];
+#pragma unroll
+    for (int j = 0; j <= R1; ++j) k1[j] = kBaseTaps[j];
+
+    // upsampled columns of this lane, as a (set a, set b) pair: s0 - R1 + lane and (lanes < IW1 - 64) s0 - R1 + 64 + lane
+    const bool has_b = lane < IW1 - 64;
+    int ca0, ca1, cb0, cb1;
+    float fa, fb;
+    up_coord(reflect101(s0 - R1 + lane, W), W0, ca0, ca1, fa);
+    up_coord(reflect101(s0 - R1 + 64 + (has_b ? lane : 0), W), W0, cb0, cb1, fb);
+    int gx0 = has_b ? min(ca0, cb0) : ca0;
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) gx0 = min(gx0, __shfl_xor(gx0, m));
+    const int a0 = __builtin_amdgcn_readfirstlane(gx0) & ~3;  // first staged source column (dword aligned)
+    ca0 -= a0; ca1 -= a0; cb0 -= a0; cb1 -= a0;
+    const pf2 fx = {fa, fb}, fx1 = {1.f - fa, 1.f - fb};
+    // staged item i (lane + 64 q) = dword i % kBaseRowDw of source row lo + i / kBaseRowDw (clamped to the image: rows
+    // past a border chunk's range are loaded but not read)
+    const uint8_t* src = gray8 + (size_t)b * H0 * pitch + a0;
+    const int it_row0 = lane / kBaseRowDw, it_col0 = 4 * (lane % kBaseRowDw);
+    const int it_row1 = (64 + lane) / kBaseRowDw, it_col1 = 4 * ((64 + lane) % kBaseRowDw);
+
+    // chunk j holds upsampled (virtual) rows u = ys - kLead + 8 j .. + 7; G0 chunk j - 2 completes there. An interior
+    // chunk (u >= 2, u + 10 <= H; u is even) reads source rows u / 2 - 1 .. u / 2 + 4 with no reflection
+    // or clamping: row u + 2t is h_t / 4 + 3 h_{t+1} / 4 and row u + 2t + 1 is 3 h_{t+1} / 4 + h_{t+2} / 4 (h_t: source
+    // row lo + t interpolated across); other chunks take the per-row coordinates.
+    const int n_chunks = (ye - ys + 7) / 8 + 2;
+    auto interior = [&](int j) {
+        const int u0 = ys - kLead + 8 * j;
+        return u0 >= 2 && u0 + 10 <= H;
+    };
+    // per-row upsampling coordinates of a border chunk on lanes 0..7, and its first source row
+    auto row_params = [&](int j, int& sy0, int& sy1, float& fy) {
+        int a_0 = 0, a_1 = 0;
+        float f = 0.f;
+        up_coord(reflect101(ys - kLead + 8 * j + (lane & 7), H), H0, a_0, a_1, f);
+        sy0 = a_0; sy1 = a_1; fy = f;
+        int l = a_0;
+#pragma unroll
+        for (int m = 4; m > 0; m >>= 1) l = min(l, __shfl_xor(l, m));
+        return __builtin_amdgcn_readfirstlane(l);
+    };
+    auto first_row = [&](int j) {
+        if (interior(j)) return (ys - kLead + 8 * j) / 2 - 1;
+        int s_0, s_1;
+        float f;
+        return row_params(j, s_0, s_1, f);
+    };
+    // Chunk j's source rows go to ring slot j mod 3 by global_load_lds_dword (two per chunk, always issued: past the
+    // last chunk the last one is reloaded into the free slot), kBasePD chunks ahead, with the waits explicit as in
+    // blur_stream_kernel. Every chunk from the third on also issues exactly 8 global stores (rows or lanes outside the
+    // image go to `sink`), so the count of vector-memory operations issued after chunk j's loads is known:
+    // 4 for j <= 2, 12 for j = 3 and 20 after.
+    int plo[3];
+    auto issue = [&](int j, auto kb) {
+        constexpr int K = decltype(kb)::value;
+        const int lo = first_row(j);
+        plo[K] = lo;
+        const uint32_t d = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)(ring + K * kBaseRingRows * kBaseRowDw));
+        const uint32_t o0 = (uint32_t)(min(lo + it_row0, H0 - 1) * pitch + it_col0);
+        const uint32_t o1 = (uint32_t)(min(lo + it_row1, H0 - 1) * pitch + it_col1);
+        asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(o0), "s"(src), "{m0}"(d) : "memory");
+        if (64 + lane < kItems)
+            asm volatile("s_nop 0\n\tglobal_load_lds_dword %0, %1" ::"v"(o1), "s"(src), "{m0}"(d + 256u) : "memory");
+    };
+    auto put_u = [&](int r, pf2 v) {
+        ch1[r * IWP1 + lane] = v.x;
+        if (has_b) ch1[r * IWP1 + 64 + lane] = v.y;
+    };
+    float win1[24];
+    issue(0, std::integral_constant<int, 0>{});
+    issue(min(1, n_chunks - 1), std::integral_constant<int, 1>{});
+    const int x = s0 + lane;
+    const bool out_lane = x < W;
+    float* g0i = g0 + (size_t)b * H * W;
+    auto chunk = [&](int j, auto jc) {
+        constexpr int J = decltype(jc)::value;  // j mod 3
+        const int lo = plo[J];
+        issue(min(j + kBasePD, n_chunks - 1), std::integral_constant<int, (J + kBasePD) % 3>{});
+        if (j >= 4)
+            asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+        else if (j == 3)
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        const uint8_t* rg = (const uint8_t*)(ring + J * kBaseRingRows * kBaseRowDw);
+        // upsampled rows of chunk j
+        if (interior(j)) {
+            pf2 h[6];
+#pragma unroll
+            for (int t = 0; t < 6; ++t) {
+                const uint8_t* rr = rg + t * kBaseRowB;
+                const pf2 p0 = {(float)rr[ca0], (float)rr[cb0]}, p1 = {(float)rr[ca1], (float)rr[cb1]};
+                h[t] = __builtin_elementwise_fma(p0, fx1, p1 * fx);
+            }
+            const pf2 q1 = {0.25f, 0.25f}, q3 = {0.75f, 0.75f};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                put_u(2 * t, __builtin_elementwise_fma(h[t], q1, h[t + 1] * q3));
+                put_u(2 * t + 1, __builtin_elementwise_fma(h[t + 1], q3, h[t + 2] * q1));
+            }
+        } else {
+            int c_sy0, c_sy1;
+            float c_fy;
+            row_params(j, c_sy0, c_sy1, c_fy);
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int sy0 = __shfl(c_sy0, r), sy1 = __shfl(c_sy1, r);
+                const float fy = __shfl(c_fy, r);
+                const uint8_t* r0 = rg + (sy0 - lo) * kBaseRowB;
+                const uint8_t* r1 = rg + (sy1 - lo) * kBaseRowB;
+                const pf2 a = __builtin_elementwise_fma(pf2{(float)r0[ca0], (float)r0[cb0]}, fx1,
+                                                        pf2{(float)r0[ca1], (float)r0[cb1]} * fx);
+                const pf2 c = __builtin_elementwise_fma(pf2{(float)r1[ca0], (float)r1[cb0]}, fx1,
+                                                        pf2{(float)r1[ca1], (float)r1[cb1]} * fx);
+                put_u(r, __builtin_elementwise_fma(a, pf2{1.f - fy, 1.f - fy}, c * pf2{fy, fy}));
+            }
+        }
+        asm volatile("" ::: "memory");
+        row_blur_chunk<R1, IWP1>(ch1, k1, lane);
+#pragma unroll
+        for (int r = 0; r < 8; ++r) win1[8 * J + r] = ch1[r * IWP1 + lane];
+        if (j < 2) return;
+        float gv[8];
+        col_blur_window<R1, J>(win1, k1, gv);
+        const int y0 = ys - kLead - 8 + 8 * j;  // G0 chunk j - 2
+#pragma unroll
+        for (int o = 0; o < 8; ++o) {
+            const int y = y0 + o;
+            // (y >= ys: the lead is one chunk)
+            float* dp = (out_lane && y < ye) ? g0i + (size_t)y * W + x : sink + lane;
+            *dp = gv[o];
+        }
+    };
+    for (int j = 0; j < n_chunks; j += 3)
+        static_for<3>([&](auto jc) {
+            if (j + decltype(jc)::value < n_chunks) chunk(j + decltype(jc)::value, jc);
+        });
+    // the prefetched rows land before the wave retires
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <bool kFromU8>
@@ -1492,7 +1787,7 @@ struct Layout {
     int Ho[kMaxOct], Wo[kMaxOct];
     size_t g[kMaxOct][kLevels];  // byte offsets
     size_t seen, seen_bytes, seen_off[kMaxOct], cand, ref, kps_sh, kp_shard_counts, kps, kp_counts, counters, sel,
-        n_sel, total;
+        n_sel, gray, sink, total;
 };
 
 int num_octaves(int H, int W) {
@@ -1543,6 +1838,8 @@ Layout make_layout(int B, int H, int W, int max_kpts) {
     L.counters = take((size_t)kMaxOct * (kCandShards + 16) * sizeof(int));
     L.sel = take((size_t)B * max_kpts * sizeof(int));
     L.n_sel = take((size_t)B * sizeof(int));
+    L.gray = take((size_t)B * H * base_pitch(W));  // the padded gray rows of the streaming base
+    L.sink = take(64 * sizeof(float));             // its stores outside the image
     L.total = off;
     return L;
 }
@@ -1668,10 +1965,36 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
     auto join_side = [&]() {
         if (hipEventRecord(ev[kMaxOct], side) == hipSuccess) (void)hipStreamWaitEvent(stream, ev[kMaxOct], 0);
     };
+    // octave 0's base as a streaming launch from the gray bytes when the call's taps are the compiled-in ones
+    // (OpenCV's defaults). GTSFM_SIFT_BASE_STREAM (test hooks): 0 selects the upsampling tile kernel, 2 makes an
+    // ineligible call fail with GTSFM_ERR_ARG instead of taking it (a test pins the two paths against each other).
+    const char* base_env = getenv("GTSFM_SIFT_BASE_STREAM");
+    const char base_mode = base_env && base_env[0] ? base_env[0] : '1';
+    const bool base_stream = base_mode != '0' && taps[0].r == kBaseR &&
+                             memcmp(taps[0].k, kBaseTaps, sizeof(kBaseTaps)) == 0;
+    if (base_mode == '2' && !base_stream) return GTSFM_ERR_ARG;
+    auto base_stream_launch = [&](int h, int w) -> int {
+        const int n_strips = (w + 63) / 64;
+        const int n_seg = max(1, min(max(3, (64 * n_cu + B * n_strips - 1) / (B * n_strips)), (h + 31) / 32));
+        const int n_blk = ((n_strips * n_seg * B + kStreamWaves - 1) / kStreamWaves + 7) / 8 * 8;
+        const int pitch = base_pitch(W);
+        const long long n_dw = (long long)B * H * (pitch / 4);
+        const dim3 ggrid((unsigned)std::min<long long>((n_dw + 255) / 256, 16 * 1024));
+        const int aligned = ((uintptr_t)d_images & 3) == 0 && ((size_t)W * channels) % 4 == 0;
+        if (channels == 3)
+            hipLaunchKernelGGL(gray_pad_kernel<3>, ggrid, dim3(256), 0, stream, d_images, ws + L.gray, B * H, W, pitch,
+                               aligned);
+        else
+            hipLaunchKernelGGL(gray_pad_kernel<1>, ggrid, dim3(256), 0, stream, d_images, ws + L.gray, B * H, W, pitch,
+                               aligned);
+        hipLaunchKernelGGL(base_stream_kernel, dim3(n_blk), dim3(64 * kStreamWaves), 0, stream, ws + L.gray, H, W,
+                           pitch, F(L.g[0][0]), F(L.sink), h, w, n_strips, n_seg, B);
+        return hipGetLastError() == hipSuccess ? GTSFM_OK : GTSFM_ERR_HIP;
+    };
     for (int o = 0; o < L.n_oct; ++o) {
         const int h = L.Ho[o], w = L.Wo[o];
         // octave o > 0 starts from the layer-3 level of octave o - 1, decimated by that level's blur launch
-        if (o == 0 && blur(nullptr, F(L.g[0][0]), nullptr, h, w, taps[0])) {
+        if (o == 0 && (base_stream ? base_stream_launch(h, w) : blur(nullptr, F(L.g[0][0]), nullptr, h, w, taps[0]))) {
             join_side();
             return GTSFM_ERR_HIP;
         }

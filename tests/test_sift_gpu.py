@@ -194,3 +194,37 @@ def test_image_mask_bit_exact_vs_oracle(dev, oracle_mod):
     for i, im in enumerate(imgs):
         ref = oracle_mod.sift(grays[i], k, mask=None if im.mask is None else mask)[0]
         np.testing.assert_array_equal(feats.keypoints[i].coordinates, ref[:, :2].astype(np.float64))
+
+
+def test_streaming_base_equals_tile_path(dev, oracle_mod, monkeypatch):
+    """Octave 0's base level runs as a streaming kernel from the gray bytes (base_stream_kernel, after gray_kernel for
+    RGB) by default; GTSFM_SIFT_BASE_STREAM=0 selects the upsampling tile kernel and =2 fails the call unless the
+    streaming base is taken (the default taps match the compiled-in ones). Both give identical keypoints, descriptors
+    and detection counts: 1080p RGB bench views (3840-wide octave 0: 60 strips), odd and minimum sizes (reflection on
+    every side of a one-strip image, source rows clamped), gray and RGB, odd pixel counts (gray_kernel's tail); the
+    smallest also against the oracle."""
+    from gtsfm_amd import device, synthetic
+
+    scene = synthetic.render_scene(4, 1080, 1920, device="cuda")
+    rng = np.random.default_rng(21)
+    cases = [scene.images.contiguous(),
+             torch.from_numpy(np.stack([_texture(rng, 333, 517) for _ in range(2)])).cuda(),
+             torch.from_numpy(np.stack([np.stack([_texture(rng, 61, 97)] * 3, axis=2) for _ in range(3)])).cuda(),
+             torch.from_numpy(_texture(rng, 16, 16)[None].copy()).cuda(),
+             torch.from_numpy(_texture(rng, 17, 29)[None].copy()).cuda()]
+    for imgs in cases:
+        out = {}
+        for mode in ("2", "0"):
+            monkeypatch.setenv("GTSFM_SIFT_BASE_STREAM", mode)
+            res = device.sift_extract(imgs, 500)
+            out[mode] = [t.cpu().numpy() for t in (res.xy, res.attr, res.desc, res.count, res.n_detected)]
+        for a, b in zip(out["2"], out["0"]):
+            np.testing.assert_array_equal(a, b)
+        assert out["2"][4].min() > 0 or imgs.shape[1] <= 17
+    monkeypatch.delenv("GTSFM_SIFT_BASE_STREAM")
+    gray = _texture(np.random.default_rng(3), 17, 29)
+    kp, desc, nd = _gpu_sift(gray, 50)
+    rkp, rdesc, rnd = oracle_mod.sift(gray, 50)
+    assert nd == rnd
+    np.testing.assert_array_equal(kp, rkp)
+    np.testing.assert_array_equal(desc, rdesc)
