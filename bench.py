@@ -595,8 +595,9 @@ def main_frontend(args, info, config: str):
         del scene.images
         torch.cuda.empty_cache()
         baseline_images = None
+        n_sample = n_img if args.cpu_baseline_full else (deep_sample(config) if deep else 16)
         if want_baseline:
-            baseline_images = host_images.numpy()[sample_images(n_img, deep_sample(config) if deep else 16)]
+            baseline_images = host_images.numpy()[sample_images(n_img, n_sample)]
     cfg = FrontEndConfig(kpts=kpts, ratio=RATIO, thresh_px=THRESH_PX, min_inliers=MIN_INLIERS,
                          min_inlier_ratio=MIN_INLIER_RATIO)
     if deep:
@@ -612,7 +613,8 @@ def main_frontend(args, info, config: str):
     cfg.bundle_adjust = args.ba
     kernels = sp_sd = sg_sd = None
     if deep:
-        sp_sd, sp_w, sg_sd, sg_w = deep_weights(dev, config == "c5", head=True if config == "c5" else "c3")
+        head = True if config == "c5" else ("c3" if args.c3_head == "c3" else False)
+        sp_sd, sp_w, sg_sd, sg_w = deep_weights(dev, config == "c5", head=head)
         kernels = HipSuperPointKernels(sp_w, "superglue" if config == "c5" else "twoway", sg_w)
     exchange, kc_all = None, np.zeros(n_img)
     if emulate:
@@ -677,6 +679,16 @@ def main_frontend(args, info, config: str):
         return {k: round(float(np.median([r.get(k, 0.0) for r in rows])), 3) for k in keys}
 
     st_host, st_res = med(stage_host), med(stage_res)
+    certificate = None
+    if config == "c3" and world == 1 and not emulate:
+        # F16_RERANK's certificate on this workload (one more, untimed matching of the step's features): how much of
+        # the shortlist the fp16 bound certified, and how the rest was recomputed exactly (whole (pair, side) tiles
+        # or per-keypoint rescans) -- the share of the matcher's time the descriptor head decides
+        from gtsfm_amd import device as hip
+
+        st = {}
+        hip.match_pairs(fe.feats.desc, fe.feats.count, fe.pairs_dev, RATIO, native.GTSFM_MATCH_F16_RERANK, stats=st)
+        certificate = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in st.items()}
     n_ok = torch.tensor([float(res.isp_ok.sum())], dtype=torch.float64, device=dev)
     n_inl_rows = torch.tensor([float(len(res.v_corr))], dtype=torch.float64, device=dev)
     # per-stage algorithmic work of this rank
@@ -802,8 +814,10 @@ def main_frontend(args, info, config: str):
                                                                       if config == "c5" else
                  "fp16-MFMA shortlist + fp32 exact re-rank") + " / fp64 RANSAC solver")
         data = ("synthetic (rendered textured room, seeds 0/1/2" + ("; 1 m strafe path" if config == "c3" else "")
-                + "); seeded random network weights with a whitened SuperPoint descriptor head "
-                "(tests/golden/make_superpoint_whitening.py" + (" --c3" if config == "c3" else "") + ")")
+                + "); seeded random network weights with " +
+                ("the plain seeded SuperPoint descriptor head (tests/superpoint_weights.py seed 0, not whitened)"
+                 if head is False else "a whitened SuperPoint descriptor head "
+                 "(tests/golden/make_superpoint_whitening.py" + (" --c3" if config == "c3" else "") + ")"))
     else:
         desc = (f"{wl}: {n_img} {'Lund Door' if config == 'c1' else 'synthetic'} {W}x{H} images, all "
                 f"{fe.total_pairs} pairs, SIFT {kpts} kpts/img, ratio {RATIO}, 5-pt RANSAC {THRESH_PX}px"
@@ -836,6 +850,8 @@ def main_frontend(args, info, config: str):
         "stage_ms_host_to_host": st_host,
         "roofline": roof,
     }
+    if certificate is not None:
+        out["matcher_certificate"] = certificate
     if emulate:
         # a per-rank measurement, not a scaling curve: value = this rank's pairs per second of its own step
         out["metric"] = "per-rank verified image-pairs/sec (one rank's share of an N-GPU job, emulated on one GPU)"
@@ -854,9 +870,12 @@ def main_frontend(args, info, config: str):
     if want_baseline:
         if deep:
             out["cpu_baseline"] = deep_cpu_baseline(baseline_images, intrinsics, n_img, kpts, sp_sd, sg_sd,
-                                                    n_img_sample=deep_sample(config))
-        else:
+                                                    n_img_sample=n_sample)
+        elif config == "c1":
             out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts)
+        else:
+            out["cpu_baseline"] = cpu_baseline(baseline_images, intrinsics, n_img, kpts, n_sift=n_sample,
+                                               n_pairs=n_img * (n_img - 1) // 2 if args.cpu_baseline_full else 120)
     if rank == 0 or emulate:
         print(json.dumps(out), flush=True)
 
@@ -875,6 +894,11 @@ def main():
     ap.add_argument("--resident-chunk", type=int, default=0)
     ap.add_argument("--pair-chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-full", action="store_true",
+                    help="time the CPU baseline on the whole workload (C2: ~100 s on 16 threads) instead of a sample")
+    ap.add_argument("--c3-head", choices=("c3", "plain"), default="c3",
+                    help="C3's SuperPoint descriptor head: the PCA-whitened one fitted to the scene, or the plain "
+                         "seeded random-weight head")
     ap.add_argument("--ba", action="store_true",
                     help="add the two-view triangulation + bundle adjustment stage (TwoViewEstimator bundle_adjust_2view)")
     ap.add_argument("--config", default="c2",

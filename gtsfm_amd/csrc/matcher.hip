@@ -1565,6 +1565,21 @@ size_t gtsfm_match_workspace_bytes(int n_img, int kmax, int dim, int n_pairs, in
     return 2 * gtsfm_align_up((size_t)n_pairs * kmax * sizeof(ExactTop2), 256);
 }
 
+int gtsfm_match_rerank_stats(const void* d_workspace, size_t workspace_bytes, int n_img, int kmax, int dim,
+                             int n_pairs, int* h_uncertified, int* h_uncertified_per_side, void* stream_v) {
+    if (!d_workspace || !h_uncertified || n_img <= 0 || kmax <= 0 || dim <= 0 || dim > kFlMaxDim || n_pairs < 0)
+        return GTSFM_ERR_ARG;
+    size_t off[10];
+    if (workspace_bytes < fl_layout(n_img, kmax, dim, n_pairs, off)) return GTSFM_ERR_CAPACITY;
+    hipStream_t stream = (hipStream_t)stream_v;
+    const unsigned char* ws = (const unsigned char*)d_workspace;
+    GTSFM_CHECK_HIP(hipMemcpyAsync(h_uncertified, ws + off[7], sizeof(int), hipMemcpyDeviceToHost, stream));
+    if (h_uncertified_per_side && n_pairs)
+        GTSFM_CHECK_HIP(hipMemcpyAsync(h_uncertified_per_side, ws + off[9], 2 * (size_t)n_pairs * sizeof(int),
+                                       hipMemcpyDeviceToHost, stream));
+    GTSFM_CHECK_HIP(hipStreamSynchronize(stream));
+    return GTSFM_OK;
+}
 
 int gtsfm_match_max_group(int kmax, int dim) {
     if (kmax <= 0 || kmax > kMaxKmaxPacked || dim <= 0 || dim > 139) return 0;

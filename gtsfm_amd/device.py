@@ -1,10 +1,12 @@
 """Device-resident batched entry points over the C ABI (include/gtsfm_hip.h).
 
 torch provides HBM allocations and the stream; every computation is a libgtsfm_hip.so kernel. Tensors passed
-in must already live on the GPU; nothing here copies to the host or synchronises.
+in must already live on the GPU; nothing here copies to the host or synchronises (except the measurement hook
+match_pairs(stats=...)).
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Tuple
 
 import numpy as np
@@ -24,7 +26,8 @@ def _workspace(nbytes: int, device: torch.device) -> torch.Tensor:
 def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, ratio: Optional[float],
                 mode: int = native.GTSFM_MATCH_INT_F16, stream: Optional[torch.cuda.Stream] = None,
                 groups: Optional[torch.Tensor] = None,
-                out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                stats: Optional[dict] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Mutual-NN + ratio matching of every (i1, i2) row of `pairs`.
 
     Args:
@@ -37,6 +40,11 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
             every pair exactly once, the pairs of a group sharing image i1 (pair_groups builds one).
         out: optional caller-owned (idx (P, kmax, 2) int32, count (P,) int32) to write into (no allocation: a
             pipelined caller keeps them across steps instead of cycling cross-stream blocks through the allocator).
+        stats: optional dict filled, for GTSFM_MATCH_F16_RERANK with dim <= 256, with the certificate's counts
+            (gtsfm_match_rerank_stats; synchronises the stream): "keypoint_sides" (sum over pairs of both images'
+            counts), "uncertified" and "uncertified_frac" (entries the fp16 shortlist did not certify, recomputed
+            exactly), "tiled_frac" (entries of (pair, side)s recomputed whole by the exact tile kernel) and
+            "rescan_frac" (uncertified entries rescanned one keypoint at a time).
 
     Returns:
         idx: (P, kmax, 2) int32 tensor holding uint32 keypoint indices, rows [0, count) valid per pair.
@@ -69,6 +77,20 @@ def match_pairs(desc: torch.Tensor, counts: torch.Tensor, pairs: torch.Tensor, r
         0 if groups is None else groups.shape[1], -1.0 if ratio is None else float(ratio), mode, _ptr(ws),
         ws.numel(), _ptr(idx), _ptr(cnt), native.stream_handle(stream))
     native.check(rc, "gtsfm_match_batched_grouped")
+    if stats is not None and mode == native.GTSFM_MATCH_F16_RERANK and dim <= 256:
+        unc = np.zeros(2 * n_pairs, dtype=np.int32)
+        n_unc = ctypes.c_int(0)
+        native.check(L.gtsfm_match_rerank_stats(_ptr(ws), ws.numel(), n_img, kmax, dim, n_pairs, ctypes.byref(n_unc),
+                                                unc.ctypes.data, native.stream_handle(stream)),
+                     "gtsfm_match_rerank_stats")
+        c = counts.cpu().numpy().astype(np.int64)
+        pr = pairs.cpu().numpy().astype(np.int64)
+        nq = np.concatenate([c[pr[:, 0]], c[pr[:, 1]]])  # side 0: rows of i1, side 1: rows of i2
+        tiled = (unc > 0) & (unc.astype(np.int64) * 32 >= nq)
+        total = max(int(nq.sum()), 1)
+        stats.update(keypoint_sides=int(nq.sum()), uncertified=int(n_unc.value),
+                     uncertified_frac=int(n_unc.value) / total, tiled_frac=int(nq[tiled].sum()) / total,
+                     rescan_frac=int(unc[~tiled].sum()) / total)
     return idx, cnt
 
 

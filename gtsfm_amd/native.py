@@ -28,7 +28,7 @@ c_size_t = ctypes.c_size_t
 c_uint64 = ctypes.c_uint64
 
 # Mirrors include/gtsfm_hip.h
-ABI_VERSION = 401  # GTSFM_HIP_ABI_VERSION: lib() refuses a library built for another ABI
+ABI_VERSION = 402  # GTSFM_HIP_ABI_VERSION: lib() refuses a library built for another ABI
 GTSFM_OK = 0
 GTSFM_ERR_ARG = -1
 GTSFM_ERR_HIP = -2
@@ -66,6 +66,7 @@ SIGNATURES = {
     ),
     "gtsfm_match_max_group": (c_int, [c_int, c_int]),
     "gtsfm_match_set_kernel_events": (c_int, [c_void_p, c_void_p]),
+    "gtsfm_match_rerank_stats": (c_int, [c_void_p, c_size_t, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "gtsfm_ransac_workspace_bytes": (c_size_t, [c_int, c_int]),
     "gtsfm_ransac_E_batched": (
         c_int,

@@ -41,7 +41,7 @@ extern "C" {
  * ---------------------------------------------------------------------------------------------- */
 /* ABI version (major*100 + minor); a binding built against this header checks that the library
  * returns GTSFM_HIP_ABI_VERSION before binding anything else. */
-#define GTSFM_HIP_ABI_VERSION 401
+#define GTSFM_HIP_ABI_VERSION 402
 int gtsfm_hip_abi_version(void);
 /* Name of the offload target the kernels were compiled for (e.g. "gfx950"). */
 const char* gtsfm_hip_target(void);
@@ -99,6 +99,14 @@ int gtsfm_match_max_group(int kmax, int dim);
  * and after the distance-GEMM kernel of every later GTSFM_MATCH_INT_F16 gtsfm_match_batched call, so a benchmark can
  * time that one kernel. NULL, NULL switches it off. Process-wide; not thread-safe. */
 int gtsfm_match_set_kernel_events(void* hip_event_start, void* hip_event_stop);
+
+/* Measurement hook (no reference counterpart): after a GTSFM_MATCH_F16_RERANK gtsfm_match_batched call (dim <= 256) has
+ * completed on `stream`, the number of (keypoint, side) entries whose fp16 shortlist was not certified (and were
+ * recomputed exactly), and optionally per pair and side (h_uncertified_per_side[side * n_pairs + p], side 0 = rows of
+ * i1). A (pair, side) with at least 1/32 of its keypoints uncertified is recomputed whole by the exact tile kernel,
+ * the rest one keypoint at a time. Same workspace and shape arguments as the call; blocks until the copies land. */
+int gtsfm_match_rerank_stats(const void* d_workspace, size_t workspace_bytes, int n_img, int kmax, int dim,
+                             int n_pairs, int* h_uncertified, int* h_uncertified_per_side, void* stream);
 
 /* ----------------------------------------------------------------------------------------------
  * Verifier: essential-matrix RANSAC over a batch of image pairs (use_intrinsics_in_verification=True path).

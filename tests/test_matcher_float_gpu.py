@@ -170,3 +170,36 @@ def test_clustered_pairs_use_exact_tiles(dev, oracle_mod, dim):
     pairs = [(0, 1), (2, 3), (1, 0), (0, 3), (4, 1), (3, 4)]
     for ratio in (0.8, None):
         _check(dev, oracle_mod, descs, pairs, ratio, n_oracle=3)
+
+
+def test_rerank_certificate_stats(dev):
+    """gtsfm_match_rerank_stats (the C3 bench line's uncertified / rescan fractions): clustered pairs go whole to the
+    exact tiles, planted ones certify nearly everything; the per-side counts add up to the total."""
+    from gtsfm_amd import device, native
+
+    rng = np.random.default_rng(77)
+    centres = _unit(rng, 4, 256)
+    clustered = [(centres[rng.integers(0, 4, n)] + 3e-3 * rng.normal(size=(n, 256)) / 16).astype(np.float32)
+                 for n in (700, 1000)]
+    c, d = _planted(rng, 900, 650, 256)
+    descs = clustered + [c, d]
+    kmax = max(len(x) for x in descs)
+    arr = np.zeros((len(descs), kmax, 256), np.float32)
+    for i, x in enumerate(descs):
+        arr[i, : len(x)] = x
+    cnt = torch.tensor([len(x) for x in descs], dtype=torch.int32, device=dev)
+    desc_t = torch.from_numpy(arr).to(dev)
+    for pairs, clustered_sides in (([(2, 3)], 0), ([(0, 1), (2, 3)], 1700)):
+        st = {}
+        device.match_pairs(desc_t, cnt, torch.tensor(pairs, dtype=torch.int32, device=dev), 0.8,
+                           native.GTSFM_MATCH_F16_RERANK, stats=st)
+        sides = sum(len(descs[i]) + len(descs[j]) for i, j in pairs)
+        assert st["keypoint_sides"] == sides
+        assert 0 <= st["rescan_frac"] <= st["uncertified_frac"] <= 1 and 0 <= st["tiled_frac"] <= 1
+        assert abs(st["tiled_frac"] - clustered_sides / sides) < 1e-9
+        if clustered_sides == 0:
+            assert st["uncertified_frac"] < 0.05
+    st = {}
+    device.match_pairs(desc_t, cnt, torch.tensor([(2, 3)], dtype=torch.int32, device=dev), 0.8,
+                       native.GTSFM_MATCH_EXACT_F32, stats=st)
+    assert st == {}
