@@ -826,6 +826,108 @@ __global__ __launch_bounds__(256) void sk_cols_kernel(const float* __restrict__ 
     }
 }
 
+// One pass over Z per Sinkhorn iteration (kmax <= kSkFusedMaxK): a 64-lane workgroup takes kSkRows rows of one pair,
+// lane l holding columns l + 64 k. Per row: u_i = log_mu - logsumexp_j(Z_ij + v_j) (sk_rows_kernel's grouping and
+// order, so u is unchanged given v), then, from the same registers, each column's running log-sum-exp of Z_ij + u_i
+// over the workgroup's rows; the partials (max, scaled sum) go to `part` and sk_vmerge_kernel turns them into v.
+// Z is read once per iteration instead of twice; the column sums run in another order than sk_cols_kernel's, so v
+// differs from the two-pass form in the last bits (the log-assignment tolerance of tests/test_superglue_gpu.py).
+constexpr int kSkRows = 64, kSkNC = 33, kSkFusedMaxK = 64 * kSkNC - 1;
+__host__ __device__ constexpr int sk_row_blocks(int kmax) { return (kmax + 1 + kSkRows - 1) / kSkRows; }
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void sk_pass_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
+                                                     int kmax, float* __restrict__ u, const float* __restrict__ v,
+                                                     float2* __restrict__ part) {
+    const int p = blockIdx.y, rb = blockIdx.x, lane = threadIdx.x;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    const int i0 = rb * kSkRows;
+    const long ld = kmax + 1;
+    float2* pp = part + ((long)p * sk_row_blocks(kmax) + rb) * ld;
+    if (i0 > m) {  // a block wholly past the rows: an empty partial for every column
+        for (int j = lane; j <= n; j += 64) pp[j] = make_float2(-INFINITY, 0.0f);
+        return;
+    }
+    const float* Zp = Z + (long)p * ld * ld;
+    __shared__ float vj[kSkNC * 64];  // v of the lane's columns (LDS: registers hold the row, its prefetch and partials)
+    float cm[kSkNC], cs[kSkNC];
+#pragma unroll
+    for (int k = 0; k < kSkNC; ++k) {
+        const int j = lane + 64 * k;
+        vj[64 * k + lane] = j <= n ? v[(long)p * ld + j] : 0.0f;
+        cm[k] = -INFINITY;
+        cs[k] = 0.0f;
+    }
+    const float norm = sk_norm(m, n);
+    const int i1 = min(m, i0 + kSkRows - 1);
+    // row i + 1's loads are issued before row i is reduced (a wave's rows are a dependent sequence otherwise)
+    float xn[kSkNC];
+    auto load_row = [&](int i) {
+        const float* row = Zp + (long)min(i, i1) * ld;
+#pragma unroll
+        for (int k = 0; k < kSkNC; ++k) {
+            const int j = lane + 64 * k;
+            xn[k] = j <= n ? row[j] : -INFINITY;
+        }
+    };
+    load_row(i0);
+    for (int i = i0; i <= i1; ++i) {
+        float x[kSkNC];
+#pragma unroll
+        for (int k = 0; k < kSkNC; ++k) x[k] = xn[k];
+        load_row(i + 1);
+        float mx = -INFINITY, s = 0.0f;
+#pragma unroll
+        for (int k0 = 0; k0 < kSkNC; k0 += 4) {
+            float y[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) y[q] = k0 + q < kSkNC ? x[k0 + q] + vj[64 * (k0 + q) + lane] : -INFINITY;
+            lse_push4(y, mx, s);
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            const float mo = __shfl_xor(mx, o), so = __shfl_xor(s, o);
+            lse_merge(mx, s, mo, so);
+        }
+        const float log_mu = i < m ? norm : logf((float)n) + norm;
+        const float ui = log_mu - (logf(s) + mx);
+        if (lane == 0) u[(long)p * ld + i] = ui;
+#pragma unroll
+        for (int k = 0; k < kSkNC; ++k) {
+            const float y = x[k] + ui;
+            const float nm = fmaxf(cm[k], y);
+            if (nm != -INFINITY) {
+                cs[k] = cs[k] * sk_exp(cm[k] - nm) + sk_exp(y - nm);
+                cm[k] = nm;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kSkNC; ++k) {
+        const int j = lane + 64 * k;
+        if (j <= n) pp[j] = make_float2(cm[k], cs[k]);
+    }
+}
+
+// v_j = log_nu - logsumexp over the row blocks' partials of column j (sk_pass_kernel)
+__global__ __launch_bounds__(256) void sk_vmerge_kernel(const float2* __restrict__ part,
+                                                        const int* __restrict__ side_counts, int kmax,
+                                                        float* __restrict__ v) {
+    const int p = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+    const int m = side_counts[2 * p], n = side_counts[2 * p + 1];
+    if (j > n) return;
+    const long ld = kmax + 1;
+    const int nrb = sk_row_blocks(kmax), used = m / kSkRows + 1;
+    const float2* pp = part + (long)p * nrb * ld + j;
+    float mx = -INFINITY, s = 0.0f;
+    for (int r = 0; r < used; ++r) {
+        const float2 q = pp[(long)r * ld];
+        lse_merge(mx, s, q.x, q.y);
+    }
+    const float norm = sk_norm(m, n);
+    const float log_nu = j < n ? norm : logf((float)m) + norm;
+    v[(long)p * ld + j] = log_nu - (logf(s) + mx);
+}
+
 // row-wise max / argmax of the final scores ((Z + u) + v) - norm over the first n columns (first index on ties)
 __global__ __launch_bounds__(256) void sk_rowmax_kernel(const float* __restrict__ Z, const int* __restrict__ side_counts,
                                                         int kmax, const float* __restrict__ u,
@@ -952,7 +1054,7 @@ __global__ __launch_bounds__(256) void sk_final_kernel(const float* __restrict__
 
 // ------------------------------------------------------------------ host-side orchestration
 struct SgLayout {
-    size_t enc_in, X, T1, T2, qkv, kvp, att, msg, hid, Z, u, v, max0, idx0, idx1, cnt, wsplit, total;
+    size_t enc_in, X, T1, T2, qkv, kvp, att, msg, hid, Z, u, v, part, max0, idx0, idx1, cnt, wsplit, total;
 };
 
 // bf16 planes of one GNN layer's four weight matrices (Wqkv, Wm, W1, W2), reused by the final projection
@@ -976,6 +1078,7 @@ __host__ SgLayout sg_layout(int P, int kmax) {
     L.Z = take((size_t)P * ld * ld * 4);
     L.u = take((size_t)P * ld * 4);
     L.v = take((size_t)P * ld * 4);
+    L.part = take((size_t)P * sk_row_blocks(kmax) * ld * sizeof(float2));  // Sinkhorn column partials
     L.max0 = take((size_t)P * kmax * 4);
     L.idx0 = take((size_t)P * kmax * 4);
     L.idx1 = take((size_t)P * kmax * 4);
@@ -1168,15 +1271,27 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
     }
     hipLaunchKernelGGL(sk_init_kernel, dim3((kmax + 256) / 256, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
                        bin, u, v);
-    // Sinkhorn in two passes over Z per iteration. Measured in round 5 and not kept: one pass (a workgroup's 8 rows of
-    // Z in LDS, their row log-sum-exps, then the columns' partial log-sum-exps from LDS, merged by a second small
-    // kernel): 7.35 ms per iteration against 2.09 + 2.01 ms here (profiles/r05l_*): 65 KB of LDS per workgroup and the
-    // load / rows / columns phases in series leave it latency-bound, while these two passes stream Z at ~4 TB/s.
-    for (int it = 0; it < sinkhorn_iters; ++it) {
-        hipLaunchKernelGGL(sk_rows_kernel, dim3((kmax + 4) / 4, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
-                           u, (const float*)v);
-        hipLaunchKernelGGL(sk_cols_kernel, dim3((kmax + 64) / 64, n_pairs), dim3(256), 0, stream, Z, side_counts,
-                           kmax, (const float*)u, v);
+    // Sinkhorn: one pass over Z per iteration (sk_pass_kernel + sk_vmerge_kernel) up to kmax = 2047 + 1 columns per
+    // lane block, else two passes (sk_rows_kernel, sk_cols_kernel). C5 slice match stage 860 -> 826 ms per step, 532
+    // -> 555 pairs/s (profiles/r06m_*). Round 5's one-pass form (a workgroup's 8 rows of Z in LDS, 65 KB, phases in
+    // series) ran 7.35 ms per iteration against 2.09 + 2.01 ms for the two passes; this one keeps the rows and the
+    // column partials in registers (one 64-lane wave per 64 rows, the next row prefetched) and needs no LDS for Z.
+    const char* sk_env = getenv("GTSFM_SG_SINKHORN_TWO_PASS");  // test hook: the two-pass form below
+    if (kmax <= kSkFusedMaxK && !(sk_env && sk_env[0] == '1')) {
+        float2* part = (float2*)(ws + L.part);
+        for (int it = 0; it < sinkhorn_iters; ++it) {
+            hipLaunchKernelGGL(sk_pass_kernel, dim3(sk_row_blocks(kmax), n_pairs), dim3(64), 0, stream, Z,
+                               side_counts, kmax, u, (const float*)v, part);
+            hipLaunchKernelGGL(sk_vmerge_kernel, dim3((kmax + 256) / 256, n_pairs), dim3(256), 0, stream,
+                               (const float2*)part, side_counts, kmax, v);
+        }
+    } else {
+        for (int it = 0; it < sinkhorn_iters; ++it) {
+            hipLaunchKernelGGL(sk_rows_kernel, dim3((kmax + 4) / 4, n_pairs), dim3(256), 0, stream, Z, side_counts,
+                               kmax, u, (const float*)v);
+            hipLaunchKernelGGL(sk_cols_kernel, dim3((kmax + 64) / 64, n_pairs), dim3(256), 0, stream, Z, side_counts,
+                               kmax, (const float*)u, v);
+        }
     }
     hipLaunchKernelGGL(sk_rowmax_kernel, dim3(kmax / 4, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax, u, v,
                        max0, idx0);
