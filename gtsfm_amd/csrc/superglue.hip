@@ -233,8 +233,10 @@ struct Gemm3Args {
     long kv_batch;
 };
 
+// Two LDS staging buffers since round 6 (one barrier per chunk; a chunk's split and stores overlap the MFMAs of the
+// chunk before): C5 slice match stage 826 -> 806 ms per step, TM = 128 launches 3.5 -> 3.27 ms (profiles/r06n_*).
 // KC: K per LDS chunk (16 or 32; rows padded to 40 elements at 32 so the fragment reads stay conflict-free);
-// SLOTS: chunks kept in flight in registers. Measured on the C5 slice (qkv / W1 / Wm+W2 launches of 992 sides):
+// SLOTS: chunks kept in flight in registers (round 5, single LDS buffer). Measured on the C5 slice (qkv / W1 / Wm+W2 launches of 992 sides):
 // <16, 1> 7.05 / 7.57 / 3.45 ms (162 VGPRs, three waves per SIMD), <16, 2> 7.87 / 8.38 / 4.17, <32, 1> 7.40 / 7.76 /
 // 4.04, <32, 2> 10.19 / 10.94 / 5.38: the kernel is bound by LDS fragment traffic (12 16-byte reads per 24 MFMAs per
 // wave), so occupancy beats prefetch depth; <16, 1> is the one launched.
@@ -243,6 +245,11 @@ struct Gemm3Args {
 // (Wm, W2) at 3.69 against 3.53, so run_gemm3 takes 256 for N >= 512.
 constexpr int kG3Kc = 16, kG3Slots = 1;
 constexpr int kG3EpiRow = 72;  // epilogue tile row stride (floats): 4 rows apart = 32 banks apart
+// dynamic LDS bytes of sg_gemm3_kernel<16, 1, TM>: two staging buffers, or the epilogue's four 32 x 72 fp32 tiles
+constexpr int sg_gemm3_lds(int tm) {
+    return (2 * 3 * (tm + kG3Tile) * 16 * 2) > 4 * 32 * kG3EpiRow * 4 ? 2 * 3 * (tm + kG3Tile) * 16 * 2
+                                                                      : 4 * 32 * kG3EpiRow * 4;
+}
 template <int KC, int SLOTS, int TM>
 __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     constexpr int kRow = KC == 16 ? 16 : 40;
@@ -250,10 +257,12 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     constexpr int RA = TM / 128;  // A rows staged per thread
     constexpr int WI = TM / 64;   // 32-row accumulator tiles per wave (2 x 2 waves over TM x 128)
     // staging planes As [3][TM][kRow] | Bs [3][128][kRow], reused by the epilogue's per-wave 32 x 72 fp32 tiles
-    constexpr int kStage = 3 * (TM + kG3Tile) * kRow, kEpi = 4 * 32 * kG3EpiRow * 2;
-    __shared__ __attribute__((aligned(16))) __bf16 smem[kStage > kEpi ? kStage : kEpi];
-    __bf16(*As)[TM][kRow] = reinterpret_cast<__bf16(*)[TM][kRow]>(smem);
-    __bf16(*Bs)[kG3Tile][kRow] = reinterpret_cast<__bf16(*)[kG3Tile][kRow]>(smem + 3 * TM * kRow);
+    // two staging buffers (chunk c in buffer c & 1): one barrier per chunk, and a chunk's split and LDS stores run
+    // while the MFMAs of the chunk before it drain
+    constexpr int kStage = 3 * (TM + kG3Tile) * kRow;
+    extern __shared__ __attribute__((aligned(16))) __bf16 smem[];
+    auto As_of = [&](int b) { return reinterpret_cast<__bf16(*)[TM][kRow]>(smem + b * kStage); };
+    auto Bs_of = [&](int b) { return reinterpret_cast<__bf16(*)[kG3Tile][kRow]>(smem + b * kStage + 3 * TM * kRow); };
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     int bx, by, z;
     xcd_tile(bx, by, z);
@@ -306,8 +315,10 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
             }
         }
     };
-    auto store = [&](auto slot) {
+    auto store = [&](auto slot, int buf) {
         constexpr int q = decltype(slot)::value;
+        __bf16(*As)[TM][kRow] = As_of(buf);
+        __bf16(*Bs)[kG3Tile][kRow] = Bs_of(buf);
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
             bf16x8 h, m, l;
@@ -334,7 +345,9 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     for (int i = 0; i < WI; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-    auto compute = [&]() {
+    auto compute = [&](int buf) {
+        __bf16(*As)[TM][kRow] = As_of(buf);
+        __bf16(*Bs)[kG3Tile][kRow] = Bs_of(buf);
 #pragma unroll
         for (int ks = 0; ks < kU; ++ks) {
             // B fragments for the chunk, then A one row tile at a time (fewer fragments live beside the accumulators)
@@ -363,31 +376,23 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
         }
     };
     using S0 = std::integral_constant<int, 0>;
-    using S1 = std::integral_constant<int, SLOTS - 1>;
+    static_assert(SLOTS == 1, "one chunk in flight in registers, two in LDS");
     load(0, S0{});
-    if constexpr (SLOTS == 2) {
-        if (KC < g.K) load(KC, S1{});
-    }
-    for (int k0 = 0; k0 < g.K; k0 += KC * SLOTS) {
-        __syncthreads();  // the previous chunk's fragments are read
-        store(S0{});
-        __syncthreads();
-        if (k0 + KC * SLOTS < g.K) load(k0 + KC * SLOTS, S0{});
-        compute();
-        if constexpr (SLOTS == 2) {
-            if (k0 + KC >= g.K) break;
-            __syncthreads();
-            store(S1{});
-            __syncthreads();
-            if (k0 + 3 * KC < g.K) load(k0 + 3 * KC, S1{});
-            compute();
+    store(S0{}, 0);
+    if (KC < g.K) load(KC, S0{});
+    __syncthreads();
+    for (int k0 = 0, buf = 0; k0 < g.K; k0 += KC, buf ^= 1) {
+        compute(buf);
+        if (k0 + KC < g.K) {
+            store(S0{}, buf ^ 1);  // chunk k0 + KC (buffer buf ^ 1 was last read by chunk k0 - KC's MFMAs)
+            if (k0 + 2 * KC < g.K) load(k0 + 2 * KC, S0{});
         }
+        __syncthreads();  // chunk k0 + KC staged; everyone done reading buffer buf
     }
     // epilogue through LDS, one 32-row accumulator tile at a time: the wave parks tile i (32 x 64 fp32, rows padded
     // to 72 floats: conflict-free both ways) in the staging buffers and then walks it with lane = column, so no
     // unrolled per-register epilogue sits beside the live accumulators
-    __syncthreads();  // every wave is done with As / Bs
-    float* T = (float*)smem + wave * 32 * kG3EpiRow;
+    float* T = (float*)smem + wave * 32 * kG3EpiRow;  // (the loop's last barrier: every wave is done with the stages)
     const int col = lane, n = n0 + 64 * wn + col;
     const bool n_ok = n < Nv;
     const float bb = n_ok && g.bias ? g.bias[n] : 0.0f;
@@ -1097,11 +1102,17 @@ hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
 hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
     if (g.kv && (g.m_lim || g.M % 64 != 0)) return hipErrorInvalidValue;  // kv stores write whole 4-key groups
     if (g.N >= 512) {
+        const void* fn = (const void*)sg_gemm3_kernel<kG3Kc, kG3Slots, 256>;
+        const int lds = sg_gemm3_lds(256);
+        if (gtsfm_set_dynamic_lds(fn, lds) != hipSuccess) return hipErrorInvalidValue;
         const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + 255) / 256), (unsigned)batches);
-        hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 256>), grid, dim3(256), 0, stream, g);
+        hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 256>), grid, dim3(256), lds, stream, g);
     } else {
+        const void* fn = (const void*)sg_gemm3_kernel<kG3Kc, kG3Slots, 128>;
+        const int lds = sg_gemm3_lds(128);
+        if (gtsfm_set_dynamic_lds(fn, lds) != hipSuccess) return hipErrorInvalidValue;
         const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + 127) / 128), (unsigned)batches);
-        hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 128>), grid, dim3(256), 0, stream, g);
+        hipLaunchKernelGGL((sg_gemm3_kernel<kG3Kc, kG3Slots, 128>), grid, dim3(256), lds, stream, g);
     }
     return hipGetLastError();
 }
@@ -1271,8 +1282,8 @@ int gtsfm_superglue_batched(const float* d_kp, const float* d_scores, const floa
     }
     hipLaunchKernelGGL(sk_init_kernel, dim3((kmax + 256) / 256, n_pairs), dim3(256), 0, stream, Z, side_counts, kmax,
                        bin, u, v);
-    // Sinkhorn: one pass over Z per iteration (sk_pass_kernel + sk_vmerge_kernel) up to kmax = 2047 + 1 columns per
-    // lane block, else two passes (sk_rows_kernel, sk_cols_kernel). C5 slice match stage 860 -> 826 ms per step, 532
+    // Sinkhorn: one pass over Z per iteration (sk_pass_kernel + sk_vmerge_kernel) for kmax <= 2048 (33 columns per
+    // lane), else two passes (sk_rows_kernel, sk_cols_kernel). C5 slice match stage 860 -> 826 ms per step, 532
     // -> 555 pairs/s (profiles/r06m_*). Round 5's one-pass form (a workgroup's 8 rows of Z in LDS, 65 KB, phases in
     // series) ran 7.35 ms per iteration against 2.09 + 2.01 ms for the two passes; this one keeps the rows and the
     // column partials in registers (one 64-lane wave per 64 rows, the next row prefetched) and needs no LDS for Z.
