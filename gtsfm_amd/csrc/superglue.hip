@@ -250,6 +250,95 @@ constexpr int sg_gemm3_lds(int tm) {
     return (2 * 3 * (tm + kG3Tile) * 16 * 2) > 4 * 32 * kG3EpiRow * 4 ? 2 * 3 * (tm + kG3Tile) * 16 * 2
                                                                       : 4 * 32 * kG3EpiRow * 4;
 }
+// Epilogue of the split GEMMs through LDS, one 32-row accumulator tile at a time: the wave parks tile i (32 x 64 fp32,
+// rows padded to 72 floats: conflict-free both ways) in the (free) staging LDS and walks it with lane = column, so no
+// unrolled per-register epilogue sits beside the live accumulators. The caller has retired every staging access.
+template <int TM>
+__device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, f32x16 (&acc)[TM / 64][2], float* smemf, int wave,
+                                            int lane, int m0, int n0, int Mv, int Nv, int z) {
+    constexpr int WI = TM / 64;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r = lane & 31, hk = lane >> 5;
+    float* T = smemf + wave * 32 * kG3EpiRow;
+    const int col = lane, n = n0 + 64 * wn + col;
+    const bool n_ok = n < Nv;
+    const float bb = n_ok && g.bias ? g.bias[n] : 0.0f;
+    const float sc = n_ok && g.bn_scale ? g.bn_scale[n] : 1.0f;
+    const float sh = n_ok && g.bn_shift ? g.bn_shift[n] : 0.0f;
+    // values (q/k/v projection, n >= 512) go to the transposed planes [..][dim][key] (four consecutive keys per
+    // 8-byte store); keys (256 <= n < 512) to [..][key][dim] (lanes along the dimension)
+    const bool vt = g.kv && n >= 2 * kD, kt = g.kv && n >= kD && n < 2 * kD;
+    auto post = [&](float v) {
+        v = v + bb;
+        if (g.bn_scale) v = v * sc + sh;
+        if (g.relu) v = v > 0.0f ? v : 0.0f;
+        if (g.alpha != 1.0f) v = v * g.alpha;
+        return v;
+    };
+#pragma unroll
+    for (int i = 0; i < WI; ++i) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int k = 0; k < 16; ++k) T[(8 * (k >> 2) + 4 * hk + (k & 3)) * kG3EpiRow + 32 * j + r] = acc[i][j][k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the tile's first row. M is a multiple of 64; Mv is M unless m_lim is set (the score GEMM), which kv mode
+        // never sets (run_gemm3 rejects it): the V^T path's four-key stores below assume Mv == M
+        const int mt = m0 + (TM / 2) * wm + 32 * i;
+        if (n_ok && mt < Mv) {
+            if (vt) {
+                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+                const int d = n - 2 * kD, hh = d / kHd, dd = d % kHd;
+                __bf16* base = g.kv + z * g.kv_batch + (long)3 * kD * g.M;
+#pragma unroll 2
+                for (int rg = 0; rg < 8; ++rg) {
+                    const int mg = mt + 4 * rg;
+                    if (mg >= Mv) break;
+                    bf16x4 pl[3];
+#pragma unroll
+                    for (int e4 = 0; e4 < 4; ++e4) {
+                        __bf16 h0, h1, h2;
+                        split3(post(T[(4 * rg + e4) * kG3EpiRow + col]), h0, h1, h2);
+                        pl[0][e4] = h0;
+                        pl[1][e4] = h1;
+                        pl[2][e4] = h2;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 3; ++q)
+                        *(bf16x4*)(base + (((long)q * kHeads + hh) * kHd + dd) * g.M + mg) = pl[q];
+                }
+            } else if (kt) {
+                const int d = n - kD, hh = d / kHd, dd = d % kHd;
+                __bf16* base = g.kv + z * g.kv_batch;
+#pragma unroll 4
+                for (int row = 0; row < 32; ++row) {
+                    const int m = mt + row;
+                    if (m >= Mv) break;
+                    __bf16 pl[3];
+                    split3(post(T[row * kG3EpiRow + col]), pl[0], pl[1], pl[2]);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
+                }
+            } else {
+                float* C = g.C + z * g.c_batch + n;
+#pragma unroll 4
+                for (int row = 0; row < 32; ++row) {
+                    const int m = mt + row;
+                    if (m >= Mv) break;
+                    const float v = post(T[row * kG3EpiRow + col]);
+                    float* c = C + (long)m * g.ldc;
+                    *c = g.residual ? *c + v : v;
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();  // the tile is read before the next one overwrites it
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 template <int KC, int SLOTS, int TM>
 __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
     constexpr int kRow = KC == 16 ? 16 : 40;
@@ -389,87 +478,140 @@ __global__ __launch_bounds__(256, 2) void sg_gemm3_kernel(Gemm3Args g) {
         }
         __syncthreads();  // chunk k0 + KC staged; everyone done reading buffer buf
     }
-    // epilogue through LDS, one 32-row accumulator tile at a time: the wave parks tile i (32 x 64 fp32, rows padded
-    // to 72 floats: conflict-free both ways) in the staging buffers and then walks it with lane = column, so no
-    // unrolled per-register epilogue sits beside the live accumulators
-    float* T = (float*)smem + wave * 32 * kG3EpiRow;  // (the loop's last barrier: every wave is done with the stages)
-    const int col = lane, n = n0 + 64 * wn + col;
-    const bool n_ok = n < Nv;
-    const float bb = n_ok && g.bias ? g.bias[n] : 0.0f;
-    const float sc = n_ok && g.bn_scale ? g.bn_scale[n] : 1.0f;
-    const float sh = n_ok && g.bn_shift ? g.bn_shift[n] : 0.0f;
-    // values (q/k/v projection, n >= 512) go to the transposed planes [..][dim][key] (four consecutive keys per
-    // 8-byte store); keys (256 <= n < 512) to [..][key][dim] (lanes along the dimension)
-    const bool vt = g.kv && n >= 2 * kD, kt = g.kv && n >= kD && n < 2 * kD;
-    auto post = [&](float v) {
-        v = v + bb;
-        if (g.bn_scale) v = v * sc + sh;
-        if (g.relu) v = v > 0.0f ? v : 0.0f;
-        if (g.alpha != 1.0f) v = v * g.alpha;
-        return v;
+    g3_epilogue<TM>(g, acc, (float*)smem, wave, lane, m0, n0, Mv, Nv, z);  // (the loop's last barrier: stages free)
+}
+
+// The same products with the operands staged by LDS-DMA (round 6), for the weight GEMMs (B = pre-split planes, A
+// fp32 rows): per 16-deep K chunk every wave issues five global_load_lds_dwordx4 pieces of 1 KiB (A: 128 rows x 64 B in
+// eight pieces of 16 rows; B: three planes x 128 columns x 32 B in twelve pieces of 32 columns), S chunks in flight in
+// an S-buffer LDS ring, waits counted (every chunk issues its five pieces, past the last chunk the last one again into
+// the free buffer) and a raw s_barrier per chunk (__syncthreads would drain the ring). A stays fp32 in LDS and is split
+// into its three planes on the fragment read -- the split3x8 of the staged form, on the same eight consecutive values,
+// so the planes, the MFMA sequence and every output are bit-identical to sg_gemm3_kernel. The LDS image is
+// lane-linear per piece (the DMA's destination is base + 16 lane), so the conflict-free layouts come from the source
+// addresses: A row r's 16-byte unit q sits at slot q ^ ((r >> 2) & 3) of its 64-byte row, B column c's half h at slot
+// h ^ ((c >> 3) & 1) of its 32 bytes (ds_read_b128 serves lanes {0-3, 12-15, 20-27}, ... together: 16 distinct
+// 4-bank groups either way).
+__host__ __device__ constexpr int sg_gemm3d_pieces(int tm) { return tm / 64 + 3; }  // per wave per chunk (A, B)
+__host__ __device__ constexpr int sg_gemm3d_lds(int tm, int stages) {
+    return stages * (tm * 16 * 4 + 3 * kG3Tile * 16 * 2) > 4 * 32 * kG3EpiRow * 4
+               ? stages * (tm * 16 * 4 + 3 * kG3Tile * 16 * 2)
+               : 4 * 32 * kG3EpiRow * 4;
+}
+
+template <int TM, int S>
+__global__ __launch_bounds__(256, 2) void sg_gemm3d_kernel(Gemm3Args g) {
+    constexpr int WI = TM / 64, RA = TM / 64;  // accumulator row tiles per wave; A pieces per wave
+    constexpr int kA = TM * 16 * 4, kB = 3 * kG3Tile * 16 * 2, kStage = kA + kB;  // bytes
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem8[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int bx, by, z;
+    xcd_tile(bx, by, z);
+    const int m0 = by * TM, n0 = bx * kG3Tile;
+    int Mv = g.M, Nv = g.N;
+    if (g.m_lim) Mv = min(Mv, g.m_lim[z * g.lim_stride]);
+    if (g.n_lim) Nv = min(Nv, g.n_lim[z * g.lim_stride + 1]);
+    if (m0 >= Mv || n0 >= Nv) return;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r = lane & 31, hk = lane >> 5;
+    const int nk = g.K / 16;
+    // this lane's source in each of the wave's pieces: (row, unit) of A, (plane, column, half) of B, clamped into the
+    // matrix (rows / columns past it are staged but never stored)
+    int a_row[RA], a_q[RA], b_pl[3], b_col[3], b_h[3];
+#pragma unroll
+    for (int t = 0; t < RA; ++t) {
+        const int row = 16 * (RA * wave + t) + (lane >> 2);
+        a_row[t] = min(m0 + row, g.M - 1);
+        a_q[t] = (lane & 3) ^ ((row >> 2) & 3);
+    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        const int pc = 3 * wave + t;  // piece 0..11: plane pc / 4, columns 32 (pc % 4) ..
+        const int col = 32 * (pc % 4) + (lane >> 1);
+        b_pl[t] = pc / 4;
+        b_col[t] = min(n0 + col, g.N - 1);
+        b_h[t] = (lane & 1) ^ ((col >> 3) & 1);
+    }
+    const float* Az = g.A + z * g.a_batch;
+    const float* A2z = g.A2 ? g.A2 + z * g.a2_batch : nullptr;
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)smem8;
+    auto issue = [&](int c, int buf) {
+        const int k0 = 16 * c;
+        const bool second = k0 >= g.Ksplit;
+        const float* abase = second ? A2z : Az;
+        const long alda = second ? g.lda2 : g.lda;
+        const int ak = second ? k0 - g.Ksplit : k0;
+        const uint32_t stage = lds_base + (uint32_t)(buf * kStage);
+#pragma unroll
+        for (int t = 0; t < RA; ++t) {
+            const uint32_t off = (uint32_t)(((long)a_row[t] * alda + ak + 4 * a_q[t]) * 4);
+            const uint32_t la = __builtin_amdgcn_readfirstlane(stage + 1024u * (RA * wave + t));
+            asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(abase), "{m0}"(la) : "memory");
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const uint32_t off = (uint32_t)((((long)b_pl[t] * g.N + b_col[t]) * g.K + k0 + 8 * b_h[t]) * 2);
+            const uint32_t la = __builtin_amdgcn_readfirstlane(stage + kA + 1024u * (3 * wave + t));
+            asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off), "s"(g.Bp), "{m0}"(la) : "memory");
+        }
     };
+    f32x16 acc[WI][2];
 #pragma unroll
-    for (int i = 0; i < WI; ++i) {
+    for (int i = 0; i < WI; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
+    auto compute = [&](int buf) {
+        const unsigned char* st = smem8 + buf * kStage;
+        bf16x8 b[3][2];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) T[(8 * (k >> 2) + 4 * hk + (k & 3)) * kG3EpiRow + 32 * j + r] = acc[i][j][k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the tile's first row. M is a multiple of 64; Mv is M unless m_lim is set (the score GEMM), which kv mode
-        // never sets (run_gemm3 rejects it): the V^T path's four-key stores below assume Mv == M
-        const int mt = m0 + (TM / 2) * wm + 32 * i;
-        if (n_ok && mt < Mv) {
-            if (vt) {
-                typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-                const int d = n - 2 * kD, hh = d / kHd, dd = d % kHd;
-                __bf16* base = g.kv + z * g.kv_batch + (long)3 * kD * g.M;
-#pragma unroll 2
-                for (int rg = 0; rg < 8; ++rg) {
-                    const int mg = mt + 4 * rg;
-                    if (mg >= Mv) break;
-                    bf16x4 pl[3];
+        for (int p = 0; p < 3; ++p)
 #pragma unroll
-                    for (int e4 = 0; e4 < 4; ++e4) {
-                        __bf16 h0, h1, h2;
-                        split3(post(T[(4 * rg + e4) * kG3EpiRow + col]), h0, h1, h2);
-                        pl[0][e4] = h0;
-                        pl[1][e4] = h1;
-                        pl[2][e4] = h2;
-                    }
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int col = 64 * wn + 32 * s2 + r;  // piece 4 p + col / 32, slot 2 (col % 32) + half
+                b[p][s2] = *(const bf16x8*)(st + kA + 1024 * (4 * p + (col >> 5)) +
+                                            16 * (2 * (col & 31) + (hk ^ ((col >> 3) & 1))));
+            }
 #pragma unroll
-                    for (int q = 0; q < 3; ++q)
-                        *(bf16x4*)(base + (((long)q * kHeads + hh) * kHd + dd) * g.M + mg) = pl[q];
-                }
-            } else if (kt) {
-                const int d = n - kD, hh = d / kHd, dd = d % kHd;
-                __bf16* base = g.kv + z * g.kv_batch;
-#pragma unroll 4
-                for (int row = 0; row < 32; ++row) {
-                    const int m = mt + row;
-                    if (m >= Mv) break;
-                    __bf16 pl[3];
-                    split3(post(T[row * kG3EpiRow + col]), pl[0], pl[1], pl[2]);
+        for (int i = 0; i < WI; ++i) {
+            const int row = (TM / 2) * wm + 32 * i + r;
+            const int f = (row >> 2) & 3;
+            const f32x4_t lo = *(const f32x4_t*)(st + 64 * row + 16 * ((2 * hk) ^ f));
+            const f32x4_t hi = *(const f32x4_t*)(st + 64 * row + 16 * ((2 * hk + 1) ^ f));
+            bf16x8 a[3];
+            split3x8(lo, hi, a[0], a[1], a[2]);
 #pragma unroll
-                    for (int q = 0; q < 3; ++q) base[(((long)q * kHeads + hh) * g.M + m) * kHd + dd] = pl[q];
-                }
-            } else {
-                float* C = g.C + z * g.c_batch + n;
-#pragma unroll 4
-                for (int row = 0; row < 32; ++row) {
-                    const int m = mt + row;
-                    if (m >= Mv) break;
-                    const float v = post(T[row * kG3EpiRow + col]);
-                    float* c = C + (long)m * g.ldc;
-                    *c = g.residual ? *c + v : v;
-                }
+            for (int j = 0; j < 2; ++j) {
+                f32x16 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0][j], c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0][j], c, 0, 0, 0);
+                acc[i][j] = c;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();  // the tile is read before the next one overwrites it
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    // chunks 0 .. S - 2 in flight before the loop; chunk c + S - 1 issued at chunk c (the last chunk again past the end)
+#pragma unroll
+    for (int c = 0; c < S - 1; ++c) issue(min(c, nk - 1), c);
+    for (int c = 0; c < nk; ++c) {
+        const int buf = c % S;
+        // this wave's pieces of chunk c landed: (S - 2) later chunks' pieces may stay in flight
+        if constexpr (S == 2)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(sg_gemm3d_pieces(TM) * (S - 2)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of chunk c landed; chunk c - 1's buffer is free
+        asm volatile("" ::: "memory");
+        issue(min(c + S - 1, nk - 1), (c + S - 1) % S);
+        compute(buf);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing reloads land before the LDS is reused
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    g3_epilogue<TM>(g, acc, (float*)smem8, wave, lane, m0, n0, Mv, Nv, z);
 }
 
 // W^T[K][N] fp32 (row-major, the packed layout) -> [3][N][K] bf16 planes for sg_gemm3_kernel; up to four matrices
@@ -1101,6 +1243,31 @@ hipError_t run_gemm(const GemmArgs& g, int batches, hipStream_t stream) {
 
 hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
     if (g.kv && (g.m_lim || g.M % 64 != 0)) return hipErrorInvalidValue;  // kv stores write whole 4-key groups
+    // LDS-DMA staging (sg_gemm3d_kernel) for the weight GEMMs whose A rows are 16-byte aligned: 256-row tiles for N >=
+    // 512, else 128, two chunks in flight. C5 slice, same box (profiles/r06p_*): q/k/v + W1 7.20 -> 6.58 ms, Wm + W2
+    // 3.35 -> 2.72 ms per launch, 551 -> 574 pairs/s (128-row tiles throughout: 563; three chunks in flight: 542).
+    // GTSFM_SG_GEMM_DMA (test and A/B hooks): 0 the register-staged kernel, 2 / 3 128-row tiles with 2 / 3 chunks.
+    const char* dma_env = getenv("GTSFM_SG_GEMM_DMA");
+    const char dma_mode = dma_env && dma_env[0] ? dma_env[0] : '4';
+    const bool aligned = g.lda % 4 == 0 && ((uintptr_t)g.A & 15) == 0 &&
+                         (!g.A2 || (g.lda2 % 4 == 0 && ((uintptr_t)g.A2 & 15) == 0)) && g.Ksplit % 16 == 0;
+    if (dma_mode != '0' && g.Bp && aligned && g.K % 16 == 0) {
+        // '2' / '3': 128-row tiles, 2 / 3 chunks in flight; '4': 256-row tiles for N >= 512, 2 chunks
+        const bool wide = dma_mode == '4' && g.N >= 512;
+        const int tm = wide ? 256 : 128, stages = dma_mode == '3' ? 3 : 2;
+        const dim3 grid((unsigned)((g.N + kG3Tile - 1) / kG3Tile), (unsigned)((g.M + tm - 1) / tm), (unsigned)batches);
+        const void* fn = wide ? (const void*)sg_gemm3d_kernel<256, 2>
+                              : (stages == 2 ? (const void*)sg_gemm3d_kernel<128, 2> : (const void*)sg_gemm3d_kernel<128, 3>);
+        const int lds = sg_gemm3d_lds(tm, stages);
+        if (gtsfm_set_dynamic_lds(fn, lds) != hipSuccess) return hipErrorInvalidValue;
+        if (wide)
+            hipLaunchKernelGGL((sg_gemm3d_kernel<256, 2>), grid, dim3(256), lds, stream, g);
+        else if (stages == 2)
+            hipLaunchKernelGGL((sg_gemm3d_kernel<128, 2>), grid, dim3(256), lds, stream, g);
+        else
+            hipLaunchKernelGGL((sg_gemm3d_kernel<128, 3>), grid, dim3(256), lds, stream, g);
+        return hipGetLastError();
+    }
     if (g.N >= 512) {
         const void* fn = (const void*)sg_gemm3_kernel<kG3Kc, kG3Slots, 256>;
         const int lds = sg_gemm3_lds(256);

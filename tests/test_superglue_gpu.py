@@ -206,3 +206,39 @@ def test_fused_sinkhorn_equals_two_pass(matcher, golden, monkeypatch):
         live = zb > -20
         np.testing.assert_allclose(za[live], zb[live], atol=1e-4)
         np.testing.assert_array_equal(ma, mb)
+
+
+@pytest.mark.parametrize("mode", ["2", "3", "4"])
+def test_dma_staged_gemm_bit_identical(matcher, golden, monkeypatch, mode):
+    """The weight GEMMs staged by LDS-DMA (sg_gemm3d_kernel: 128-row tiles with 2 or 3 chunks in flight, or 256-row
+    tiles; GTSFM_SG_GEMM_DMA) split A on
+    the fragment read with the staged kernel's split3x8 and run the same MFMA sequence, so the whole network's output
+    (log-assignment, matches, scores) is identical bit for bit to the register-staged kernel (GTSFM_SG_GEMM_DMA=0), on
+    C5's 2048 x 2048 and on a ragged pair."""
+    from gtsfm_amd import device, native
+
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    res = {}
+    for m in ("0", mode):
+        monkeypatch.setenv("GTSFM_SG_GEMM_DMA", m)
+        out = []
+        for name in ("c5_2048x2048", "mid_700x650"):
+            kp0, kp1, d0, d1, shape, _ = _case(golden, name)
+            n0, n1 = len(kp0), len(kp1)
+            kmax = (max(n0, n1) + 63) // 64 * 64
+            kp = np.zeros((2, kmax, 2), np.float32)
+            sc = np.zeros((2, kmax), np.float32)
+            de = np.zeros((2, kmax, 256), np.float32)
+            kp[0, :n0], kp[1, :n1] = kp0.coordinates, kp1.coordinates
+            sc[0, :n0], sc[1, :n1] = kp0.responses, kp1.responses
+            de[0, :n0], de[1, :n1] = d0, d1
+            ws = torch.empty(native.lib().gtsfm_superglue_workspace_bytes(1, kmax), dtype=torch.uint8, device="cuda")
+            idx, cnt, ms = device.superglue_match(t(kp), t(sc), t(de), t(np.array([n0, n1], np.int32)),
+                                                  t(np.array([shape[:2], shape[:2]], np.int32)),
+                                                  t(np.array([[0, 1]], np.int32)), matcher.weights(), workspace=ws)
+            Z = device.superglue_log_assignment(ws, 1, kmax, 0).cpu().numpy()[: n0 + 1, : n1 + 1]
+            out.append((Z, idx[0, : int(cnt[0])].cpu().numpy(), ms[0, :n0].cpu().numpy()))
+        res[m] = out
+    for a, b in zip(res["0"], res[mode]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
