@@ -1247,6 +1247,9 @@ hipError_t run_gemm3(const Gemm3Args& g, int batches, hipStream_t stream) {
     // 512, else 128, two chunks in flight. C5 slice, same box (profiles/r06p_*): q/k/v + W1 7.20 -> 6.58 ms, Wm + W2
     // 3.35 -> 2.72 ms per launch, 551 -> 574 pairs/s (128-row tiles throughout: 563; three chunks in flight: 542).
     // GTSFM_SG_GEMM_DMA (test and A/B hooks): 0 the register-staged kernel, 2 / 3 128-row tiles with 2 / 3 chunks.
+    // Measured and not kept (profiles/r06q_*): the GNN's A operands pre-split into bf16 planes by their producers
+    // (attention / GEMM epilogues) and staged as planes, no split in the loop: bit-identical but 7.54 / 3.82 ms per
+    // launch against 6.39 / 2.70 -- 1.5x the operand bytes and a third more LDS-DMA pieces cost more than the split.
     const char* dma_env = getenv("GTSFM_SG_GEMM_DMA");
     const char dma_mode = dma_env && dma_env[0] ? dma_env[0] : '4';
     const bool aligned = g.lda % 4 == 0 && ((uintptr_t)g.A & 15) == 0 &&
