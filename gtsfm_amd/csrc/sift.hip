@@ -1205,12 +1205,15 @@ __global__ __launch_bounds__(64 * kExWaves) void extrema_kernel(GaussSet G, int 
     // refine the block's own candidates now, while the strip's Gaussian rows are still in L2 (a separate pass
     // re-fetched each candidate's 3x3x3 window from HBM)
     // (entries dealt round-robin to the waves: a short list keeps every wave busy on the dependent gathers)
+#ifndef GTSFM_ABL_NO_REFINE  // timing ablation (tools/build_variants_src.sh): candidates found, not refined. C2
+    // octave 0 (r06, profiles/r06s_*): 5.03 ms with the refinement, 4.15 without -- the sweep is the cost
     for (int base0 = 0; base0 < n; base0 += 64 * kExWaves) {
         const int i = base0 + lane * kExWaves + wave;
         Refined res;
         const bool keep = i < n && refine_one(list[i], G, H, W, seen, res);
         append_refined(keep, res, out, n_out, out_cap);
     }
+#endif
 }
 
 // Candidates left in the kCandShards global segments (extrema blocks whose LDS list overflowed) are refined here.
