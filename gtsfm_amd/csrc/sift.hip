@@ -1012,10 +1012,16 @@ __device__ __forceinline__ void append_refined(bool keep, const Refined& res, Re
 // levels' 24. Measured in round 5 and not kept: windows of 64 outputs aligned to 128-B lines, the halo columns
 // loaded separately (lanes 0 / 63 take them through the DPP's old operand): bit-exact, but 366 vs 367 us per launch
 // with the same FETCH_SIZE (the straddled lines are L2 hits) and 103 instead of 79 VGPRs (profiles/r05d_*).
-constexpr int kExWaves = 4, kExOut = 62, kExStrip = 72;
+#ifndef GTSFM_EX_STRIP
+#define GTSFM_EX_STRIP 72
+#endif
+#ifndef GTSFM_EX_AHEAD
+#define GTSFM_EX_AHEAD 6
+#endif
+constexpr int kExWaves = 4, kExOut = 62, kExStrip = GTSFM_EX_STRIP;
 // rows of loads in flight per wave (a multiple of 3 dividing kExStrip): 6 / 9 / 12 measured 4.98 / 5.08 / 5.10 ms for
 // octave 0 beside the next octave's blurs (profiles/r05at_*): the sweep is not waiting on its prefetch depth
-constexpr int kExAhead = 6;
+constexpr int kExAhead = GTSFM_EX_AHEAD;
 static_assert(kExAhead % 3 == 0 && kExStrip % kExAhead == 0, "row slots rotate by 3 within a strip");
 // Candidate list sharded over kCandShards counters/segments (one global atomic per block on one of 256 counters).
 constexpr int kCandShards = 256;
@@ -1556,7 +1562,14 @@ __global__ __launch_bounds__(kTopkThreads) void topk_kernel(const KeyRec* __rest
 }
 
 // ------------------------------------------------------------------ descriptors: one wave per kept keypoint
-constexpr int kDescChunk = 512;
+#ifndef GTSFM_DESC_CHUNK
+#define GTSFM_DESC_CHUNK 512
+#endif
+#ifndef GTSFM_DESC_COPIES
+#define GTSFM_DESC_COPIES 2
+#endif
+constexpr int kDescChunk = GTSFM_DESC_CHUNK;
+static_assert(kDescChunk >= 128 && kDescChunk % 64 == 0, "the descriptor's 128 values reuse the sample list");
 
 __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict__ kps, int kp_cap,
                                                         const int* __restrict__ sel, const int* __restrict__ n_sel,
@@ -1566,10 +1579,10 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
     constexpr int d = 4, n = 8, HB = (d + 2) * (d + 2) * (n + 2);
     // kCopies private histograms (lane & 1 picks one): adjacent samples usually land in the same bins, and same-address
     // LDS atomics of one instruction serialise. Integer (fixed-point) sums, so merging the copies is exact.
-    constexpr int kCopies = 2, HBP = HB + 1;  // +1: copies start on different banks
+    constexpr int kCopies = GTSFM_DESC_COPIES, HBP = HB + 1;  // +1: copies start on different banks
     __shared__ unsigned long long hist[kCopies * HBP];
     __shared__ int slist[kDescChunk];  // valid samples of the current chunk, (i << 16) | (j & 0xffff)
-    __shared__ float dst[128];
+    float* const dst = (float*)slist;  // the finished descriptor (the sample list is dead by then)
     __shared__ float dnorm;
     const int lane = threadIdx.x;
     for (int slot = blockIdx.x; slot < n_img * max_kpts; slot += gridDim.x) {
@@ -1645,6 +1658,9 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
                 g[2] = p[-W];
                 g[3] = p[W];
             };
+#ifdef GTSFM_ABL_DESC_NOATOM
+            unsigned abl_acc = 0;
+#endif
             float gn[4];
             int svn = 0;
             if (nit > 0) taps(lane * nit, gn, svn);
@@ -1689,7 +1705,13 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             // stay below 255 every fixed-point value is below 2^32 and is the single truncating conversion
             // (uint32_t)(v 2^24) -- the same integer as to_fix_nn, at a third of its instructions
             auto put = [&](int at, float v, bool small) {
+#if defined(GTSFM_ABL_DESC_U32)  // timing ablation only (wrong sums): 32-bit LDS atomics
+                atomicAdd((unsigned*)&hc[at], (uint32_t)v);
+#elif defined(GTSFM_ABL_DESC_NOATOM)  // timing ablation only (wrong sums): one register sum, no atomics
+                abl_acc += (uint32_t)v + (unsigned)at;
+#else
                 atomicAdd(&hc[at], small ? (unsigned long long)(uint32_t)v : to_fix_scaled(v));
+#endif
             };
             auto put8 = [&](bool small) {
                 put(idx, v_rco000, small);
@@ -1706,6 +1728,9 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             else
                 put8(false);
             }
+#ifdef GTSFM_ABL_DESC_NOATOM
+            atomicAdd((unsigned*)&hc[lane], abl_acc);
+#endif
             __syncthreads();  // slist is rewritten by the next chunk
         }
         // finalisation: the element-wise steps run one element per lane, the two norms are sequential sums in the
@@ -1962,6 +1987,9 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
             sides[dev] = st;
         }
         side = sides[dev];
+        // GTSFM_SIFT_SERIAL=1 (profiling hook): detection on the caller's stream, so every kernel runs alone
+        const char* serial = getenv("GTSFM_SIFT_SERIAL");
+        if (serial && serial[0] == '1') side = stream;
         ev = evs[dev];
     }
     // an error inside the octave loop still joins the side stream's work to the caller's stream
@@ -2068,7 +2096,9 @@ int gtsfm_sift_batched(const uint8_t* d_images, const uint8_t* d_masks, int n_im
     // real inputs; GTSFM_SIFT_DESC_WIDE=1 forces it for every sample so that tests can pin it against the oracle.
     const char* wide = getenv("GTSFM_SIFT_DESC_WIDE");
     const float narrow_below = (wide && wide[0] == '1') ? 0.f : 255.f;
-    hipLaunchKernelGGL(descriptor_kernel, dim3(min(B * max_kpts, 16384)), dim3(64), 0, stream,
+    // one workgroup per output row: the dispatcher balances the keypoints (a grid-stride loop over 16384 workgroups
+    // ended on a partial last round: C2 2131 -> 1975 us, profiles/r06v_*)
+    hipLaunchKernelGGL(descriptor_kernel, dim3(B * max_kpts), dim3(64), 0, stream,
                        (const KeyRec*)(ws + L.kps), kKpCapPerImg, (const int*)(ws + L.sel), d_counts, B, max_kpts, T,
                        narrow_below, d_xy, d_attr, d_desc);
     GTSFM_CHECK_HIP(hipGetLastError());
