@@ -1,5 +1,5 @@
 """Kernel time of the last front-end step in a rocprofv3 kernel_trace.csv: from the last launch of the anchor kernel
-(default: the u8 base blur, the first SIFT kernel of an extraction) to the end of the trace, per kernel name (count,
+(default: the first SIFT kernel of an extraction, gray_pad_kernel or the u8 base blur) to the end of the trace, per kernel name (count,
 busy ms) plus the idle gaps between consecutive kernels.
 
     python tools/step_trace.py <kernel_trace.csv> [anchor] [end_anchor]
@@ -9,7 +9,9 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-anchor = sys.argv[2] if len(sys.argv) > 2 else "blur2d_kernel<5, true>"
+anchor = sys.argv[2] if len(sys.argv) > 2 else None
+if anchor is None:  # the first SIFT kernel of an extraction: the gray staging (round 6), else the u8 base blur
+    anchor = "gray_pad_kernel" if any("gray_pad_kernel" in r["Kernel_Name"] for r in rows) else "blur2d_kernel<5, true>"
 starts = [i for i, r in enumerate(rows) if anchor in r["Kernel_Name"]]
 i0 = starts[-2] if len(starts) > 1 else starts[-1]  # the last full step (the final one may be instrumented)
 i1 = starts[-1] if len(starts) > 1 else len(rows)
