@@ -1733,6 +1733,9 @@ __device__ __forceinline__ int wave_gc_label(const float* Ef, const float4* pts,
         keys[i] = k;
     }
     __syncthreads();
+#ifdef GTSFM_RANSAC_PROF
+    const unsigned long long gc_t0 = clock64();
+#endif
     for (int kk = 2; kk <= n2; kk <<= 1)
         for (int j = kk >> 1; j > 0; j >>= 1) {
             for (int i = lane; i < n2; i += 64) {
@@ -1747,6 +1750,9 @@ __device__ __forceinline__ int wave_gc_label(const float* Ef, const float4* pts,
             }
             __syncthreads();
         }
+#ifdef GTSFM_RANSAC_PROF
+    if (lane == 0) atomicAdd(&g_rprof[29], clock64() - gc_t0);
+#endif
     // every run head (first element of a cell) scans its run: prefix sums of the MSAC terms and 2 E(m) for all m
     int n_in = 0;
     const long long Q = 65536;
@@ -1849,6 +1855,7 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
         cur_sc = msac_d(bestE, cur);
     else
         cur = count_d(bestE);
+    RPROF(22);
     const bool gc = msac && M <= kGcMaxM;
     if (gc) {  // graph-cut LO (oracle_ransac_E: the MSAC path)
         int n2 = 1;
@@ -1862,6 +1869,8 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
             for (int e = 0; e < 9; ++e) Ef[e] = (float)bestE[e];
             const int n_lab = in_lds ? wave_gc_label(Ef, pts, M, thr2, scale, inv_cell, gc_keys_lds, gc_lab_lds, lane)
                                      : wave_gc_label(Ef, pts, M, thr2, scale, inv_cell, keys, lab, lane);
+            RPROF(23);
+            RPROF_COUNT(28, 1);
             if (n_lab < 8) break;
             double En[9];
             if (!wave_refit(x1, x2, M, nullptr, 0.0, lab, bestE, En, lane, jac_a, jac_v)) break;
@@ -1872,8 +1881,10 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
                 if (ok)
                     for (int e = 0; e < 9; ++e) En[e] = Et[e];
             }
+            RPROF(24);
             int c;
             const uint32_t sc = msac_d(En, c);
+            RPROF(25);
             if (sc >= cur_sc) break;
             cur_sc = sc;
             cur = c;
@@ -1924,6 +1935,7 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
         for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m);
         cur = c;
     }
+    RPROF(26);
     __syncthreads();  // mask visible to every lane of the workgroup
     // recoverPose: decomposition (redundant per lane) + wave cheirality vote
     double U[9], s[3], V[9];
@@ -1963,7 +1975,7 @@ __global__ __launch_bounds__(64, 2) void ransac_refine_kernel(const int* __restr
         if (out.n_hyp) out.n_hyp[p] = done;
         if (out.n_models) out.n_models[p] = ps.n_models;
     }
-    RPROF(15);
+    RPROF(27);
 }
 
 }  // namespace

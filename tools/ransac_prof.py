@@ -22,7 +22,8 @@ from gtsfm_amd.frontend.all_pairs import AllPairsFrontEnd, FrontEndConfig  # noq
 NAMES = {0: "s1 sample+load", 1: "s1 nullspace", 2: "s1 A rows", 3: "s1 Gauss-Jordan", 4: "s1 store",
          5: "s2 load", 6: "s2 B + det poly", 7: "s2 Sturm chain", 8: "s2 isolation", 9: "s2 bisection",
          10: "s2 Newton", 11: "s2 E from roots + store", 12: "s2 tail", 13: "score: candidates", 14: "score: chunk sync",
-         15: "refine"}
+         22: "refine: first MSAC", 23: "refine: GC labels (keys+sort+runs)", 24: "refine: refits", 25: "refine: MSAC of refit",
+         26: "refine: final mask", 27: "refine: recoverPose"}
 
 
 def main():
@@ -39,9 +40,10 @@ def main():
     fe.step(resident=True)
     fn(buf, 1)
     c = np.array(buf[:], dtype=np.float64)
-    tot = {"solve1": c[0:5].sum(), "solve2": c[5:13].sum(), "score": c[13:15].sum(), "refine": c[15]}
+    tot = {"solve1": c[0:5].sum(), "solve2": c[5:13].sum(), "score": c[13:15].sum(), "refine": c[22:28].sum()}
     print(f"waves: solve1 {int(c[16])}  solve2 {int(c[17])}  score workgroups {int(c[18])}")
     print(f"isolation iterations (lane 0 sum) {int(c[20])}, real roots (lane 0 sum) {int(c[21])}")
+    print(f"refine: GC iterations {int(c[28])}, of which bitonic sort cycles {c[29]:.4g} (inside 'GC labels')")
     allt = sum(tot.values())
     for k, name in NAMES.items():
         print(f"{name:26s} {c[k]:14.4g} cycles  {100 * c[k] / allt:5.1f} % of all wave-cycles")
