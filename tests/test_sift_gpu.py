@@ -228,3 +228,35 @@ def test_streaming_base_equals_tile_path(dev, oracle_mod, monkeypatch):
     assert nd == rnd
     np.testing.assert_array_equal(kp, rkp)
     np.testing.assert_array_equal(desc, rdesc)
+
+
+def test_blank_and_tiny_images(dev, oracle_mod):
+    """A uniform image has no DoG extremum: the drop-in returns the reference's empty result (zero keypoints with the
+    SIFT dtypes, a (0, 128) descriptor array), as the oracle does, alone and inside a batch beside textured images (the
+    batch's other rows are unchanged). The minimum accepted size (16 x 16) runs."""
+    from gtsfm_amd import device
+    from gtsfm_amd.common.image import Image
+    from gtsfm_amd.frontend.detector_descriptor.sift import SIFTDetectorDescriptor
+
+    blank = np.full((120, 160), 97, np.uint8)
+    kps, desc = SIFTDetectorDescriptor(max_keypoints=300).detect_and_describe(Image(np.stack([blank] * 3, axis=2)))
+    assert len(kps) == 0 and desc.shape == (0, 128)
+    assert kps.coordinates.dtype == np.float64
+    rkp, rdesc, rnd = oracle_mod.sift(blank, 300)
+    assert rnd == 0 and len(rkp) == 0
+    rng = np.random.default_rng(12)
+    tex = _texture(rng, 120, 160)
+    batch = device.sift_extract(torch.from_numpy(np.stack([tex, blank, tex])).cuda(), 300)
+    alone = device.sift_extract(torch.from_numpy(tex[None].copy()).cuda(), 300)
+    cnt = batch.count.cpu().numpy()
+    assert cnt[1] == 0 and cnt[0] == cnt[2] == int(alone.count[0]) > 0
+    n = int(cnt[0])
+    for j in (0, 2):
+        np.testing.assert_array_equal(batch.xy[j, :n].cpu().numpy(), alone.xy[0, :n].cpu().numpy())
+        np.testing.assert_array_equal(batch.desc[j, :n].cpu().numpy(), alone.desc[0, :n].cpu().numpy())
+    assert not batch.desc[1].any() and not batch.xy[1].any()  # padding rows zeroed
+    tiny = _texture(rng, 16, 16)
+    kp, d, nd = _gpu_sift(tiny, 50)
+    rkp, rdesc, rnd = oracle_mod.sift(tiny, 50)
+    assert nd == rnd
+    np.testing.assert_array_equal(kp, rkp)
