@@ -1658,9 +1658,6 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
                 g[2] = p[-W];
                 g[3] = p[W];
             };
-#ifdef GTSFM_ABL_DESC_NOATOM
-            unsigned abl_acc = 0;
-#endif
             float gn[4];
             int svn = 0;
             if (nit > 0) taps(lane * nit, gn, svn);
@@ -1705,13 +1702,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             // stay below 255 every fixed-point value is below 2^32 and is the single truncating conversion
             // (uint32_t)(v 2^24) -- the same integer as to_fix_nn, at a third of its instructions
             auto put = [&](int at, float v, bool small) {
-#if defined(GTSFM_ABL_DESC_U32)  // timing ablation only (wrong sums): 32-bit LDS atomics
-                atomicAdd((unsigned*)&hc[at], (uint32_t)v);
-#elif defined(GTSFM_ABL_DESC_NOATOM)  // timing ablation only (wrong sums): one register sum, no atomics
-                abl_acc += (uint32_t)v + (unsigned)at;
-#else
                 atomicAdd(&hc[at], small ? (unsigned long long)(uint32_t)v : to_fix_scaled(v));
-#endif
             };
             auto put8 = [&](bool small) {
                 put(idx, v_rco000, small);
@@ -1728,9 +1719,6 @@ __global__ __launch_bounds__(64) void descriptor_kernel(const KeyRec* __restrict
             else
                 put8(false);
             }
-#ifdef GTSFM_ABL_DESC_NOATOM
-            atomicAdd((unsigned*)&hc[lane], abl_acc);
-#endif
             __syncthreads();  // slist is rewritten by the next chunk
         }
         // finalisation: the element-wise steps run one element per lane, the two norms are sequential sums in the
