@@ -1,6 +1,9 @@
 """Per RANSAC kernel: registers, LDS and the waves per SIMD they allow (MI355X: 512 VGPR+AGPR per lane per SIMD in
 granules of 8, 160 KiB LDS per CU, 4 SIMDs per CU, at most 8 waves per SIMD), from a rocprofv3 kernel trace; plus the
-PMC summary's per-dispatch counters (tools/gpu_pmc_ransac.sh) and the mean resident waves per SIMD they imply.
+PMC summary's per-dispatch counters (tools/gpu_pmc_ransac.sh) and the mean resident waves per SIMD they imply:
+SQ_WAVE_CYCLES x 4 (the counter counts quad-cycles, MI355X_MICROARCH.md) / (mean launch us x clock x 1024 SIMDs).
+The trace's register and LDS columns can omit AGPRs and dynamic LDS; the code object's notes are authoritative
+(profiles/r06aq_ransac_occupancy/README.md takes them from there).
 
     python tools/ransac_occupancy.py <kernel_trace.csv> <pmc_ransac_summary.txt> > table.md
 """
@@ -10,6 +13,7 @@ import re
 import sys
 
 N_SIMD = 256 * 4
+CLOCK_MHZ = 2000  # profiled runs hold ~1.9-2.0 GHz (MI355X_MICROARCH.md)
 
 
 def main():
@@ -43,10 +47,10 @@ def main():
         w_lds = wg_lds * waves_per_wg / 4
         bound = min(w_regs, w_lds, 8)
         occ = "-"
+        mean_us = sum(dur[short]) / len(dur[short])
         for k, d in pmc.items():
-            if short.split("<")[0] in k and "SQ_WAVE_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
-                # SQ_WAVE_CYCLES: wave-cycles summed over the chip; GRBM_GUI_ACTIVE: busy cycles summed over 8 XCDs
-                occ = f"{float(d['SQ_WAVE_CYCLES']) / (float(d['GRBM_GUI_ACTIVE']) / 8) / N_SIMD:.2f}"
+            if short.split("<")[0] in k and "SQ_WAVE_CYCLES" in d:
+                occ = f"{float(d['SQ_WAVE_CYCLES']) * 4 / (mean_us * CLOCK_MHZ * N_SIMD):.2f}"
         print(f"| {short} | {v} | {a} | {lds} | {wg} | {w_regs} | {wg_lds if lds else '-'} | {bound:g} | "
               f"{sum(dur[short]) / len(dur[short]):.1f} | {occ} |")
 
